@@ -1,0 +1,216 @@
+"""bench.py — Mray/s (primary+shadow) of the MI355X voxel ray-trace path.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config C1] [--no-cpu]
+
+A step = one frame of the C1 workload (BASELINE.json configs[1]): 1920x1080, 1024^3 world
+(monu3.vox tiled), 1 spp, Trace depth 0 = primary ray + one light sample
+with its shadow ray(s), accumulate + tonemap + RGB8, all inside libvpx_hip.so's single
+render kernel.  Inputs (world, tables, accumulator) are resident in HBM before timing.
+
+N > 1 (torchrun, one rank per GPU): weak scaling — the frame grows with N (N x 1920x1080
+pixels), its 16x16 tiles are dealt round-robin to ranks, each rank renders its tiles into a
+packed buffer, an RCCL gather (torch.distributed, backend nccl) brings them to rank 0,
+which composites (unpack + accumulate + tonemap).  Timed region: barrier + sync on both
+sides, max over ranks.  value = all rays of all ranks / that time.
+
+roofline: algorithmic bytes of the render kernel per launch = DDA cells read x 1 B +
+W*H*36 B (accumulator float4 read+write + RGB8 write), SURVEY.md §8(d) / DESIGN.md §5,
+divided by the kernel's average duration measured with HIP events on its own stream.
+cpu_baseline: the CPU restatement (oracle/, C, -O2) on a bounded pixel sample of the same
+frame on this host's cores (rank 0, N = 1 only).
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+import __graft_entry__ as entry  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+METRIC = "Mray/s (primary+shadow) at 1920×1080, 1024³ world; 1/2/4/8-GPU"
+
+
+def weak_size(n):
+    """Frame of N x 1920x1080 pixels: 1 -> 1920x1080, 2 -> 3840x1080, 4 -> 3840x2160, 8 -> 7680x2160."""
+    a = 1 << math.ceil(math.log2(n) / 2) if n > 1 else 1
+    b = n // a
+    if a * b != n:
+        a, b = n, 1
+    return 1920 * a, 1080 * b
+
+
+def build_scene(pkg, cfg, width=None, height=None):
+    desc = pkg.scene.CONFIGS[cfg]()
+    if width and (width, height) != (desc.width, desc.height):
+        desc = desc.with_size(width, height)
+    return desc
+
+
+def cpu_baseline(pkg, desc, budget_s=12.0):
+    """Oracle timed on a bounded sample (whole rows, evenly spaced) of the same frame."""
+    orc = entry.load_oracle()
+    t0 = time.time()
+    o = orc.Oracle(pkg.abi, desc)
+    gen_s = time.time() - t0
+    threads = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
+    p = desc.frame_params(0)
+    W, H = desc.width, desc.height
+    # calibrate on 2 rows, then size the sample to ~budget_s
+    rows = np.array([H // 2, H // 3], np.int64)
+    ids = (rows[:, None] * W + np.arange(W)[None, :]).reshape(-1)
+    t = time.time()
+    _, st = o.render_pixels(p, ids, threads)
+    dt = max(time.time() - t, 1e-3)
+    per_row = dt / len(rows)
+    nrows = int(max(4, min(H, budget_s / per_row)))
+    rows = np.linspace(0, H - 1, nrows).astype(np.int64)
+    ids = (rows[:, None] * W + np.arange(W)[None, :]).reshape(-1)
+    t = time.time()
+    _, st = o.render_pixels(p, ids, threads)
+    dt = time.time() - t
+    rays = st.primary_rays + st.shadow_rays
+    return {"value": round(rays / dt / 1e6, 4), "unit": "Mray/s", "cores": threads, "kind": "port",
+            "sample": f"{nrows} evenly spaced rows of the {W}x{H} frame ({len(ids)} pixels, {rays} primary+shadow "
+                      f"rays, {dt:.1f} s); world generated on host in {gen_s:.1f} s"}
+
+
+def run(args):
+    pkg = entry.load_package()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    n = args.gpus
+    if world != n:
+        raise SystemExit(f"--gpus {n} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    dist = None
+    if n > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    W, H = weak_size(n)
+    desc = build_scene(pkg, args.config, W, H)
+    if n == 1 and args.config != "C1":
+        W, H = desc.width, desc.height
+    stream = torch.cuda.current_stream()
+    ctx = pkg.context.Context(local)
+    ctx.set_stream(stream.cuda_stream)
+    ctx.load_scene(desc)
+    torch.cuda.synchronize()
+    acc = torch.zeros(W * H * 4, dtype=torch.float32, device="cuda") if rank == 0 else None
+    rgb = torch.zeros(W * H, dtype=torch.int32, device="cuda") if rank == 0 else None
+    if n > 1:
+        L = ctx.packed_len(W, H, n)
+        packed = torch.zeros(L * 4, dtype=torch.float32, device="cuda")
+        gathered = [torch.empty_like(packed) for _ in range(n)] if rank == 0 else None
+        gbuf = torch.empty(n * L * 4, dtype=torch.float32, device="cuda") if rank == 0 else None
+
+    frame = [0]
+    ev = []
+
+    def step(record=False):
+        p = desc.frame_params(frame_index=frame[0])
+        e0 = e1 = None
+        if record:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+        if n == 1:
+            ctx.render(p, acc.data_ptr(), rgb.data_ptr())
+            if record:
+                e1.record(stream)
+        else:
+            ctx.render_tiles(p, rank, n, packed.data_ptr())
+            if record:
+                e1.record(stream)
+            dist.gather(packed, gathered, dst=0)
+            if rank == 0:
+                torch.cat(gathered, out=gbuf)
+                ctx.composite_tiles(p, n, gbuf.data_ptr(), acc.data_ptr(), rgb.data_ptr())
+        if record:
+            ev.append((e0, e1))
+        frame[0] += 1
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    ctx.counters(reset=True)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(record=True)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    ks = [a.elapsed_time(b) for a, b in ev]
+    st = ctx.counters()
+    local_rays = float(st.primary_rays + st.shadow_rays)
+    vals = torch.tensor([elapsed, local_rays, float(st.primary_rays), float(st.shadow_rays), float(st.dda_cells),
+                         float(np.mean(ks))], dtype=torch.float64, device="cuda")
+    if dist:
+        mx = vals.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        sm = vals.clone()
+        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+        elapsed = mx[0].item()
+        rays, prim, shad, cells = sm[1].item(), sm[2].item(), sm[3].item(), sm[4].item()
+        kernel_ms = mx[5].item()
+    else:
+        rays, prim, shad, cells = local_rays, float(st.primary_rays), float(st.shadow_rays), float(st.dda_cells)
+        kernel_ms = float(np.mean(ks))
+    if rank == 0:
+        K = args.steps
+        ms_step = elapsed * 1000.0 / K
+        value = rays / elapsed / 1e6
+        # roofline of the dominant kernel (render), per launch on one GPU
+        cells_per_launch = float(st.dda_cells) / K
+        pix_per_launch = float(st.primary_rays) / K
+        alg_bytes = cells_per_launch * 1.0 + pix_per_launch * 36.0
+        achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
+        out = {
+            "metric": METRIC, "value": round(value, 3), "unit": "Mray/s", "n_gpus": n, "steps": K,
+            "warmup": args.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic world: monu3.vox (decoded by the reference's ogt_vox) tiled into a "
+                    f"{desc.grids[0].n}^3 u8 grid on device; fixed lights/camera (SURVEY.md §8(d))",
+            "config": {"workload": f"{args.config}: {W}x{H}, {desc.grids[0].n}^3 {desc.name}, 1 spp, "
+                                   f"Trace depth {desc.max_bounces} (primary+shadow)",
+                       "width": W, "height": H, "world_n": desc.grids[0].n, "max_bounces": desc.max_bounces,
+                       "spp": 1, "parallelism": "single GPU" if n == 1 else f"tile-shard x{n} + RCCL gather to rank 0"},
+            "rays_per_step": {"primary": prim / K, "shadow": shad / K, "dda_cells": cells / K},
+            "mpix_per_s": round(prim / elapsed / 1e6, 3),
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                         "kernel": "render_tiles", "kernel_ms": round(kernel_ms, 4),
+                         "alg_bytes_per_launch": round(alg_bytes)},
+            "cpu_baseline": None,
+        }
+        if n == 1 and not args.no_cpu:
+            out["cpu_baseline"] = cpu_baseline(pkg, desc, args.cpu_budget)
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="C1")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    run(ap.parse_args())
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,270 @@
+/*
+ * vpx.h — C-ABI of the MI355X (gfx950) voxel ray-trace library `libvpx_hip.so`.
+ *
+ * This is the drop-in boundary behind `Renderer::Tick(deltaTime)` of
+ * Tycro-Games/Raytracer-VoxPopuli.  The host keeps its tmpl8 template, window,
+ * UI and game logic; inside `Renderer::Update()` it calls `vpx_render` instead
+ * of the per-pixel `Trace` loop (reference renderer.cpp:1646-1891), and the
+ * library owns persistent device copies of the voxel grids, the volume
+ * transforms and the material / light tables.
+ *
+ * Every function returns VPX_OK (0) or a negative VPX_E_* status; nothing
+ * throws across the ABI and nothing aborts.  `vpx_last_error(ctx)` returns a
+ * human-readable message for the last failure on that context.
+ *
+ * All structs are plain-old-data with fixed layout (asserted in vpx_api.cpp);
+ * matrices are tmpl8 `mat4::cell` order (row-major, translation in cells 3/7/11).
+ *
+ * Reference interfaces replaced (file:line in the reference tree):
+ *   vpx_render            Renderer::Update            renderer.cpp:1646-1891
+ *                         (+ Renderer::Trace           renderer.cpp:1076-1328)
+ *   vpx_find_nearest      Renderer::FindNearest       renderer.cpp:946-1018
+ *                         Scene::FindNearest          template/scene.cpp:751-811
+ *   vpx_is_occluded       Renderer::IsOccluded        renderer.cpp:209-243
+ *                         Scene::IsOccluded           template/scene.cpp:1009-1047
+ *   vpx_trace             Renderer::Trace(Ray&, int)  renderer.cpp:1076
+ *   vpx_focus_distance    focus ray in Renderer::Tick renderer.cpp:1987-1991
+ *   vpx_upload_grid       Scene::grid (owned by host) template/scene.h:258
+ *   vpx_set_volumes       Renderer::voxelVolumes      renderer.h:211
+ *   vpx_set_materials     Renderer::materials         renderer.h:190, MaterialSetUp renderer.cpp:357-443
+ *   vpx_set_lights        point/spot/area/dirLight    renderer.h:193-197
+ *   vpx_set_shapes        Renderer::spheres/triangles renderer.h:207-208
+ *   vpx_set_camera        Renderer::camera            renderer.h:181, template/camera.h:14-192
+ * Host-side helpers that restate reference host code (no GPU needed):
+ *   vpx_camera_look_at       Camera::HandleInput basis   template/camera.h:113-181
+ *   vpx_volume_set_transform Scene::SetTransform         template/scene.cpp:373-405
+ *   vpx_default_materials    Renderer::MaterialSetUp     renderer.cpp:357-443
+ */
+#ifndef VPX_H_
+#define VPX_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VPX_ABI_VERSION 1
+
+/* ---- status codes ---------------------------------------------------------------- */
+#define VPX_OK 0
+#define VPX_E_INVALID (-1)   /* bad argument (null pointer, size, id)           */
+#define VPX_E_DEVICE (-2)    /* HIP runtime error                              */
+#define VPX_E_NOMEM (-3)     /* device allocation failed                       */
+#define VPX_E_STATE (-4)     /* call order (e.g. render before any volume)     */
+
+/* ---- material indices (MaterialType::MatType, template/scene.h:36-58) ------------- */
+#define VPX_MAT_NON_METAL_WHITE 0
+#define VPX_MAT_NON_METAL_PINK 4
+#define VPX_MAT_METAL_HIGH 5
+#define VPX_MAT_METAL_LOW 7
+#define VPX_MAT_GLASS 8
+#define VPX_MAT_SMOKE_LOW_DENSITY 9
+#define VPX_MAT_SMOKE_PLAYER 14
+#define VPX_MAT_EMISSIVE 15
+#define VPX_MAT_NONE 255
+#define VPX_NUM_MATERIALS 256
+
+/* ---- frame flags -------------------------------------------------------------------- */
+#define VPX_FLAG_AA 0x1u        /* sub-pixel jitter x+RandomFloat()*aa (renderer.cpp:1682-1708)   */
+#define VPX_FLAG_DOF 0x2u       /* thin-lens jitter (template/camera.h:68-83)                    */
+#define VPX_FLAG_NO_TONEMAP 0x4u /* skip accumulate/tonemap: write raw radiance to accum (tests) */
+
+/* ---- POD scene description -------------------------------------------------------- */
+
+/* One voxel volume (a `Scene` in the reference, template/scene.h:173-266). */
+typedef struct vpx_volume {
+    uint32_t grid_id;       /* grid uploaded with vpx_upload_grid; volumes may share a grid */
+    uint32_t reserved;
+    float matrix[16];       /* Scene::matrix    (object -> world)                */
+    float inv_matrix[16];   /* Scene::invMatrix (world -> object) — used as-is    */
+    float b0[3];            /* Scene::cube.b[0]                                  */
+    float b1[3];            /* Scene::cube.b[1]                                  */
+} vpx_volume;               /* 160 bytes */
+
+/* Material (src/Materials/Material.h:3-12), indexed by voxel value. */
+typedef struct vpx_material {
+    float albedo[3];
+    float roughness;
+    float emissive;         /* emissiveStrength */
+    float ior;              /* IOR */
+    float pad[2];
+} vpx_material;             /* 32 bytes */
+
+typedef struct vpx_point_light {  /* PointLightData, src/Lighting/PointLight.h:3-7 */
+    float position[3];
+    float color[3];
+} vpx_point_light;
+
+typedef struct vpx_spot_light {   /* SpotLightData, src/Lighting/SpotLight.h:12-18 */
+    float position[3];
+    float direction[3];
+    float color[3];
+    float angle;                  /* cosine of the cone half-angle */
+} vpx_spot_light;
+
+typedef struct vpx_area_light {   /* SphereAreaLightData, src/Lighting/SphereAreaLight.h:2-9 */
+    float position[3];
+    float color[3];
+    float color_multiplier;
+    float radius;
+} vpx_area_light;
+
+typedef struct vpx_dir_light {    /* DirectionalLightData, src/Lighting/DirectionalLight.h:2-6 */
+    float direction[3];
+    float color[3];
+} vpx_dir_light;
+
+typedef struct vpx_sphere {       /* Sphere, src/BVH/Shapes.h:4-68 */
+    float center[3];
+    float radius;
+    uint32_t material;
+    uint32_t pad[3];
+} vpx_sphere;
+
+typedef struct vpx_triangle {     /* Triangle, src/BVH/Shapes.h:71-150 */
+    float position[3];
+    float v0[3], v1[3], v2[3];
+    uint32_t material;
+    uint32_t pad[3];
+} vpx_triangle;
+
+/* Camera state used by primary-ray generation (template/camera.h:68-110, 183-191). */
+typedef struct vpx_camera {
+    float cam_pos[3];
+    float top_left[3];
+    float top_right[3];
+    float bottom_left[3];
+    float right[3];
+    float up[3];
+    float focal_distance;
+    float defocus_jitter;
+} vpx_camera;
+
+/* Per-frame parameters (the knobs of Renderer::Update / Trace). */
+typedef struct vpx_frame_params {
+    uint32_t width, height;       /* SCRWIDTH/SCRHEIGHT (compile-time in the reference)     */
+    int32_t max_bounces;          /* depth handed to Trace (Renderer::maxBounces)           */
+    uint32_t frame_index;         /* numRenderedFrames: weight 1/(n+1) and seed stream      */
+    uint32_t seed_base;           /* added to the pixel key of the per-pixel seed           */
+    uint32_t flags;               /* VPX_FLAG_*                                             */
+    float aa_strength;            /* antiAliasingStrength                                   */
+    int32_t area_samples;         /* numCheckShadowsAreaLight                               */
+    float sky[3];                 /* SampleSky colour when activateSky == false             */
+    uint32_t reserved;
+} vpx_frame_params;
+
+/* Ray for the unit entries (a `Ray` built with Ray(origin, direction), scene.cpp:83-93). */
+typedef struct vpx_ray {
+    float origin[3];
+    float direction[3];           /* normalised by the library exactly like the Ray ctor   */
+    float tmax;                   /* Ray::t on entry (1e34 = unbounded)                     */
+    uint32_t inside_glass;        /* Ray::isInsideGlass                                     */
+} vpx_ray;
+
+typedef struct vpx_hit {
+    float t;                      /* Ray::t after the call                                  */
+    float normal[3];              /* Ray::rayNormal                                         */
+    int32_t vox_index;            /* Renderer::FindNearest return: -2 none, -1 analytic, i  */
+    uint32_t material;            /* Ray::indexMaterial (255 = NONE)                        */
+    uint32_t cells;               /* DDA cells read for this ray                            */
+    uint32_t inside_glass;        /* Ray::isInsideGlass after the call                      */
+} vpx_hit;
+
+/* Work counters of one render call (always on; per-wave reduced on device). */
+typedef struct vpx_stats {
+    uint64_t primary_rays;        /* W*H                                                     */
+    uint64_t shadow_rays;         /* IsOccluded calls actually made                          */
+    uint64_t bounce_rays;         /* FindNearest calls beyond the primary                    */
+    uint64_t dda_cells;           /* grid cells read by every DDA (nearest + shadow + exits) */
+    float kernel_ms;              /* device time of the trace kernel (HIP events)            */
+    float total_ms;               /* device time of the whole call                           */
+} vpx_stats;
+
+typedef struct vpx_ctx vpx_ctx;
+
+/* ---- lifetime ------------------------------------------------------------------------ */
+int vpx_create(int device, vpx_ctx** out);
+int vpx_destroy(vpx_ctx* ctx);
+const char* vpx_last_error(const vpx_ctx* ctx);
+int vpx_abi_version(void);
+/* Use an external HIP stream (hipStream_t as void*); NULL = the context's own stream. */
+int vpx_set_stream(vpx_ctx* ctx, void* hip_stream);
+int vpx_synchronize(vpx_ctx* ctx);
+
+/* ---- world ----------------------------------------------------------------------------- */
+/* Upload a dense N^3 grid of MatType bytes, index x + y*N + z*N*N (scene.h:241-248). */
+int vpx_upload_grid(vpx_ctx* ctx, uint32_t grid_id, const uint8_t* cells, uint32_t n);
+/* Build-defined world generator on device: a grid-oriented model
+   (mx*my*mz bytes, index x + y*mx + z*mx*my) tiled with period (px,py,pz) above a
+   NON_METAL_WHITE ground slab of `ground` cells.  Same result as oracle_tiled_world. */
+int vpx_generate_tiled_grid(vpx_ctx* ctx, uint32_t grid_id, uint32_t n, const uint8_t* model,
+                            uint32_t mx, uint32_t my, uint32_t mz,
+                            uint32_t px, uint32_t py, uint32_t pz, uint32_t ground);
+/* FNV-1a-style 64-bit checksum of a device grid (for size-independent parity checks). */
+int vpx_grid_checksum(vpx_ctx* ctx, uint32_t grid_id, uint64_t* out);
+int vpx_set_volumes(vpx_ctx* ctx, const vpx_volume* volumes, uint32_t count);
+int vpx_set_materials(vpx_ctx* ctx, const vpx_material* materials, uint32_t count);
+int vpx_set_lights(vpx_ctx* ctx,
+                   const vpx_point_light* points, uint32_t n_points,
+                   const vpx_spot_light* spots, uint32_t n_spots,
+                   const vpx_area_light* areas, uint32_t n_areas,
+                   const vpx_dir_light* dir);
+int vpx_set_shapes(vpx_ctx* ctx, const vpx_sphere* spheres, uint32_t n_spheres,
+                   const vpx_triangle* triangles, uint32_t n_triangles);
+int vpx_set_camera(vpx_ctx* ctx, const vpx_camera* camera);
+
+/* ---- the hot path -------------------------------------------------------------------- */
+/* One frame: primary rays, Trace(ray, max_bounces) per pixel, running-average accumulate
+   (w = 1/(frame_index+1)), Reinhard-Jodie tonemap, RGB8 pack.  `accum` (float4[W*H]) and
+   `rgb8` (uint32[W*H]) are DEVICE pointers; accum is read-modify-write. Either may be NULL
+   when VPX_FLAG_NO_TONEMAP is not set for rgb8.  `stats` (host) may be NULL.            */
+int vpx_render(vpx_ctx* ctx, const vpx_frame_params* params, float* accum, uint32_t* rgb8,
+               vpx_stats* stats);
+/* Tile-sharded variant for multi-GPU: render the tiles t (tile_w x tile_h, row-major tile
+   order) with t % n_ranks == rank into a packed float4 buffer (tile after tile, row-major
+   inside a tile; partial edge tiles padded with zeros).  DEVICE pointer.                */
+int vpx_render_tiles(vpx_ctx* ctx, const vpx_frame_params* params, uint32_t tile_w,
+                     uint32_t tile_h, uint32_t rank, uint32_t n_ranks, float* packed,
+                     vpx_stats* stats);
+/* Number of float4 elements one rank's packed buffer holds (all ranks use the max). */
+uint64_t vpx_tiles_packed_len(uint32_t width, uint32_t height, uint32_t tile_w,
+                              uint32_t tile_h, uint32_t n_ranks);
+/* Rank-0 composite: `gathered` = n_ranks packed buffers back to back (DEVICE); unpack,
+   accumulate into accum and tonemap into rgb8 exactly like vpx_render's epilogue.      */
+int vpx_composite_tiles(vpx_ctx* ctx, const vpx_frame_params* params, uint32_t tile_w,
+                        uint32_t tile_h, uint32_t n_ranks, const float* gathered,
+                        float* accum, uint32_t* rgb8);
+
+/* Work counters accumulated on device over every render call since the last reset
+   (no per-frame synchronisation); kernel_ms/total_ms are not filled here.            */
+int vpx_get_counters(vpx_ctx* ctx, vpx_stats* out, int reset);
+
+/* ---- unit entries (host pointers; mirror the reference per-ray functions) ---------- */
+int vpx_find_nearest(vpx_ctx* ctx, const vpx_ray* rays, uint32_t n, vpx_hit* hits);
+int vpx_is_occluded(vpx_ctx* ctx, const vpx_ray* rays, uint32_t n, uint8_t* occluded);
+/* Trace(ray, depth) with an explicit xorshift32 state per ray; radiance = float3[n]. */
+int vpx_trace(vpx_ctx* ctx, const vpx_ray* rays, const uint32_t* seeds, uint32_t n,
+              int32_t depth, const float sky[3], int32_t area_samples, float* radiance);
+/* Focus ray of Renderer::Tick (world-space ray against every Scene::FindNearest). */
+int vpx_focus_distance(vpx_ctx* ctx, uint32_t width, uint32_t height, float* focal_distance);
+
+/* ---- host-side helpers restating reference host code (no device work) -------------- */
+/* Camera basis exactly as Camera::HandleInput(0) leaves it (camera.h:121-178). */
+int vpx_camera_look_at(const float pos[3], const float target[3], uint32_t width,
+                       uint32_t height, vpx_camera* out);
+/* Scene::SetCubeBoundaries + Scene::SetTransform (scene.cpp:213-217, 373-405). */
+int vpx_volume_set_transform(const float position[3], const float scale[3],
+                             const float rotation[3], vpx_volume* out);
+/* Renderer::MaterialSetUp table, padded to 256 entries (renderer.cpp:357-443). */
+int vpx_default_materials(vpx_material* out256);
+/* Per-pixel xorshift32 state used by vpx_render: 0x12345678 + WangHash((k+1)*17),
+   k = seed_base + frame_index*W*H + y*W + x  (InitSeed, template/tmpl8math.cpp:35-38). */
+uint32_t vpx_pixel_seed(uint32_t seed_base, uint32_t frame_index, uint32_t width,
+                        uint32_t height, uint32_t x, uint32_t y);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VPX_H_ */

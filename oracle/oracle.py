@@ -1,0 +1,168 @@
+"""ctypes binding of oracle/liboracle.so — TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this
+module; it is the checker, never the thing measured or shipped.  Parity status of the
+trace path: UNPINNED (see vpx_oracle.h and DESIGN.md §3).
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liboracle.so")
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE, "liboracle.so"], check=True)
+
+
+def _lib(abi):
+    if not os.path.exists(LIB_PATH):
+        build()
+    lib = C.CDLL(LIB_PATH)
+    P = C.POINTER
+    lib.oracle_find_nearest.argtypes = [C.c_void_p, P(abi.Ray), C.c_uint32, P(abi.Hit)]
+    lib.oracle_is_occluded.argtypes = [C.c_void_p, P(abi.Ray), C.c_uint32, C.c_void_p, C.c_void_p]
+    lib.oracle_trace.argtypes = [C.c_void_p, P(abi.Ray), C.c_void_p, C.c_uint32, C.c_int32, P(C.c_float), C.c_int32,
+                                 C.c_void_p, P(abi.Stats)]
+    lib.oracle_render_pixels.argtypes = [C.c_void_p, P(abi.FrameParams), C.c_void_p, C.c_uint32, C.c_void_p,
+                                         P(abi.Stats), C.c_int]
+    lib.oracle_render.argtypes = [C.c_void_p, P(abi.FrameParams), C.c_void_p, C.c_void_p, P(abi.Stats), C.c_int]
+    lib.oracle_accumulate_tonemap.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p]
+    lib.oracle_accumulate_tonemap.restype = None
+    lib.oracle_focus_distance.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32]
+    lib.oracle_focus_distance.restype = C.c_float
+    lib.oracle_load_model.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, P(C.c_float),
+                                      C.c_void_p]
+    lib.oracle_load_model.restype = None
+    lib.oracle_orient_model.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p]
+    lib.oracle_orient_model.restype = None
+    lib.oracle_tiled_world.argtypes = [C.c_void_p] + [C.c_uint32] * 8 + [C.c_void_p]
+    lib.oracle_tiled_world.restype = None
+    lib.oracle_grid_checksum.argtypes = [C.c_void_p, C.c_uint64]
+    lib.oracle_grid_checksum.restype = C.c_uint64
+    lib.oracle_wang_hash.argtypes = [C.c_uint32]
+    lib.oracle_wang_hash.restype = C.c_uint32
+    lib.oracle_xorshift32.argtypes = [P(C.c_uint32)]
+    lib.oracle_xorshift32.restype = C.c_uint32
+    lib.oracle_random_float.argtypes = [P(C.c_uint32)]
+    lib.oracle_random_float.restype = C.c_float
+    lib.oracle_pixel_seed.argtypes = [C.c_uint32] * 6
+    lib.oracle_pixel_seed.restype = C.c_uint32
+    lib.oracle_offset_ray.argtypes = [P(C.c_float), P(C.c_float), P(C.c_float)]
+    lib.oracle_offset_ray.restype = None
+    lib.oracle_cube_intersect.argtypes = [P(C.c_float)] * 5
+    lib.oracle_cube_intersect.restype = C.c_float
+    return lib
+
+
+class OracleGrid(C.Structure):
+    _fields_ = [("cells", C.c_void_p), ("n", C.c_uint32)]
+
+
+def _scene_struct(abi):
+    class OracleScene(C.Structure):
+        _fields_ = [("grids", C.POINTER(OracleGrid)), ("num_grids", C.c_uint32),
+                    ("volumes", C.POINTER(abi.Volume)), ("num_volumes", C.c_uint32),
+                    ("materials", C.POINTER(abi.Material)),
+                    ("points", C.POINTER(abi.PointLight)), ("num_points", C.c_uint32),
+                    ("spots", C.POINTER(abi.SpotLight)), ("num_spots", C.c_uint32),
+                    ("areas", C.POINTER(abi.AreaLight)), ("num_areas", C.c_uint32),
+                    ("dir", abi.DirLight),
+                    ("spheres", C.POINTER(abi.Sphere)), ("num_spheres", C.c_uint32),
+                    ("triangles", C.POINTER(abi.Triangle)), ("num_triangles", C.c_uint32),
+                    ("camera", abi.Camera)]
+    return OracleScene
+
+
+class Oracle:
+    """CPU restatement bound to one SceneDesc (grids materialised on the host)."""
+
+    def __init__(self, abi, desc, grid_cells=None):
+        self.abi = abi
+        self.lib = _lib(abi)
+        self.desc = desc
+        self._keep = []
+        cells = grid_cells if grid_cells is not None else [self.host_grid(g) for g in desc.grids]
+        self.cells = [np.ascontiguousarray(c, np.uint8) for c in cells]
+        grids = (OracleGrid * len(self.cells))(*[OracleGrid(c.ctypes.data, g.n) for c, g in zip(self.cells, desc.grids)])
+        S = _scene_struct(abi)
+        s = S()
+        s.grids, s.num_grids = grids, len(self.cells)
+        s.volumes, s.num_volumes = desc.volumes, len(desc.volumes)
+        s.materials = desc.materials
+        arr = lambda T, xs: (T * max(1, len(xs)))(*xs)
+        pts, sps, ars = arr(abi.PointLight, desc.points), arr(abi.SpotLight, desc.spots), arr(abi.AreaLight, desc.areas)
+        s.points, s.num_points = pts, len(desc.points)
+        s.spots, s.num_spots = sps, len(desc.spots)
+        s.areas, s.num_areas = ars, len(desc.areas)
+        s.dir = desc.dir_light
+        sph, tri = arr(abi.Sphere, desc.spheres), arr(abi.Triangle, desc.triangles)
+        s.spheres, s.num_spheres = sph, len(desc.spheres)
+        s.triangles, s.num_triangles = tri, len(desc.triangles)
+        s.camera = desc.camera
+        self._keep += [grids, pts, sps, ars, sph, tri]
+        self.s = s
+
+    def host_grid(self, spec):
+        """Materialise a GridSpec on the host with the oracle's own generator."""
+        if spec.dense is not None:
+            return spec.dense
+        n = spec.n
+        out = np.empty(n * n * n, np.uint8)
+        m = np.ascontiguousarray(spec.model, np.uint8)
+        mx, my, mz = spec.model_dims
+        px, py, pz = spec.period
+        self.lib.oracle_tiled_world(m.ctypes.data, mx, my, mz, px, py, pz, spec.ground, n, out.ctypes.data)
+        return out
+
+    def set_camera(self, cam):
+        self.s.camera = cam
+
+    @property
+    def ptr(self):
+        return C.byref(self.s)
+
+    def find_nearest(self, rays):
+        n = len(rays)
+        hits = (self.abi.Hit * max(1, n))()
+        assert self.lib.oracle_find_nearest(self.ptr, rays, n, hits) == 0
+        return hits
+
+    def is_occluded(self, rays):
+        n = len(rays)
+        occ = np.zeros(max(1, n), np.uint8)
+        cells = np.zeros(max(1, n), np.uint32)
+        assert self.lib.oracle_is_occluded(self.ptr, rays, n, occ.ctypes.data, cells.ctypes.data) == 0
+        return occ[:n], cells[:n]
+
+    def trace(self, rays, seeds, depth, sky, area_samples=3):
+        n = len(rays)
+        seeds = np.ascontiguousarray(seeds, np.uint32)
+        out = np.zeros((max(1, n), 3), np.float32)
+        st = self.abi.Stats()
+        assert self.lib.oracle_trace(self.ptr, rays, seeds.ctypes.data, n, depth, self.abi.vec3(sky), area_samples,
+                                     out.ctypes.data, C.byref(st)) == 0
+        return out[:n], st
+
+    def render_pixels(self, params, pixel_ids, threads=0):
+        ids = np.ascontiguousarray(pixel_ids, np.uint32)
+        out = np.zeros((max(1, len(ids)), 4), np.float32)
+        st = self.abi.Stats()
+        assert self.lib.oracle_render_pixels(self.ptr, C.byref(params), ids.ctypes.data, len(ids), out.ctypes.data,
+                                             C.byref(st), threads) == 0
+        return out[: len(ids)], st
+
+    def render(self, params, accum=None, threads=0):
+        w, h = params.width, params.height
+        acc = np.zeros((h * w, 4), np.float32) if accum is None else accum
+        rgb = np.zeros(h * w, np.uint32)
+        st = self.abi.Stats()
+        assert self.lib.oracle_render(self.ptr, C.byref(params), acc.ctypes.data, rgb.ctypes.data, C.byref(st),
+                                      threads) == 0
+        return acc, rgb, st
+
+    def focus_distance(self, width, height):
+        return self.lib.oracle_focus_distance(self.ptr, width, height)

@@ -1,0 +1,1190 @@
+/*
+ * vpx_oracle.c — CPU restatement of the reference per-pixel voxel ray-trace path.
+ *
+ * TEST INFRASTRUCTURE ONLY (the checker, never the product).  See vpx_oracle.h for
+ * the parity status ("parity unpinned" for the trace path; the .vox decode is pinned).
+ *
+ * Every function names the reference file:line it restates.  Expressions keep the
+ * reference's operand order; the file is compiled with -ffp-contract=off -fno-fast-math
+ * and runs with FTZ|DAZ set (template/template.cpp:130).  Decisions on the reference's
+ * platform-dependent operations:
+ *   - FastReciprocal (rcpps + Newton, renderer.cpp:929-934) and _mm_rsqrt_ps
+ *     (tmpl8math.h:2356-2360) -> exact 1/x and 1/sqrtf(x);
+ *   - unspecified argument evaluation order (make_float3(RandomFloat(), ...)) -> left
+ *     to right;
+ *   - sinf/cosf/powf/expf/SVML -> correctly rounded float results, computed as
+ *     (float)f((double)x);
+ *   - GetVoxel's 32-bit index arithmetic (scene.h:246) -> 64-bit (wraps at N >= 2048).
+ */
+#include "vpx_oracle.h"
+
+#include <limits.h>
+#include <math.h>
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+#include <unistd.h>
+#if defined(__x86_64__) || defined(__i386__)
+#include <xmmintrin.h>
+#define ORACLE_X86 1
+#endif
+
+#define NONE_MAT 255u
+#define PI_F 3.14159265358979323846264f /* common.h:8 */
+#define BIG_T 1e34f
+
+/* ------------------------------------------------------------------ vector math -- */
+/* float3 operators of template/tmpl8math.h (operator+ :913, operator- :1361, ...). */
+typedef struct { float x, y, z; } v3;
+
+static inline v3 V3(float x, float y, float z) { v3 r = {x, y, z}; return r; }
+static inline v3 v3f(const float* p) { return V3(p[0], p[1], p[2]); }
+static inline v3 vadd(v3 a, v3 b) { return V3(a.x + b.x, a.y + b.y, a.z + b.z); }
+static inline v3 vsub(v3 a, v3 b) { return V3(a.x - b.x, a.y - b.y, a.z - b.z); }
+static inline v3 vmul(v3 a, v3 b) { return V3(a.x * b.x, a.y * b.y, a.z * b.z); }
+static inline v3 vdiv(v3 a, v3 b) { return V3(a.x / b.x, a.y / b.y, a.z / b.z); }
+static inline v3 vmuls(v3 a, float s) { return V3(a.x * s, a.y * s, a.z * s); }
+static inline v3 vdivs(v3 a, float s) { return V3(a.x / s, a.y / s, a.z / s); }
+static inline v3 vneg(v3 a) { return V3(-a.x, -a.y, -a.z); }
+static inline float vdot(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; } /* :2259 */
+static inline float vlength(v3 a) { return sqrtf(vdot(a, a)); }                   /* :2319 */
+static inline v3 vnormalize(v3 v) /* tmpl8math.h:2350-2354, rsqrtf = 1/sqrtf (:411) */
+{
+    const float inv = 1.0f / sqrtf(vdot(v, v));
+    return vmuls(v, inv);
+}
+static inline v3 vcross(v3 a, v3 b) /* tmpl8math.h:2494 */
+{
+    return V3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+/* std::min / std::max as libstdc++/MSVC define them (NaN and signed-zero exact). */
+static inline float smin(float a, float b) { return (b < a) ? b : a; }
+static inline float smax(float a, float b) { return (a < b) ? b : a; }
+
+static inline uint32_t f2u_bits(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }
+static inline float u2f_bits(uint32_t u) { float f; memcpy(&f, &u, 4); return f; }
+
+/* static_cast<int>(float) as x86 cvttss2si evaluates it (out of range / NaN -> INT_MIN). */
+static inline int f2i_trunc(float f)
+{
+    if (!(f > -2147483904.0f && f < 2147483648.0f)) return INT_MIN;
+    return (int)f;
+}
+
+/* Correctly rounded float transcendentals (see header comment). */
+static inline float cr_sinf(float x) { return (float)sin((double)x); }
+static inline float cr_cosf(float x) { return (float)cos((double)x); }
+static inline float cr_expf(float x) { return (float)exp((double)x); }
+static inline float cr_powf(float x, float y) { return (float)pow((double)x, (double)y); }
+
+/* ----------------------------------------------------------------------- RNG -- */
+/* WangHash, template/tmpl8math.cpp:20-27 */
+uint32_t oracle_wang_hash(uint32_t s)
+{
+    s = (s ^ 61u) ^ (s >> 16);
+    s *= 9u, s = s ^ (s >> 4);
+    s *= 0x27d4eb2du;
+    s = s ^ (s >> 15);
+    return s;
+}
+
+/* RandomUInt, template/tmpl8math.cpp:119-125 (Marsaglia xorshift32, 13/17/5) */
+uint32_t oracle_xorshift32(uint32_t* seed)
+{
+    uint32_t s = *seed;
+    s ^= s << 13;
+    s ^= s >> 17;
+    s ^= s << 5;
+    *seed = s;
+    return s;
+}
+
+/* RandomFloat, template/tmpl8math.cpp:130-133 */
+float oracle_random_float(uint32_t* seed)
+{
+    return (float)oracle_xorshift32(seed) * 2.3283064365387e-10f;
+}
+
+/* InitSeed on a fresh thread-local seed (tmpl8math.cpp:16, 35-38) keyed by pixel. */
+uint32_t oracle_pixel_seed(uint32_t seed_base, uint32_t frame_index, uint32_t width,
+                           uint32_t height, uint32_t x, uint32_t y)
+{
+    const uint32_t k = seed_base + frame_index * (width * height) + y * width + x;
+    return 0x12345678u + oracle_wang_hash((k + 1u) * 17u);
+}
+
+/* ---------------------------------------------------------------------- Ray -- */
+/* Ray, template/scene.h:64-155 */
+typedef struct {
+    v3 O, D, rD, Dsign, N;
+    float t;
+    int inside;   /* isInsideGlass */
+    uint32_t mat; /* indexMaterial */
+} ray_t;
+
+/* Ray::ComputeDsign, template/scene.cpp:49-57 (== ComputeDsign_SSE :59-80) */
+static inline v3 compute_dsign(v3 d)
+{
+    const float sx = (float)(f2u_bits(d.x) >> 31), sy = (float)(f2u_bits(d.y) >> 31),
+                sz = (float)(f2u_bits(d.z) >> 31);
+    return vmuls(vadd(V3(sx * 2 - 1, sy * 2 - 1, sz * 2 - 1), V3(1, 1, 1)), 0.5f);
+}
+
+/* Ray::Ray(origin, direction, rayLength = 1e34), template/scene.cpp:83-93 */
+static ray_t make_ray(v3 o, v3 dir)
+{
+    ray_t r;
+    r.O = o;
+    r.t = BIG_T;
+    r.D = vnormalize(dir);
+    r.rD = V3(1 / r.D.x, 1 / r.D.y, 1 / r.D.z);
+    r.Dsign = compute_dsign(r.D);
+    r.N = V3(0, 0, 0);
+    r.inside = 0;
+    r.mat = NONE_MAT;
+    return r;
+}
+
+static inline v3 ray_point(const ray_t* r) { return vadd(r->O, vmuls(r->D, r->t)); } /* scene.h:80-83 */
+
+/* ----------------------------------------------------------------- transforms -- */
+/* TransformPosition_SSEM, template/tmpl8math.cpp:369-380: pairwise (a0m0+a1m1)+(a2m2+m3) */
+static inline v3 xform_pos_ssem(v3 a, const float* m)
+{
+    return V3((a.x * m[0] + a.y * m[1]) + (a.z * m[2] + m[3]),
+              (a.x * m[4] + a.y * m[5]) + (a.z * m[6] + m[7]),
+              (a.x * m[8] + a.y * m[9]) + (a.z * m[10] + m[11]));
+}
+/* TransformVector_SSEM, template/tmpl8math.cpp:393-402 */
+static inline v3 xform_vec_ssem(v3 a, const float* m)
+{
+    return V3((a.x * m[0] + a.y * m[1]) + a.z * m[2], (a.x * m[4] + a.y * m[5]) + a.z * m[6],
+              (a.x * m[8] + a.y * m[9]) + a.z * m[10]);
+}
+/* TransformPosition, template/tmpl8math.cpp:345-348 with operator*(float4, mat4) :337-343 */
+static inline v3 xform_pos(v3 a, const float* m)
+{
+    return V3(m[0] * a.x + m[1] * a.y + m[2] * a.z + m[3] * 1.0f,
+              m[4] * a.x + m[5] * a.y + m[6] * a.z + m[7] * 1.0f,
+              m[8] * a.x + m[9] * a.y + m[10] * a.z + m[11] * 1.0f);
+}
+/* TransformVector, template/tmpl8math.cpp:350-353 */
+static inline v3 xform_vec(v3 a, const float* m)
+{
+    return V3(m[0] * a.x + m[1] * a.y + m[2] * a.z + m[3] * 0.0f,
+              m[4] * a.x + m[5] * a.y + m[6] * a.z + m[7] * 0.0f,
+              m[8] * a.x + m[9] * a.y + m[10] * a.z + m[11] * 0.0f);
+}
+
+/* OffsetRay, template/tmpl8math.cpp:473-487 (Ray Tracing Gems ch. 6) */
+static v3 offset_ray(v3 p, v3 n)
+{
+    const int ox = f2i_trunc(256.0f * n.x), oy = f2i_trunc(256.0f * n.y), oz = f2i_trunc(256.0f * n.z);
+    const float pix = u2f_bits(f2u_bits(p.x) + (uint32_t)((p.x < 0) ? -ox : ox));
+    const float piy = u2f_bits(f2u_bits(p.y) + (uint32_t)((p.y < 0) ? -oy : oy));
+    const float piz = u2f_bits(f2u_bits(p.z) + (uint32_t)((p.z < 0) ? -oz : oz));
+    const float origin = 1.0f / 32.0f, fs = 1.0f / 65536.0f;
+    return V3(fabsf(p.x) < origin ? p.x + fs * n.x : pix, fabsf(p.y) < origin ? p.y + fs * n.y : piy,
+              fabsf(p.z) < origin ? p.z + fs * n.z : piz);
+}
+
+void oracle_offset_ray(const float p[3], const float n[3], float out[3])
+{
+    const v3 r = offset_ray(v3f(p), v3f(n));
+    out[0] = r.x, out[1] = r.y, out[2] = r.z;
+}
+
+/* --------------------------------------------------------------------- voxels -- */
+typedef struct {
+    const oracle_scene* sc;
+    uint32_t rng;
+    float sky[3];
+    int area_samples;
+    uint64_t shadow_rays, nearest_calls, dda_cells;
+} tctx;
+
+typedef struct {
+    int sx, sy, sz;  /* step */
+    uint32_t X, Y, Z;
+    float t;
+    v3 tdelta, tmax;
+} dda_t;
+
+/* Cube::Intersect, template/scene.cpp:166-202 */
+static float cube_intersect(v3 b0, v3 b1, const ray_t* r)
+{
+    const int signx = r->D.x < 0, signy = r->D.y < 0, signz = r->D.z < 0;
+    const float bx[2] = {b0.x, b1.x}, by[2] = {b0.y, b1.y}, bz[2] = {b0.z, b1.z};
+    float tmin_x = (bx[signx] - r->O.x) * r->rD.x;
+    float tmax_x = (bx[1 - signx] - r->O.x) * r->rD.x;
+    const float tmin_y = (by[signy] - r->O.y) * r->rD.y;
+    const float tmax_y = (by[1 - signy] - r->O.y) * r->rD.y;
+    if (tmin_x > tmax_y || tmin_y > tmax_x) return BIG_T;
+    tmin_x = smax(tmin_x, tmin_y);
+    tmax_x = smin(tmax_x, tmax_y);
+    const float tmin_z = (bz[signz] - r->O.z) * r->rD.z;
+    const float tmax_z = (bz[1 - signz] - r->O.z) * r->rD.z;
+    if (tmin_x > tmax_z || tmin_z > tmax_x) return BIG_T;
+    tmin_x = smax(tmin_x, tmin_z);
+    if (tmin_x > 0) return tmin_x;
+    return BIG_T;
+}
+
+float oracle_cube_intersect(const float b0[3], const float b1[3], const float o[3],
+                            const float d[3], const float rd[3])
+{
+    ray_t r;
+    r.O = v3f(o), r.D = v3f(d), r.rD = v3f(rd);
+    return cube_intersect(v3f(b0), v3f(b1), &r);
+}
+
+/* Cube::Contains, template/scene.cpp:205-210 */
+static inline int cube_contains(v3 b0, v3 b1, v3 p)
+{
+    return p.x >= b0.x && p.y >= b0.y && p.z >= b0.z && p.x <= b1.x && p.y <= b1.y && p.z <= b1.z;
+}
+
+/* Scene::Setup3DDDA, template/scene.cpp:719-749 */
+static int setup_dda(const vpx_volume* vol, uint32_t n, const ray_t* r, dda_t* s)
+{
+    const v3 b0 = v3f(vol->b0), b1 = v3f(vol->b1);
+    s->t = 0;
+    if (!cube_contains(b0, b1, r->O)) {
+        s->t = cube_intersect(b0, b1, r);
+        if (s->t > 1e33f) return 0;
+    }
+    const v3 vmin = b0;
+    const v3 vmax = vsub(b1, b0);
+    const float g = (float)n;
+    const float cell = 1.0f / g;
+    const v3 stepf = vsub(V3(1, 1, 1), vmuls(r->Dsign, 2)); /* 1 - Dsign*2 */
+    s->sx = f2i_trunc(stepf.x), s->sy = f2i_trunc(stepf.y), s->sz = f2i_trunc(stepf.z);
+    const v3 pos = vdiv(vmuls(vadd(vsub(r->O, vmin), vmuls(r->D, s->t + 0.00005f)), g), vmax);
+    const v3 planes = vmuls(vsub(V3(ceilf(pos.x), ceilf(pos.y), ceilf(pos.z)), r->Dsign), cell);
+    const int hi = (int)(n - 1);
+    int px = f2i_trunc(pos.x), py = f2i_trunc(pos.y), pz = f2i_trunc(pos.z);
+    px = px < 0 ? 0 : (px > hi ? hi : px); /* clamp(int3, 0, gridsize-1), tmpl8math.h:2110-2113 */
+    py = py < 0 ? 0 : (py > hi ? hi : py);
+    pz = pz < 0 ? 0 : (pz > hi ? hi : pz);
+    s->X = (uint32_t)px, s->Y = (uint32_t)py, s->Z = (uint32_t)pz;
+    s->tdelta = vmul(V3(cell * (float)s->sx, cell * (float)s->sy, cell * (float)s->sz), r->rD);
+    s->tmax = vmul(vsub(vmul(planes, vmax), vsub(r->O, vmin)), r->rD);
+    return 1;
+}
+
+static inline uint8_t grid_at(const oracle_grid* g, uint32_t x, uint32_t y, uint32_t z)
+{
+    const uint64_t n = g->n;
+    return g->cells[(uint64_t)x + (uint64_t)y * n + (uint64_t)z * n * n];
+}
+
+/* One Amanatides-Woo step, shared by FindNearest/FindMaterialExit/FindSmokeExit
+   (scene.cpp:773-802).  Returns 0 when the walk leaves the grid. */
+static inline int dda_step(dda_t* s, uint32_t n)
+{
+    if (s->tmax.x < s->tmax.y) {
+        if (s->tmax.x < s->tmax.z) {
+            s->t = s->tmax.x, s->X += (uint32_t)s->sx;
+            if (s->X >= n) return 0;
+            s->tmax.x += s->tdelta.x;
+        } else {
+            s->t = s->tmax.z, s->Z += (uint32_t)s->sz;
+            if (s->Z >= n) return 0;
+            s->tmax.z += s->tdelta.z;
+        }
+    } else {
+        if (s->tmax.y < s->tmax.z) {
+            s->t = s->tmax.y, s->Y += (uint32_t)s->sy;
+            if (s->Y >= n) return 0;
+            s->tmax.y += s->tdelta.y;
+        } else {
+            s->t = s->tmax.z, s->Z += (uint32_t)s->sz;
+            if (s->Z >= n) return 0;
+            s->tmax.z += s->tdelta.z;
+        }
+    }
+    return 1;
+}
+
+/* Ray::GetNormalVoxel, template/scene.cpp:121-148 */
+static v3 normal_voxel(const ray_t* r, uint32_t n, const float* matrix)
+{
+    const v3 i1 = vmuls(ray_point(r), (float)n);
+    const v3 fg = V3(i1.x - floorf(i1.x), i1.y - floorf(i1.y), i1.z - floorf(i1.z));
+    const v3 d = V3(smin(fg.x, 1.0f - fg.x), smin(fg.y, 1.0f - fg.y), smin(fg.z, 1.0f - fg.z));
+    const float mind = smin(smin(d.x, d.y), d.z);
+    const v3 sign = vsub(vmuls(r->Dsign, 2), V3(1, 1, 1));
+    const v3 nn = V3(mind == d.x ? sign.x : 0.0f, mind == d.y ? sign.y : 0.0f, mind == d.z ? sign.z : 0.0f);
+    return vnormalize(xform_vec(nn, matrix));
+}
+
+/* Scene::FindNearest, template/scene.cpp:751-811 */
+static int scene_find_nearest(tctx* c, const vpx_volume* vol, ray_t* r)
+{
+    const oracle_grid* g = &c->sc->grids[vol->grid_id];
+    dda_t s;
+    if (!setup_dda(vol, g->n, r, &s)) return 0;
+    while (s.t < r->t) {
+        const uint8_t cell = grid_at(g, s.X, s.Y, s.Z);
+        c->dda_cells++;
+        if (cell != NONE_MAT && s.t < r->t) {
+            r->t = s.t;
+            r->N = normal_voxel(r, g->n, vol->matrix);
+            r->mat = cell;
+            return 1;
+        }
+        if (!dda_step(&s, g->n)) break;
+    }
+    return 0;
+}
+
+/* Scene::FindMaterialExit (:875-939) and Scene::FindSmokeExit (:941-1006). */
+static int scene_find_exit(tctx* c, const vpx_volume* vol, ray_t* r, int smoke)
+{
+    const oracle_grid* g = &c->sc->grids[vol->grid_id];
+    dda_t s;
+    if (!setup_dda(vol, g->n, r, &s)) return 0;
+    for (;;) {
+        const uint8_t cell = grid_at(g, s.X, s.Y, s.Z);
+        c->dda_cells++;
+        const int leave = smoke ? (cell > VPX_MAT_SMOKE_PLAYER || cell < VPX_MAT_SMOKE_LOW_DENSITY)
+                                : (cell != VPX_MAT_GLASS);
+        if (leave) {
+            r->t = s.t;
+            r->N = normal_voxel(r, g->n, vol->matrix);
+            r->mat = cell;
+            return 1;
+        }
+        if (!dda_step(&s, g->n)) break;
+    }
+    r->t = s.t;
+    return 0;
+}
+
+/* Scene::IsOccluded, template/scene.cpp:1009-1047 */
+static int scene_is_occluded(tctx* c, const vpx_volume* vol, const ray_t* r)
+{
+    const oracle_grid* g = &c->sc->grids[vol->grid_id];
+    const uint32_t n = g->n;
+    dda_t s;
+    if (!setup_dda(vol, n, r, &s)) return 0;
+    while (s.t < r->t) {
+        const uint8_t cell = grid_at(g, s.X, s.Y, s.Z);
+        c->dda_cells++;
+        if (cell != NONE_MAT) return s.t < r->t;
+        if (s.tmax.x < s.tmax.y) {
+            if (s.tmax.x < s.tmax.z) {
+                if ((s.X += (uint32_t)s.sx) >= n) return 0;
+                s.t = s.tmax.x, s.tmax.x += s.tdelta.x;
+            } else {
+                if ((s.Z += (uint32_t)s.sz) >= n) return 0;
+                s.t = s.tmax.z, s.tmax.z += s.tdelta.z;
+            }
+        } else {
+            if (s.tmax.y < s.tmax.z) {
+                if ((s.Y += (uint32_t)s.sy) >= n) return 0;
+                s.t = s.tmax.y, s.tmax.y += s.tdelta.y;
+            } else {
+                if ((s.Z += (uint32_t)s.sz) >= n) return 0;
+                s.t = s.tmax.z, s.tmax.z += s.tdelta.z;
+            }
+        }
+    }
+    return 0;
+}
+
+/* ------------------------------------------------------------------ analytic -- */
+/* Sphere::Hit, src/BVH/Shapes.h:12-42 */
+static void sphere_hit(const vpx_sphere* sp, ray_t* r)
+{
+    const v3 center = v3f(sp->center);
+    const v3 to = vsub(r->O, center);
+    const float b = vdot(to, r->D);
+    const float c = vdot(to, to) - (sp->radius * sp->radius);
+    const float disc = b * b - c;
+    if (c > 0.0f && b > 0.0f) return;
+    if (disc < 0) return;
+    const float len = -b - sqrtf(disc);
+    if (len > r->t) return;
+    if (len < 0) return;
+    const v3 ip = vadd(r->O, vmuls(r->D, len));
+    const v3 outn = vdivs(vsub(ip, center), sp->radius);
+    const int outside = vdot(r->D, outn) < 0;
+    r->N = outside ? outn : vneg(outn);
+    r->inside = !outside;
+    r->t = len;
+    r->mat = sp->material;
+}
+
+/* Sphere::IsHit, src/BVH/Shapes.h:44-63 */
+static int sphere_is_hit(const vpx_sphere* sp, const ray_t* r)
+{
+    const v3 center = v3f(sp->center);
+    const v3 to = vsub(r->O, center);
+    const float b = vdot(to, r->D);
+    const float c = vdot(to, to) - (sp->radius * sp->radius);
+    const float disc = b * b - c;
+    if (c > 0.0f && b > 0.0f) return 0;
+    if (disc < 0) return 0;
+    const float len = -b - sqrtf(disc);
+    if (len < 0) return 0;
+    if (len > r->t) return 0;
+    return 1;
+}
+
+/* Triangle::Hit / IsHit, src/BVH/Shapes.h:79-139 (Moller-Trumbore). */
+static int tri_core(const vpx_triangle* tr, const ray_t* r, float* tout, v3* e1o, v3* e2o)
+{
+    const v3 pos = v3f(tr->position);
+    const v3 p1 = vadd(pos, v3f(tr->v0)), p2 = vadd(pos, v3f(tr->v1)), p3 = vadd(pos, v3f(tr->v2));
+    const v3 e1 = vsub(p2, p1), e2 = vsub(p3, p1);
+    const v3 h = vcross(r->D, e2);
+    const float a = vdot(e1, h);
+    if (a > -0.0001f && a < 0.0001f) return 0;
+    const float f = 1 / a;
+    const v3 s = vsub(r->O, p1);
+    const float u = f * vdot(s, h);
+    if (u < 0 || u > 1) return 0;
+    const v3 q = vcross(s, e1);
+    const float v = f * vdot(r->D, q);
+    if (v < 0 || u + v > 1) return 0;
+    *tout = f * vdot(e2, q);
+    *e1o = e1, *e2o = e2;
+    return 1;
+}
+
+static void tri_hit(const vpx_triangle* tr, ray_t* r)
+{
+    float t;
+    v3 e1, e2;
+    if (!tri_core(tr, r, &t, &e1, &e2)) return;
+    if (t > 0.0001f) {
+        if (r->t > t) {
+            r->t = t;
+            r->mat = tr->material;
+            const v3 nrm = vnormalize(vcross(e1, e2));
+            const int outside = vdot(r->D, nrm) < 0;
+            r->N = outside ? nrm : vneg(nrm);
+        }
+    }
+}
+
+static int tri_is_hit(const vpx_triangle* tr, const ray_t* r)
+{
+    float t;
+    v3 e1, e2;
+    if (!tri_core(tr, r, &t, &e1, &e2)) return 0;
+    if (t < 0.0001f) return 0;
+    if (t > r->t) return 0;
+    return 1;
+}
+
+/* ------------------------------------------------------------- renderer level -- */
+/* Renderer::FindNearest, renderer.cpp:946-1018 */
+static int32_t renderer_find_nearest(tctx* c, ray_t* r)
+{
+    const oracle_scene* sc = c->sc;
+    int32_t vox = -2;
+    c->nearest_calls++;
+    for (uint32_t i = 0; i < sc->num_volumes; i++) {
+        const ray_t backup = *r;
+        const float* inv = sc->volumes[i].inv_matrix;
+        r->O = xform_pos_ssem(backup.O, inv);
+        r->D = xform_vec_ssem(backup.D, inv);
+        r->rD = V3(1.0f / r->D.x, 1.0f / r->D.y, 1.0f / r->D.z); /* FastReciprocal -> exact */
+        r->Dsign = compute_dsign(r->D);
+        if (scene_find_nearest(c, &sc->volumes[i], r)) vox = (int32_t)i;
+        r->O = backup.O, r->D = backup.D, r->rD = backup.rD, r->Dsign = backup.Dsign;
+    }
+    if (sc->num_spheres || sc->num_triangles) {
+        ray_t sh = make_ray(r->O, r->D);
+        for (uint32_t i = 0; i < sc->num_spheres; i++) sphere_hit(&sc->spheres[i], &sh);
+        for (uint32_t i = 0; i < sc->num_triangles; i++) tri_hit(&sc->triangles[i], &sh);
+        if (r->t > sh.t) {
+            r->t = sh.t;
+            r->mat = sh.mat;
+            r->N = sh.N;
+            r->inside = sh.inside;
+            vox = -1;
+        }
+    }
+    return vox;
+}
+
+/* Renderer::IsOccluded, renderer.cpp:209-243 */
+static int renderer_is_occluded(tctx* c, ray_t* r)
+{
+    const oracle_scene* sc = c->sc;
+    for (uint32_t i = 0; i < sc->num_volumes; i++) {
+        const ray_t backup = *r;
+        const float* inv = sc->volumes[i].inv_matrix;
+        r->O = xform_pos(backup.O, inv);
+        r->D = xform_vec(backup.D, inv);
+        r->rD = V3(1 / r->D.x, 1 / r->D.y, 1 / r->D.z);
+        r->Dsign = compute_dsign(r->D);
+        const int occ = scene_is_occluded(c, &sc->volumes[i], r);
+        r->O = backup.O, r->D = backup.D, r->rD = backup.rD, r->Dsign = backup.Dsign;
+        if (occ) return 1;
+    }
+    for (uint32_t i = 0; i < sc->num_spheres; i++)
+        if (sphere_is_hit(&sc->spheres[i], r)) return 1;
+    for (uint32_t i = 0; i < sc->num_triangles; i++)
+        if (tri_is_hit(&sc->triangles[i], r)) return 1;
+    return 0;
+}
+
+static int shadow_occluded(tctx* c, ray_t* r)
+{
+    c->shadow_rays++;
+    return renderer_is_occluded(c, r);
+}
+
+static inline v3 albedo_of(tctx* c, uint32_t m) { return v3f(c->sc->materials[m].albedo); }
+static inline float rf(tctx* c) { return oracle_random_float(&c->rng); }
+
+/* RandomDirection, template/tmpl8math.cpp:76-93 (positive octant only) */
+static v3 random_direction(tctx* c)
+{
+    for (;;) {
+        const float a = rf(c), b = rf(c), d = rf(c); /* brace-init: left to right */
+        const v3 p = V3(a, b, d);
+        if (vdot(p, p) < 1) return vnormalize(p);
+    }
+}
+
+/* RandomSphereSample, template/tmpl8math.h:2502-2511 */
+static v3 random_sphere_sample(tctx* c)
+{
+    const float theta = rf(c) * 2 * PI_F;
+    const float phi = rf(c) * PI_F;
+    const float r = rf(c);
+    const float x = r * cr_sinf(phi) * cr_cosf(theta);
+    const float y = r * cr_sinf(phi) * cr_sinf(theta);
+    const float z = r * cr_cosf(phi);
+    return V3(x, y, z);
+}
+
+/* DiffuseReflection, template/tmpl8math.h:2518-2528 (argument order: left to right) */
+static v3 diffuse_reflection(tctx* c, v3 n)
+{
+    v3 r;
+    do {
+        const float a = rf(c) * 2 - 1;
+        const float b = rf(c) * 2 - 1;
+        const float d = rf(c) * 2 - 1;
+        r = V3(a, b, d);
+    } while (vdot(r, r) > 1);
+    if (vdot(r, n) < 0) r = vmuls(r, -1.0f);
+    return vnormalize(r);
+}
+
+/* Renderer::Reflect / Refract, renderer.cpp:913-925 */
+static inline v3 reflect(v3 d, v3 n) { return vsub(d, vmuls(vmuls(n, 2.0f), vdot(n, d))); }
+static inline v3 refract(v3 d, v3 n, float ratio)
+{
+    const float cos_t = smin(vdot(vneg(d), n), 1.0f);
+    const v3 rper = vmuls(vadd(d, vmuls(n, cos_t)), ratio);
+    const v3 rpar = vmuls(n, -sqrtf(fabsf(1.0f - vdot(rper, rper))));
+    return vadd(rper, rpar);
+}
+
+/* SchlickReflectance (renderer.cpp:1588-1594), SchlickReflectanceNonMetal (:1611-1616) */
+static inline float schlick(float cosine, float ior)
+{
+    float r0 = (1 - ior) / (1 + ior);
+    r0 = r0 * r0;
+    return r0 + (1 - r0) * cr_powf((1 - cosine), 5);
+}
+static inline float schlick_nonmetal(float cosine)
+{
+    const float r0 = 0.04f;
+    return r0 + (1 - r0) * cr_powf((1 - cosine), 5);
+}
+
+/* Renderer::Absorption, renderer.cpp:1596-1608 */
+static inline v3 absorption(v3 color, float intensity, float dist)
+{
+    const v3 flipped = vsub(V3(1, 1, 1), color);
+    const v3 e = vmuls(flipped, (-dist) * intensity);
+    return V3(cr_expf(e.x), cr_expf(e.y), cr_expf(e.z));
+}
+
+/* PointLightEvaluate, renderer.cpp:102-131 */
+static v3 point_light(tctx* c, const ray_t* r, const vpx_point_light* l)
+{
+    const v3 ip = ray_point(r);
+    const v3 dir = vsub(v3f(l->position), ip);
+    const float dst = vlength(dir);
+    const v3 dn = vmuls(dir, 1.0f / dst);
+    const v3 n = r->N;
+    const float cos_t = vdot(dn, n);
+    if (cos_t <= 0.0f) return V3(0, 0, 0);
+    const v3 li = vmuls(vmuls(v3f(l->color), smax(0.0f, cos_t)), 1.0f / (dst * dst));
+    const v3 origin = offset_ray(ip, n);
+    const v3 k = albedo_of(c, r->mat);
+    ray_t sh = make_ray(origin, dn);
+    sh.t = dst;
+    if (shadow_occluded(c, &sh)) return V3(0, 0, 0);
+    return vmul(li, k);
+}
+
+/* SpotLightEvaluate, renderer.cpp:133-159 (no N.L term) */
+static v3 spot_light(tctx* c, const ray_t* r, const vpx_spot_light* l)
+{
+    const v3 ip = ray_point(r);
+    const v3 dir = vsub(v3f(l->position), ip);
+    const float dst = vlength(dir);
+    const v3 dn = vdivs(dir, dst);
+    const v3 n = r->N;
+    const float cos_t = vdot(dn, v3f(l->direction));
+    if (cos_t <= l->angle) return V3(0, 0, 0);
+    const float alpha = 1.0f - (1.0f - cos_t) * 1.0f / (1.0f - l->angle);
+    const v3 li = vdivs(vmuls(v3f(l->color), smax(0.0f, cos_t)), dst * dst);
+    const v3 k = albedo_of(c, r->mat);
+    ray_t sh = make_ray(offset_ray(ip, n), dn);
+    sh.t = dst;
+    if (shadow_occluded(c, &sh)) return V3(0, 0, 0);
+    return vmuls(vmul(li, k), alpha);
+}
+
+/* AreaLightEvaluation, renderer.cpp:161-207 (PI4 expands textually: *PI*4.0f) */
+static v3 area_light(tctx* c, const ray_t* r, const vpx_area_light* l)
+{
+    const v3 ip = ray_point(r);
+    const v3 n = r->N;
+    const v3 center = v3f(l->position);
+    const float radius = l->radius;
+    v3 inc = V3(0, 0, 0);
+    const v3 k = albedo_of(c, r->mat);
+    const v3 point = offset_ray(ip, n);
+    for (int i = 0; i < c->area_samples; i++) {
+        v3 rp = random_direction(c);
+        rp = vmuls(rp, radius);
+        rp = vadd(rp, center);
+        const v3 dir = vsub(rp, ip);
+        const float dst = vlength(dir);
+        const v3 dn = vmuls(dir, 1 / dst);
+        const float cos_t = vdot(dn, n);
+        if (cos_t <= 0) continue;
+        ray_t sh = make_ray(point, dn);
+        sh.t = dst;
+        if (shadow_occluded(c, &sh)) continue;
+        v3 li = vmuls(v3f(l->color), cos_t);
+        li = vmuls(li, l->color_multiplier);
+        li = vmuls(li, radius * radius);
+        li = vmuls(li, PI_F);
+        li = vmuls(li, 4.0f);
+        li = vdivs(li, dst * dst);
+        inc = vadd(inc, li);
+    }
+    inc = vdivs(inc, (float)c->area_samples);
+    return vmul(inc, k);
+}
+
+/* DirectionalLightEvaluate, renderer.cpp:315-338 (direction not normalised) */
+static v3 dir_light(tctx* c, const ray_t* r, const vpx_dir_light* l)
+{
+    const v3 ip = ray_point(r);
+    const v3 dir = vneg(v3f(l->direction));
+    const v3 n = r->N;
+    const float cos_t = vdot(dir, n);
+    if (cos_t <= 0) return V3(0, 0, 0);
+    const v3 li = vmuls(v3f(l->color), smax(0.0f, cos_t));
+    const v3 k = albedo_of(c, r->mat);
+    ray_t sh = make_ray(offset_ray(ip, n), dir);
+    if (shadow_occluded(c, &sh)) return V3(0, 0, 0);
+    return vmul(li, k);
+}
+
+/* Renderer::Illumination, renderer.cpp:738-764 */
+static v3 illumination(tctx* c, const ray_t* r)
+{
+    const oracle_scene* sc = c->sc;
+    const uint64_t pc = sc->num_points, sc_ = sc->num_spots, ac = sc->num_areas;
+    const uint64_t light_count = pc + sc_ + ac + 1;
+    const float rnd = rf(c) * (float)light_count;
+    const uint64_t idx = (uint64_t)rnd;
+    v3 inc;
+    if (idx < pc)
+        inc = point_light(c, r, &sc->points[idx]);
+    else if (idx < ac + pc)
+        inc = area_light(c, r, &sc->areas[idx - pc]);
+    else if (idx < ac + sc_ + pc)
+        inc = spot_light(c, r, &sc->spots[idx - ac - pc]);
+    else
+        inc = dir_light(c, r, &sc->dir);
+    return vmuls(inc, (float)light_count);
+}
+
+/* Object-space helper of the glass/smoke branches (renderer.cpp:1160-1173, 1266-1279). */
+static int exit_march(tctx* c, ray_t* r, int32_t vox, int smoke)
+{
+    const vpx_volume* vol = &c->sc->volumes[vox];
+    const ray_t backup = *r;
+    r->O = xform_pos(backup.O, vol->inv_matrix);
+    r->D = xform_vec(backup.D, vol->inv_matrix);
+    r->rD = V3(1 / r->D.x, 1 / r->D.y, 1 / r->D.z);
+    r->Dsign = compute_dsign(r->D);
+    const int res = scene_find_exit(c, vol, r, smoke);
+    r->O = backup.O, r->D = backup.D, r->rD = backup.rD, r->Dsign = backup.Dsign;
+    return res;
+}
+
+/* Renderer::Trace, renderer.cpp:1076-1328 */
+static v3 trace(tctx* c, ray_t* r, int depth)
+{
+    if (depth < 0) return V3(0, 0, 0);
+    const int32_t vox = renderer_find_nearest(c, r);
+    if (r->mat == NONE_MAT) return V3(c->sky[0], c->sky[1], c->sky[2]); /* SampleSky :2308-2313 */
+    const vpx_material* mat = &c->sc->materials[r->mat];
+    switch (r->mat) {
+    case 5: case 6: case 7: { /* metals :1103-1114 */
+        const v3 refl = reflect(r->D, r->N);
+        const v3 o = offset_ray(ray_point(r), r->N);
+        const v3 d = vadd(refl, vmuls(random_sphere_sample(c), mat->roughness));
+        ray_t nr = make_ray(o, d);
+        return vmul(trace(c, &nr, depth - 1), albedo_of(c, r->mat));
+    }
+    case 0: case 4: case 1: case 2: case 3: { /* non-metals :1117-1144 */
+        v3 color = V3(0, 0, 0);
+        if (rf(c) > schlick_nonmetal(vdot(vneg(r->D), r->N))) {
+            const v3 rdir = vadd(r->N, random_sphere_sample(c));
+            const v3 inc = illumination(c, r);
+            ray_t nr = make_ray(offset_ray(ray_point(r), r->N), rdir);
+            color = vadd(color, inc);
+            color = vadd(color, vmul(trace(c, &nr, depth - 1), albedo_of(c, r->mat)));
+        } else {
+            const v3 refl = reflect(r->D, r->N);
+            const v3 o = offset_ray(ray_point(r), r->N);
+            const v3 d = vadd(refl, vmuls(random_sphere_sample(c), mat->roughness));
+            ray_t nr = make_ray(o, d);
+            color = trace(c, &nr, depth - 1);
+        }
+        return color;
+    }
+    case VPX_MAT_GLASS: { /* :1146-1209 */
+        v3 color = V3(1, 1, 1);
+        int in_glass = r->inside;
+        const float ior = mat->ior;
+        const float ratio = in_glass ? ior : 1.0f / ior;
+        int inside_volume = 1;
+        if (in_glass) {
+            color = albedo_of(c, r->mat);
+            if (vox >= 0) inside_volume = exit_march(c, r, vox, 0); /* vox < 0: UB guard */
+        }
+        if (!inside_volume) {
+            r->O = vadd(r->O, vmuls(r->D, r->t));
+            r->t = 0;
+        }
+        const float cos_t = smin(vdot(vneg(r->D), r->N), 1.0f);
+        const float sin_t = sqrtf(1.0f - cos_t * cos_t);
+        const int cannot = ratio * sin_t > 1.0f;
+        v3 rdir, rn;
+        if (cannot || schlick(cos_t, ratio) > rf(c)) {
+            rdir = reflect(r->D, r->N);
+            rn = r->N;
+        } else {
+            rdir = refract(r->D, r->N, ratio);
+            in_glass = !in_glass;
+            rn = vneg(r->N);
+        }
+        ray_t nr = make_ray(offset_ray(ray_point(r), rn), rdir);
+        nr.inside = in_glass;
+        return vmul(trace(c, &nr, depth - 1), color);
+    }
+    case 9: case 10: case 11: case 12: case 13: case 14: { /* smoke :1210-1314 */
+        v3 color = V3(1, 1, 1);
+        int in_glass = r->inside;
+        const float ratio = 1.0f;
+        int inside_volume = 1;
+        float intensity = 0, dist = 0;
+        if (vox == 0) (void)illumination(c, r); /* player light probe :1228-1240 */
+        if (in_glass) {
+            intensity = mat->emissive;
+            color = albedo_of(c, r->mat);
+            if (vox >= 0) inside_volume = exit_march(c, r, vox, 1);
+            dist = r->t;
+        }
+        const float threshold = rf(c) * 100 - intensity;
+        if (rf(c) * dist > threshold) {
+            const float lo = r->t * .45f, hi = r->t;
+            const float tt = lo + rf(c) * (hi - lo); /* Rand(min, max), tmpl8math.cpp:154 */
+            r->O = vadd(r->O, vmuls(r->D, tt));
+            r->D = random_direction(c);
+            r->t = 0;
+        }
+        color = absorption(color, intensity, dist);
+        if (!inside_volume) {
+            r->O = vadd(r->O, vmuls(r->D, r->t));
+            r->t = 0;
+        }
+        const v3 rdir = refract(r->D, r->N, ratio);
+        in_glass = !in_glass;
+        const v3 rn = vneg(r->N);
+        ray_t nr = make_ray(offset_ray(ray_point(r), rn), rdir);
+        nr.inside = in_glass;
+        return vmul(trace(c, &nr, depth - 1), color);
+    }
+    case VPX_MAT_EMISSIVE: /* :1315-1316 */
+        return vmuls(albedo_of(c, r->mat), mat->emissive);
+    default: { /* model materials :1319-1326 */
+        const v3 rdir = diffuse_reflection(c, r->N);
+        const v3 inc = illumination(c, r);
+        ray_t nr = make_ray(offset_ray(ray_point(r), r->N), rdir);
+        return vmul(vadd(trace(c, &nr, depth - 1), inc), albedo_of(c, r->mat));
+    }
+    }
+}
+
+/* ------------------------------------------------------------------ FTZ/DAZ -- */
+typedef struct { unsigned int csr; } fpstate;
+static inline fpstate fp_enter(void)
+{
+    fpstate s = {0};
+#ifdef ORACLE_X86
+    s.csr = _mm_getcsr();
+    _mm_setcsr(s.csr | 0x8040u); /* FTZ | DAZ, template/template.cpp:130 */
+#endif
+    return s;
+}
+static inline void fp_leave(fpstate s)
+{
+#ifdef ORACLE_X86
+    _mm_setcsr(s.csr);
+#else
+    (void)s;
+#endif
+}
+
+static ray_t ray_from_api(const vpx_ray* in)
+{
+    ray_t r = make_ray(v3f(in->origin), v3f(in->direction));
+    r.t = in->tmax;
+    r.inside = in->inside_glass ? 1 : 0;
+    return r;
+}
+
+static void tctx_init(tctx* c, const oracle_scene* sc)
+{
+    memset(c, 0, sizeof(*c));
+    c->sc = sc;
+    c->sky[0] = 0.392f, c->sky[1] = 0.584f, c->sky[2] = 0.829f;
+    c->area_samples = 3;
+}
+
+int oracle_find_nearest(const oracle_scene* sc, const vpx_ray* rays, uint32_t n, vpx_hit* hits)
+{
+    if (!sc || (!rays && n) || (!hits && n)) return VPX_E_INVALID;
+    const fpstate fs = fp_enter();
+    tctx c;
+    tctx_init(&c, sc);
+    for (uint32_t i = 0; i < n; i++) {
+        ray_t r = ray_from_api(&rays[i]);
+        const uint64_t before = c.dda_cells;
+        const int32_t vox = renderer_find_nearest(&c, &r);
+        hits[i].t = r.t;
+        hits[i].normal[0] = r.N.x, hits[i].normal[1] = r.N.y, hits[i].normal[2] = r.N.z;
+        hits[i].vox_index = vox;
+        hits[i].material = r.mat;
+        hits[i].cells = (uint32_t)(c.dda_cells - before);
+        hits[i].inside_glass = (uint32_t)r.inside;
+    }
+    fp_leave(fs);
+    return VPX_OK;
+}
+
+int oracle_is_occluded(const oracle_scene* sc, const vpx_ray* rays, uint32_t n, uint8_t* occluded,
+                       uint32_t* cells)
+{
+    if (!sc || (!rays && n) || (!occluded && n)) return VPX_E_INVALID;
+    const fpstate fs = fp_enter();
+    tctx c;
+    tctx_init(&c, sc);
+    for (uint32_t i = 0; i < n; i++) {
+        ray_t r = ray_from_api(&rays[i]);
+        const uint64_t before = c.dda_cells;
+        occluded[i] = (uint8_t)renderer_is_occluded(&c, &r);
+        if (cells) cells[i] = (uint32_t)(c.dda_cells - before);
+    }
+    fp_leave(fs);
+    return VPX_OK;
+}
+
+int oracle_trace(const oracle_scene* sc, const vpx_ray* rays, const uint32_t* seeds, uint32_t n,
+                 int32_t depth, const float sky[3], int32_t area_samples, float* radiance,
+                 vpx_stats* stats)
+{
+    if (!sc || (!rays && n) || (!seeds && n) || (!radiance && n)) return VPX_E_INVALID;
+    const fpstate fs = fp_enter();
+    tctx c;
+    tctx_init(&c, sc);
+    if (sky) c.sky[0] = sky[0], c.sky[1] = sky[1], c.sky[2] = sky[2];
+    c.area_samples = area_samples;
+    for (uint32_t i = 0; i < n; i++) {
+        ray_t r = ray_from_api(&rays[i]);
+        c.rng = seeds[i];
+        const v3 v = trace(&c, &r, depth);
+        radiance[3 * i] = v.x, radiance[3 * i + 1] = v.y, radiance[3 * i + 2] = v.z;
+    }
+    if (stats) {
+        memset(stats, 0, sizeof(*stats));
+        stats->primary_rays = n;
+        stats->shadow_rays = c.shadow_rays;
+        stats->bounce_rays = c.nearest_calls - (c.nearest_calls ? n : 0);
+        stats->dda_cells = c.dda_cells;
+    }
+    fp_leave(fs);
+    return VPX_OK;
+}
+
+/* ------------------------------------------------------------------- pixels -- */
+/* Primary ray: Camera::GetPrimaryRayNoDOF (camera.h:103-110) or GetPrimaryRay with the
+   thin-lens jitter (camera.h:68-83) when VPX_FLAG_DOF; sub-pixel jitter as the AVX path
+   computes it, fma(rand, aa, x) (renderer.cpp:1699-1708).  The primary D is normalised
+   exactly (the reference's _mm_rsqrt_ps normalize is vendor-specific).
+   Per-pixel stream order: [AA: rx, ry] [DOF: r, theta] then Trace. */
+static v3 pixel_sample(tctx* c, const vpx_frame_params* p, uint32_t x, uint32_t y)
+{
+    const vpx_camera* cam = &c->sc->camera;
+    c->rng = oracle_pixel_seed(p->seed_base, p->frame_index, p->width, p->height, x, y);
+    float fx = (float)x, fy = (float)y;
+    if (p->flags & VPX_FLAG_AA) {
+        const float rx = rf(c), ry = rf(c);
+        fx = fmaf(rx, p->aa_strength, fx);
+        fy = fmaf(ry, p->aa_strength, fy);
+    }
+    const float u = fx * (1.0f / (float)p->width);
+    const float v = fy * (1.0f / (float)p->height);
+    const v3 tl = v3f(cam->top_left), tr = v3f(cam->top_right), bl = v3f(cam->bottom_left);
+    const v3 P = vadd(vadd(tl, vmuls(vsub(tr, tl), u)), vmuls(vsub(bl, tl), v));
+    const v3 cp = v3f(cam->cam_pos);
+    ray_t r;
+    if (p->flags & VPX_FLAG_DOF) {
+        const float rr = sqrtf(rf(c));
+        const float theta = rf(c) * (2 * PI_F);
+        const float cx = cr_cosf(theta) * rr, cy = cr_sinf(theta) * rr;
+        const float jx = cx * cam->defocus_jitter / (float)p->width;
+        const float jy = cy * cam->defocus_jitter / (float)p->width;
+        const v3 focal = vadd(cp, vmuls(vnormalize(vsub(P, cp)), cam->focal_distance));
+        const v3 o = vadd(vadd(cp, vmuls(v3f(cam->right), jx)), vmuls(v3f(cam->up), jy));
+        r = make_ray(o, vsub(focal, o));
+    } else {
+        r = make_ray(cp, vsub(P, cp));
+    }
+    return trace(c, &r, p->max_bounces);
+}
+
+/* GetLuminance (renderer.cpp:2237-2240), ApplyReinhardJodie (:2222-2234),
+   RGBF32_to_RGB8 (template/precomp.h:372-388), lerp (tmpl8math.h:2210-2213). */
+static uint32_t tonemap_pack(const float* acc)
+{
+    const v3 col = V3(acc[0], acc[1], acc[2]);
+    const float lum = vdot(col, V3(0.2126f, 0.7152f, 0.0722f));
+    const v3 rh = vdiv(col, V3(1.0f + col.x, 1.0f + col.y, 1.0f + col.z));
+    const v3 la = vdivs(col, 1.0f + lum);
+    const float o[3] = {la.x + rh.x * (rh.x - la.x), la.y + rh.y * (rh.y - la.y), la.z + rh.z * (rh.z - la.z)};
+    const uint32_t r = (uint32_t)(int64_t)(255.0f * smin(1.0f, o[0]));
+    const uint32_t g = (uint32_t)(int64_t)(255.0f * smin(1.0f, o[1]));
+    const uint32_t b = (uint32_t)(int64_t)(255.0f * smin(1.0f, o[2]));
+    return (r << 16) + (g << 8) + b;
+}
+
+/* Accumulator blend of the AVX path: acc = fma(1-w, acc, px*w) (renderer.cpp:1797-1828). */
+void oracle_accumulate_tonemap(const float* s4, uint32_t frame_index, float* acc4, uint32_t* rgb8)
+{
+    const fpstate fs = fp_enter();
+    const float w = 1.0f / ((float)frame_index + 1.0f);
+    const float iw = 1.0f - w;
+    for (int k = 0; k < 4; k++) acc4[k] = fmaf(iw, acc4[k], s4[k] * w);
+    if (rgb8) *rgb8 = tonemap_pack(acc4);
+    fp_leave(fs);
+}
+
+typedef struct {
+    const oracle_scene* sc;
+    const vpx_frame_params* p;
+    const uint32_t* ids;
+    uint32_t n;
+    float* out4;
+    float* accum;
+    uint32_t* rgb8;
+    uint32_t tid, nthreads;
+    uint64_t shadow, nearest, cells;
+} job_t;
+
+static void* render_worker(void* arg)
+{
+    job_t* j = (job_t*)arg;
+    const fpstate fs = fp_enter();
+    tctx c;
+    tctx_init(&c, j->sc);
+    c.sky[0] = j->p->sky[0], c.sky[1] = j->p->sky[1], c.sky[2] = j->p->sky[2];
+    c.area_samples = j->p->area_samples;
+    const uint32_t W = j->p->width;
+    const float w = 1.0f / ((float)j->p->frame_index + 1.0f);
+    const float iw = 1.0f - w;
+    for (uint32_t i = j->tid; i < j->n; i += j->nthreads) {
+        const uint32_t id = j->ids ? j->ids[i] : i;
+        const v3 v = pixel_sample(&c, j->p, id % W, id / W);
+        if (j->out4) {
+            float* o = j->out4 + 4 * (uint64_t)i;
+            o[0] = v.x, o[1] = v.y, o[2] = v.z, o[3] = 0.0f;
+        }
+        if (j->accum) {
+            float* a = j->accum + 4 * (uint64_t)id;
+            const float s[4] = {v.x, v.y, v.z, 0.0f};
+            for (int k = 0; k < 4; k++) a[k] = fmaf(iw, a[k], s[k] * w);
+            if (j->rgb8) j->rgb8[id] = tonemap_pack(a);
+        }
+    }
+    j->shadow = c.shadow_rays, j->nearest = c.nearest_calls, j->cells = c.dda_cells;
+    fp_leave(fs);
+    return NULL;
+}
+
+static int run_jobs(const oracle_scene* sc, const vpx_frame_params* p, const uint32_t* ids,
+                    uint32_t n, float* out4, float* accum, uint32_t* rgb8, vpx_stats* stats,
+                    int threads)
+{
+    if (threads <= 0) {
+        const long hc = sysconf(_SC_NPROCESSORS_ONLN);
+        threads = hc > 0 ? (int)hc : 1;
+    }
+    if (threads > 256) threads = 256;
+    job_t jobs[256];
+    pthread_t th[256];
+    for (int t = 0; t < threads; t++) {
+        jobs[t] = (job_t){sc, p, ids, n, out4, accum, rgb8, (uint32_t)t, (uint32_t)threads, 0, 0, 0};
+    }
+    int started = 0;
+    for (int t = 1; t < threads; t++) {
+        if (pthread_create(&th[t], NULL, render_worker, &jobs[t]) != 0) break;
+        started = t;
+    }
+    if (started < threads - 1) { /* could not start all: run the rest inline */
+        for (int t = started + 1; t < threads; t++) render_worker(&jobs[t]);
+    }
+    render_worker(&jobs[0]);
+    for (int t = 1; t <= started; t++) pthread_join(th[t], NULL);
+    if (stats) {
+        memset(stats, 0, sizeof(*stats));
+        stats->primary_rays = n;
+        for (int t = 0; t < threads; t++) {
+            stats->shadow_rays += jobs[t].shadow;
+            stats->bounce_rays += jobs[t].nearest;
+            stats->dda_cells += jobs[t].cells;
+        }
+        stats->bounce_rays -= n;
+    }
+    return VPX_OK;
+}
+
+int oracle_render_pixels(const oracle_scene* sc, const vpx_frame_params* p, const uint32_t* ids,
+                         uint32_t n, float* sample4, vpx_stats* stats, int threads)
+{
+    if (!sc || !p || !sample4 || (!ids && n)) return VPX_E_INVALID;
+    return run_jobs(sc, p, ids, n, sample4, NULL, NULL, stats, threads);
+}
+
+int oracle_render(const oracle_scene* sc, const vpx_frame_params* p, float* accum, uint32_t* rgb8,
+                  vpx_stats* stats, int threads)
+{
+    if (!sc || !p || !accum) return VPX_E_INVALID;
+    return run_jobs(sc, p, NULL, p->width * p->height, NULL, accum, rgb8, stats, threads);
+}
+
+/* Focus ray of Renderer::Tick (renderer.cpp:1987-1991): GetPrimaryRay(W/2, H/2) with DOF
+   jitter is not applied here (integer centre, circle drawn from the thread RNG in the
+   reference); the ray is tested against every Scene in WORLD space (reference quirk). */
+float oracle_focus_distance(const oracle_scene* sc, uint32_t width, uint32_t height)
+{
+    const fpstate fs = fp_enter();
+    tctx c;
+    tctx_init(&c, sc);
+    const vpx_camera* cam = &sc->camera;
+    const float u = (float)(width / 2) * (1.0f / (float)width);
+    const float v = (float)(height / 2) * (1.0f / (float)height);
+    const v3 tl = v3f(cam->top_left), tr = v3f(cam->top_right), bl = v3f(cam->bottom_left);
+    const v3 P = vadd(vadd(tl, vmuls(vsub(tr, tl), u)), vmuls(vsub(bl, tl), v));
+    const v3 cp = v3f(cam->cam_pos);
+    const v3 focal = vadd(cp, vmuls(vnormalize(vsub(P, cp)), cam->focal_distance));
+    ray_t r = make_ray(cp, vsub(focal, cp));
+    for (uint32_t i = 0; i < sc->num_volumes; i++) scene_find_nearest(&c, &sc->volumes[i], &r);
+    const float t = r.t;
+    fp_leave(fs);
+    return smax(-1.0f, smin(t, 1e4f)); /* clamp(t, -1, 1e4), tmpl8math.h:2105-2108 */
+}
+
+/* -------------------------------------------------------------------- worlds -- */
+/* Scene::LoadModel placement, template/scene.cpp:449-529 (ResetGrid() -> NONE first;
+   only downscales when size_x > gridsize; y/z swapped; out-of-range writes dropped). */
+void oracle_load_model(const uint8_t* vox, uint32_t sx, uint32_t sy, uint32_t sz, uint32_t n,
+                       const float scale_model[3], uint8_t* out)
+{
+    const uint64_t n64 = n;
+    memset(out, NONE_MAT, n64 * n64 * n64);
+    float scl[3] = {scale_model[0], scale_model[1], scale_model[2]};
+    if (sx > n) {
+        scl[0] *= (float)n / (float)sx;
+        scl[1] *= (float)n / (float)sy;
+        scl[2] *= (float)n / (float)sz;
+    }
+    for (uint32_t z = 0; z < sz; ++z)
+        for (uint32_t y = 0; y < sy; ++y)
+            for (uint32_t x = 0; x < sx; ++x) {
+                const int gx = f2i_trunc((float)x * scl[0]);
+                const int gy = f2i_trunc((float)z * scl[1]);
+                const int gz = f2i_trunc((float)y * scl[2]);
+                const uint8_t c = vox[x + (uint64_t)y * sx + (uint64_t)z * sx * sy];
+                if (c == 0) continue;
+                if (gx < 0 || gy < 0 || gz < 0 || (uint32_t)gx >= n || (uint32_t)gy >= n || (uint32_t)gz >= n)
+                    continue;
+                out[(uint64_t)gx + (uint64_t)gy * n64 + (uint64_t)gz * n64 * n64] = c;
+            }
+}
+
+void oracle_orient_model(const uint8_t* vox, uint32_t sx, uint32_t sy, uint32_t sz, uint8_t* out)
+{
+    /* grid-oriented dims: gx = sx, gy = sz, gz = sy */
+    for (uint32_t z = 0; z < sz; ++z)
+        for (uint32_t y = 0; y < sy; ++y)
+            for (uint32_t x = 0; x < sx; ++x) {
+                const uint8_t c = vox[x + (uint64_t)y * sx + (uint64_t)z * sx * sy];
+                out[x + (uint64_t)z * sx + (uint64_t)y * sx * sz] = c ? c : (uint8_t)NONE_MAT;
+            }
+}
+
+void oracle_tiled_world(const uint8_t* model, uint32_t mx, uint32_t my, uint32_t mz, uint32_t px,
+                        uint32_t py, uint32_t pz, uint32_t ground, uint32_t n, uint8_t* out)
+{
+    const uint64_t n64 = n;
+    for (uint64_t z = 0; z < n64; z++)
+        for (uint64_t y = 0; y < n64; y++) {
+            uint8_t* row = out + y * n64 + z * n64 * n64;
+            if (y < ground) {
+                memset(row, VPX_MAT_NON_METAL_WHITE, n64);
+                continue;
+            }
+            const uint64_t ly = (y - ground) % py, lz = z % pz;
+            for (uint64_t x = 0; x < n64; x++) {
+                const uint64_t lx = x % px;
+                row[x] = (lx < mx && ly < my && lz < mz) ? model[lx + ly * mx + lz * mx * my] : (uint8_t)NONE_MAT;
+            }
+        }
+}
+
+/* Order-independent checksum: sum_i (cell_i + 1) * splitmix64(i)  (mod 2^64). */
+static inline uint64_t splitmix64(uint64_t x)
+{
+    x += 0x9e3779b97f4a7c15ull;
+    x = (x ^ (x >> 30)) * 0xbf58476d1ce4e5b9ull;
+    x = (x ^ (x >> 27)) * 0x94d049bb133111ebull;
+    return x ^ (x >> 31);
+}
+
+uint64_t oracle_grid_checksum(const uint8_t* cells, uint64_t count)
+{
+    uint64_t s = 0;
+    for (uint64_t i = 0; i < count; i++) s += (uint64_t)(cells[i] + 1u) * splitmix64(i);
+    return s;
+}

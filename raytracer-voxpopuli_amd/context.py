@@ -1,0 +1,145 @@
+"""Python handle on one libvpx_hip.so context (one GPU).  Thin: every call is the C-ABI."""
+import ctypes as C
+
+import numpy as np
+
+from . import abi
+
+
+class Context:
+    def __init__(self, device=0):
+        self.lib = abi.load_library()
+        h = C.c_void_p()
+        rc = self.lib.vpx_create(int(device), C.byref(h))
+        if rc != abi.VPX_OK:
+            raise abi.VpxError(f"vpx_create(device={device}) failed ({rc}): no usable HIP device")
+        self.h = h
+        self.device = device
+        self.scene = None
+
+    # ------------------------------------------------------------------ lifetime
+    def close(self):
+        if self.h:
+            self.lib.vpx_destroy(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _chk(self, rc, what):
+        abi.check(self.lib, self.h, rc, what)
+
+    def set_stream(self, stream_handle):
+        self._chk(self.lib.vpx_set_stream(self.h, C.c_void_p(stream_handle or 0)), "vpx_set_stream")
+
+    def synchronize(self):
+        self._chk(self.lib.vpx_synchronize(self.h), "vpx_synchronize")
+
+    # ------------------------------------------------------------------- scene
+    def load_scene(self, desc, upload_grids=True):
+        if upload_grids:
+            for gid, g in enumerate(desc.grids):
+                g.upload(self.lib, self.h, gid)
+        self._chk(self.lib.vpx_set_volumes(self.h, desc.volumes, len(desc.volumes)), "vpx_set_volumes")
+        self._chk(self.lib.vpx_set_materials(self.h, desc.materials, 256), "vpx_set_materials")
+        pts = (abi.PointLight * max(1, len(desc.points)))(*desc.points)
+        sps = (abi.SpotLight * max(1, len(desc.spots)))(*desc.spots)
+        ars = (abi.AreaLight * max(1, len(desc.areas)))(*desc.areas)
+        self._chk(self.lib.vpx_set_lights(self.h, pts, len(desc.points), sps, len(desc.spots), ars, len(desc.areas),
+                                          C.byref(desc.dir_light)), "vpx_set_lights")
+        sph = (abi.Sphere * max(1, len(desc.spheres)))(*desc.spheres)
+        tri = (abi.Triangle * max(1, len(desc.triangles)))(*desc.triangles)
+        self._chk(self.lib.vpx_set_shapes(self.h, sph, len(desc.spheres), tri, len(desc.triangles)),
+                  "vpx_set_shapes")
+        self.set_camera(desc.camera)
+        self.scene = desc
+
+    def set_camera(self, cam):
+        self._chk(self.lib.vpx_set_camera(self.h, C.byref(cam)), "vpx_set_camera")
+
+    def grid_checksum(self, grid_id=0):
+        out = C.c_uint64()
+        self._chk(self.lib.vpx_grid_checksum(self.h, grid_id, C.byref(out)), "vpx_grid_checksum")
+        return out.value
+
+    # ---------------------------------------------------------------- hot path
+    def render(self, params, accum_ptr, rgb_ptr=None, stats=False):
+        st = abi.Stats() if stats else None
+        self._chk(self.lib.vpx_render(self.h, C.byref(params), C.c_void_p(accum_ptr), C.c_void_p(rgb_ptr or 0),
+                                      C.byref(st) if st is not None else None), "vpx_render")
+        return st
+
+    def render_tiles(self, params, rank, n_ranks, packed_ptr, stats=False, tile=16):
+        st = abi.Stats() if stats else None
+        self._chk(self.lib.vpx_render_tiles(self.h, C.byref(params), tile, tile, rank, n_ranks,
+                                            C.c_void_p(packed_ptr), C.byref(st) if st is not None else None),
+                  "vpx_render_tiles")
+        return st
+
+    def packed_len(self, width, height, n_ranks, tile=16):
+        return int(self.lib.vpx_tiles_packed_len(width, height, tile, tile, n_ranks))
+
+    def composite_tiles(self, params, n_ranks, gathered_ptr, accum_ptr, rgb_ptr=None, tile=16):
+        self._chk(self.lib.vpx_composite_tiles(self.h, C.byref(params), tile, tile, n_ranks, C.c_void_p(gathered_ptr),
+                                               C.c_void_p(accum_ptr), C.c_void_p(rgb_ptr or 0)),
+                  "vpx_composite_tiles")
+
+    def counters(self, reset=False):
+        st = abi.Stats()
+        self._chk(self.lib.vpx_get_counters(self.h, C.byref(st), 1 if reset else 0), "vpx_get_counters")
+        return st
+
+    # ------------------------------------------------------------- unit entries
+    def find_nearest(self, rays):
+        n = len(rays)
+        hits = (abi.Hit * max(1, n))()
+        self._chk(self.lib.vpx_find_nearest(self.h, rays, n, hits), "vpx_find_nearest")
+        return hits
+
+    def is_occluded(self, rays):
+        n = len(rays)
+        occ = np.zeros(max(1, n), np.uint8)
+        self._chk(self.lib.vpx_is_occluded(self.h, rays, n, occ.ctypes.data_as(C.c_void_p)), "vpx_is_occluded")
+        return occ[:n]
+
+    def trace(self, rays, seeds, depth, sky=abi.SKY_DEFAULT, area_samples=3):
+        n = len(rays)
+        seeds = np.ascontiguousarray(seeds, np.uint32)
+        out = np.zeros((max(1, n), 3), np.float32)
+        self._chk(self.lib.vpx_trace(self.h, rays, seeds.ctypes.data_as(C.c_void_p), n, depth, abi.vec3(sky),
+                                     area_samples, out.ctypes.data_as(C.c_void_p)), "vpx_trace")
+        return out[:n]
+
+    def focus_distance(self, width, height):
+        f = C.c_float()
+        self._chk(self.lib.vpx_focus_distance(self.h, width, height, C.byref(f)), "vpx_focus_distance")
+        return f.value
+
+
+def make_rays(origins, directions, tmax=1e34, inside=0):
+    """ctypes array of abi.Ray from (n,3) arrays."""
+    o = np.asarray(origins, np.float32).reshape(-1, 3)
+    d = np.asarray(directions, np.float32).reshape(-1, 3)
+    n = len(o)
+    arr = (abi.Ray * n)()
+    view = np.frombuffer(arr, dtype=np.dtype([("o", "<f4", 3), ("d", "<f4", 3), ("t", "<f4"), ("g", "<u4")]))
+    view["o"] = o
+    view["d"] = d
+    view["t"] = np.broadcast_to(np.asarray(tmax, np.float32), (n,))
+    view["g"] = np.broadcast_to(np.asarray(inside, np.uint32), (n,))
+    return arr
+
+
+def hits_to_numpy(hits, n):
+    dt = np.dtype([("t", "<f4"), ("normal", "<f4", 3), ("vox_index", "<i4"), ("material", "<u4"), ("cells", "<u4"),
+                   ("inside_glass", "<u4")])
+    return np.frombuffer(hits, dtype=dt, count=n).copy()

@@ -1,0 +1,230 @@
+// vpx_host.cpp — host-side helpers of libvpx_hip.so that restate reference HOST code
+// (camera basis, volume transforms, the default material table).  No device work.
+//
+// They exist so a caller that does not link the tmpl8 template (tests, bench, the C++
+// host mirror in host/) builds exactly the inputs the reference would hand the trace
+// path.  Float expressions keep the reference's operand order (built -ffp-contract=off);
+// sinf/cosf are the correctly rounded values (f64 evaluation), as on the device.
+#include <cmath>
+#include <cstring>
+
+#include "../../include/vpx.h"
+
+namespace {
+
+struct v3 {
+    float x, y, z;
+};
+inline v3 add(v3 a, v3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+inline v3 sub(v3 a, v3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+inline v3 mul(v3 a, float s) { return {a.x * s, a.y * s, a.z * s}; }
+inline float dot(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+inline v3 cross(v3 a, v3 b) { return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
+inline v3 normalize(v3 v) {  // tmpl8math.h:2350-2354 (rsqrtf = 1 / sqrtf)
+    const float inv = 1.0f / std::sqrt(dot(v, v));
+    return mul(v, inv);
+}
+inline void put(float* d, v3 v) { d[0] = v.x, d[1] = v.y, d[2] = v.z; }
+
+// mat4 (tmpl8math.h:2592-2873): row-major cells, default identity.
+struct mat4 {
+    float c[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+};
+mat4 matmul(const mat4& a, const mat4& b) {  // operator*(mat4, mat4), tmpl8math.cpp:281-294
+    mat4 r;
+    for (int i = 0; i < 16; i += 4)
+        for (int j = 0; j < 4; ++j)
+            r.c[i + j] = (a.c[i + 0] * b.c[j + 0]) + (a.c[i + 1] * b.c[j + 4]) + (a.c[i + 2] * b.c[j + 8]) +
+                         (a.c[i + 3] * b.c[j + 12]);
+    return r;
+}
+mat4 translate(v3 p) {
+    mat4 r;
+    r.c[3] = p.x, r.c[7] = p.y, r.c[11] = p.z;
+    return r;
+}
+mat4 scale(v3 s) {
+    mat4 r;
+    r.c[0] = s.x, r.c[5] = s.y, r.c[10] = s.z;
+    return r;
+}
+
+// 4x4 inverse by cofactors (the MESA gluInvertMatrix formulation that mat4::Inverted
+// uses, tmpl8math.h:2828-2873), products and sums evaluated left to right.
+mat4 inverted(const mat4& m) {
+    const float* c = m.c;
+    float inv[16];
+    inv[0] = c[5] * c[10] * c[15] - c[5] * c[11] * c[14] - c[9] * c[6] * c[15] + c[9] * c[7] * c[14] +
+             c[13] * c[6] * c[11] - c[13] * c[7] * c[10];
+    inv[1] = -c[1] * c[10] * c[15] + c[1] * c[11] * c[14] + c[9] * c[2] * c[15] - c[9] * c[3] * c[14] -
+             c[13] * c[2] * c[11] + c[13] * c[3] * c[10];
+    inv[2] = c[1] * c[6] * c[15] - c[1] * c[7] * c[14] - c[5] * c[2] * c[15] + c[5] * c[3] * c[14] +
+             c[13] * c[2] * c[7] - c[13] * c[3] * c[6];
+    inv[3] = -c[1] * c[6] * c[11] + c[1] * c[7] * c[10] + c[5] * c[2] * c[11] - c[5] * c[3] * c[10] -
+             c[9] * c[2] * c[7] + c[9] * c[3] * c[6];
+    inv[4] = -c[4] * c[10] * c[15] + c[4] * c[11] * c[14] + c[8] * c[6] * c[15] - c[8] * c[7] * c[14] -
+             c[12] * c[6] * c[11] + c[12] * c[7] * c[10];
+    inv[5] = c[0] * c[10] * c[15] - c[0] * c[11] * c[14] - c[8] * c[2] * c[15] + c[8] * c[3] * c[14] +
+             c[12] * c[2] * c[11] - c[12] * c[3] * c[10];
+    inv[6] = -c[0] * c[6] * c[15] + c[0] * c[7] * c[14] + c[4] * c[2] * c[15] - c[4] * c[3] * c[14] -
+             c[12] * c[2] * c[7] + c[12] * c[3] * c[6];
+    inv[7] = c[0] * c[6] * c[11] - c[0] * c[7] * c[10] - c[4] * c[2] * c[11] + c[4] * c[3] * c[10] +
+             c[8] * c[2] * c[7] - c[8] * c[3] * c[6];
+    inv[8] = c[4] * c[9] * c[15] - c[4] * c[11] * c[13] - c[8] * c[5] * c[15] + c[8] * c[7] * c[13] +
+             c[12] * c[5] * c[11] - c[12] * c[7] * c[9];
+    inv[9] = -c[0] * c[9] * c[15] + c[0] * c[11] * c[13] + c[8] * c[1] * c[15] - c[8] * c[3] * c[13] -
+             c[12] * c[1] * c[11] + c[12] * c[3] * c[9];
+    inv[10] = c[0] * c[5] * c[15] - c[0] * c[7] * c[13] - c[4] * c[1] * c[15] + c[4] * c[3] * c[13] +
+              c[12] * c[1] * c[7] - c[12] * c[3] * c[5];
+    inv[11] = -c[0] * c[5] * c[11] + c[0] * c[7] * c[9] + c[4] * c[1] * c[11] - c[4] * c[3] * c[9] -
+              c[8] * c[1] * c[7] + c[8] * c[3] * c[5];
+    inv[12] = -c[4] * c[9] * c[14] + c[4] * c[10] * c[13] + c[8] * c[5] * c[14] - c[8] * c[6] * c[13] -
+              c[12] * c[5] * c[10] + c[12] * c[6] * c[9];
+    inv[13] = c[0] * c[9] * c[14] - c[0] * c[10] * c[13] - c[8] * c[1] * c[14] + c[8] * c[2] * c[13] +
+              c[12] * c[1] * c[10] - c[12] * c[2] * c[9];
+    inv[14] = -c[0] * c[5] * c[14] + c[0] * c[6] * c[13] + c[4] * c[1] * c[14] - c[4] * c[2] * c[13] -
+              c[12] * c[1] * c[6] + c[12] * c[2] * c[5];
+    inv[15] = c[0] * c[5] * c[10] - c[0] * c[6] * c[9] - c[4] * c[1] * c[10] + c[4] * c[2] * c[9] +
+              c[8] * c[1] * c[6] - c[8] * c[2] * c[5];
+    const float det = c[0] * inv[0] + c[1] * inv[4] + c[2] * inv[8] + c[3] * inv[12];
+    mat4 r;
+    if (det != 0) {
+        const float invdet = 1.0f / det;
+        for (int i = 0; i < 16; i++) r.c[i] = inv[i] * invdet;
+    }
+    return r;
+}
+
+// quat (tmpl8math.h:2951-3066): fromAxisAngle, Hamilton product, toMatrix.
+struct quat {
+    float w = 1, x = 0, y = 0, z = 0;
+};
+quat from_axis_angle(v3 axis, float theta) {
+    quat q;
+    q.w = (float)std::cos((double)(theta / 2));
+    const float s = (float)std::sin((double)(theta / 2));
+    q.x = axis.x * s, q.y = axis.y * s, q.z = axis.z * s;
+    return q;
+}
+quat qmul(const quat& a, const quat& q) {
+    quat r;
+    r.w = a.w * q.w - a.x * q.x - a.y * q.y - a.z * q.z;
+    r.x = a.w * q.x + a.x * q.w + a.y * q.z - a.z * q.y;
+    r.y = a.w * q.y - a.x * q.z + a.y * q.w + a.z * q.x;
+    r.z = a.w * q.z + a.x * q.y - a.y * q.x + a.z * q.w;
+    return r;
+}
+mat4 to_matrix(const quat& q) {
+    const float w = q.w, x = q.x, y = q.y, z = q.z;
+    mat4 m;
+    m.c[0] = 1 - 2 * y * y - 2 * z * z;
+    m.c[1] = 2 * x * y - 2 * w * z, m.c[2] = 2 * x * z + 2 * w * y, m.c[4] = 2 * x * y + 2 * w * z;
+    m.c[5] = 1 - 2 * x * x - 2 * z * z;
+    m.c[6] = 2 * y * z - 2 * w * x, m.c[8] = 2 * x * z - 2 * w * y, m.c[9] = 2 * y * z + 2 * w * x;
+    m.c[10] = 1 - 2 * x * x - 2 * y * y;
+    return m;
+}
+
+}  // namespace
+
+extern "C" {
+
+// Camera basis as Camera::HandleInput(0) leaves it with no key held (camera.h:113-181).
+int vpx_camera_look_at(const float pos[3], const float target[3], uint32_t width, uint32_t height,
+                       vpx_camera* out) {
+    if (!pos || !target || !out || !width || !height) return VPX_E_INVALID;
+    const v3 cam = {pos[0], pos[1], pos[2]};
+    v3 tgt = {target[0], target[1], target[2]};
+    const v3 tmp_up = {0, 1, 0};
+    const float aspect = (float)width / (float)height;  // ASPECT, camera.h:183
+    v3 ahead = normalize(sub(tgt, cam));
+    v3 right = normalize(cross(tmp_up, ahead));
+    v3 up = normalize(cross(ahead, right));
+    ahead = normalize(sub(tgt, cam));
+    right = normalize(cross(tmp_up, ahead));
+    up = normalize(cross(ahead, right));
+    tgt = add(cam, ahead);
+    ahead = normalize(sub(tgt, cam));
+    up = normalize(cross(ahead, right));
+    right = normalize(cross(up, ahead));
+    const v3 base = add(cam, mul(ahead, 2.0f));
+    put(out->cam_pos, cam);
+    put(out->top_left, add(sub(base, mul(right, aspect)), up));
+    put(out->top_right, add(add(base, mul(right, aspect)), up));
+    put(out->bottom_left, sub(sub(base, mul(right, aspect)), up));
+    put(out->right, right);
+    put(out->up, up);
+    out->focal_distance = 1.0f;  // Camera::focalDistance default, camera.h:189
+    out->defocus_jitter = 2.0f;  // Camera::defocusJitter default, camera.h:191
+    return VPX_OK;
+}
+
+// Scene(position, N) cube + Scene::SetTransform(rotation) with Scene::scale = scale and
+// Scene::position (the member, distinct from the cube position) = 0
+// (template/scene.cpp:213-217, 373-405, 431-445).
+int vpx_volume_set_transform(const float position[3], const float scl[3], const float rotation[3],
+                             vpx_volume* out) {
+    if (!position || !scl || !rotation || !out) return VPX_E_INVALID;
+    const v3 b0 = {position[0], position[1], position[2]};
+    const v3 b1 = add(b0, v3{1, 1, 1});
+    const v3 center = mul(add(b0, b1), 0.5f);
+    const mat4 to_pivot = translate(add(center, v3{0, 0, 0}));
+    const mat4 back = translate(v3{-center.x, -center.y, -center.z});
+    const mat4 s = scale(v3{scl[0], scl[1], scl[2]});
+    quat q = from_axis_angle(v3{1, 0, 0}, rotation[0]);
+    q = qmul(from_axis_angle(v3{0, 1, 0}, rotation[1]), q);
+    q = qmul(from_axis_angle(v3{0, 0, 1}, rotation[2]), q);
+    const mat4 rot = to_matrix(q);
+    const mat4 m = matmul(matmul(matmul(to_pivot, s), rot), back);
+    const mat4 inv = inverted(matmul(matmul(matmul(to_pivot, rot), s), back));
+    std::memcpy(out->matrix, m.c, sizeof(m.c));
+    std::memcpy(out->inv_matrix, inv.c, sizeof(inv.c));
+    put(out->b0, b0);
+    put(out->b1, b1);
+    return VPX_OK;
+}
+
+// Renderer::MaterialSetUp (renderer.cpp:357-443); entries 16..255 white, roughness 1.
+int vpx_default_materials(vpx_material* out) {
+    if (!out) return VPX_E_INVALID;
+    auto mk = [](float r, float g, float b, float rough) {
+        vpx_material m{};
+        m.albedo[0] = r, m.albedo[1] = g, m.albedo[2] = b;
+        m.roughness = rough;
+        m.emissive = 0.0f;
+        m.ior = 1.5f;  // Material::IOR default, Material.h:11
+        return m;
+    };
+    for (int i = 0; i < VPX_NUM_MATERIALS; ++i) out[i] = mk(1, 1, 1, 1.0f);
+    out[0] = mk(1, 1, 1, 1.0f);      // NON_METAL_WHITE
+    out[1] = mk(1, 0, 0, 0.6f);      // NON_METAL_RED
+    out[2] = mk(0, 0, 1, 0.25f);     // NON_METAL_BLUE
+    out[3] = mk(0, 1, 0, 0.0f);      // NON_METAL_GREEN
+    out[4] = mk(1, .6f, .8f, 0.3f);  // NON_METAL_PINK (partialMetal)
+    out[5] = mk(1, 1, 1, 1.0f);      // METAL_HIGH
+    out[6] = mk(0, 1, 1, 0.5f);      // METAL_MID
+    out[7] = mk(0.9f, 0.9f, 0.9f, 0.01f);  // METAL_LOW
+    out[8] = mk(1, 0.5f, 1, 1.0f);   // GLASS
+    out[8].ior = 1.45f;
+    const float smoke_em[6] = {3.0f, 8.0f, 12.0f, 15.0f, 16.0f, 22.0f};
+    for (int i = 0; i < 6; ++i) {    // SMOKE_LOW_DENSITY .. SMOKE_PLAYER
+        out[9 + i] = mk(1.0f, 0.7f, 1.0f, 1.0f);
+        out[9 + i].ior = 1.0f;
+        out[9 + i].emissive = smoke_em[i];
+    }
+    out[14].albedo[0] = out[14].albedo[1] = out[14].albedo[2] = 0.0f;  // smoke5 float3{0}
+    out[15] = mk(1.0f, 0.7f, 1.0f, 1.0f);  // EMISSIVE
+    out[15].emissive = 5.0f;
+    return VPX_OK;
+}
+
+}  // extern "C"
+
+// Fixed POD layouts of the ABI (mirrored by raytracer-voxpopuli_amd/abi.py STRUCT_SIZES).
+static_assert(sizeof(vpx_volume) == 160, "vpx_volume layout");
+static_assert(sizeof(vpx_material) == 32, "vpx_material layout");
+static_assert(sizeof(vpx_point_light) == 24 && sizeof(vpx_spot_light) == 40, "light layout");
+static_assert(sizeof(vpx_area_light) == 32 && sizeof(vpx_dir_light) == 24, "light layout");
+static_assert(sizeof(vpx_sphere) == 32 && sizeof(vpx_triangle) == 64, "shape layout");
+static_assert(sizeof(vpx_camera) == 80 && sizeof(vpx_frame_params) == 48, "camera/frame layout");
+static_assert(sizeof(vpx_ray) == 32 && sizeof(vpx_hit) == 32 && sizeof(vpx_stats) == 40, "ray/hit/stats layout");

@@ -1,0 +1,739 @@
+// vpx_trace.hpp — device-side voxel ray-trace path for gfx950 (CDNA4).
+//
+// One ray per lane.  The reference's recursive Renderer::Trace (renderer.cpp:1076-1328)
+// is a single chain (every material makes at most one recursive call), so it runs here
+// as a loop that records one (a, b, form) combine record per level and folds them
+// bottom-up at the end — the same rounding order as the recursion, so results are
+// bit-identical to the CPU restatement, not merely close.
+//
+// Float semantics match the reference as restated in oracle/vpx_oracle.c: the library is
+// built with -ffp-contract=off and f32 denormal flush (template/template.cpp:130 sets
+// FTZ|DAZ); division and sqrt are correctly rounded (hipcc default); std::min/std::max
+// are spelled as the exact ternaries; sin/cos/pow/exp are the correctly rounded f32
+// values obtained through f64.  No approximations (rcp/rsq) are used anywhere.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/vpx.h"
+
+namespace vpx {
+
+constexpr uint32_t kNone = 255u;
+constexpr float kPi = 3.14159265358979323846264f;  // common.h:8
+constexpr float kBig = 1e34f;
+constexpr int kMaxLevels = 16;                     // max_bounces <= 14 -> 15 levels
+
+// ----------------------------------------------------------------------- device view
+struct DevGrid {
+    const uint8_t* cells;
+    uint32_t n;
+    uint32_t pad;
+};
+
+struct SceneView {
+    const DevGrid* grids;
+    const vpx_volume* volumes;
+    const vpx_material* materials;
+    const vpx_point_light* points;
+    const vpx_spot_light* spots;
+    const vpx_area_light* areas;
+    const vpx_sphere* spheres;
+    const vpx_triangle* triangles;
+    uint32_t num_volumes, num_points, num_spots, num_areas, num_spheres, num_triangles;
+    vpx_dir_light dir;
+    float sky[3];
+    int32_t area_samples;
+};
+
+struct f3 {
+    float x, y, z;
+};
+
+__device__ __forceinline__ f3 mk(float x, float y, float z) { return f3{x, y, z}; }
+__device__ __forceinline__ f3 ld3(const float* p) { return f3{p[0], p[1], p[2]}; }
+__device__ __forceinline__ f3 operator+(f3 a, f3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ f3 operator-(f3 a, f3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ f3 operator*(f3 a, f3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
+__device__ __forceinline__ f3 operator/(f3 a, f3 b) { return mk(a.x / b.x, a.y / b.y, a.z / b.z); }
+__device__ __forceinline__ f3 operator*(f3 a, float s) { return mk(a.x * s, a.y * s, a.z * s); }
+__device__ __forceinline__ f3 operator/(f3 a, float s) { return mk(a.x / s, a.y / s, a.z / s); }
+__device__ __forceinline__ f3 operator-(f3 a) { return mk(-a.x, -a.y, -a.z); }
+__device__ __forceinline__ float dot(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ float length(f3 a) { return __fsqrt_rn(dot(a, a)); }
+__device__ __forceinline__ f3 normalize(f3 v) {
+    const float inv = __fdiv_rn(1.0f, __fsqrt_rn(dot(v, v)));
+    return v * inv;
+}
+__device__ __forceinline__ f3 cross(f3 a, f3 b) {
+    return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+// std::min / std::max exactly (first operand returned on ties / NaN).
+__device__ __forceinline__ float smin(float a, float b) { return (b < a) ? b : a; }
+__device__ __forceinline__ float smax(float a, float b) { return (a < b) ? b : a; }
+
+// static_cast<int>(float) as the x86 reference evaluates it (cvttss2si: INT_MIN when
+// out of range or NaN); v_cvt_i32_f32 would saturate instead.
+__device__ __forceinline__ int trunc_i32(float f) {
+    return (f > -2147483904.0f && f < 2147483648.0f) ? (int)f : (int)0x80000000u;
+}
+__device__ __forceinline__ float sign_of(float d) { return (float)(__float_as_uint(d) >> 31); }
+__device__ __forceinline__ f3 dsign(f3 d) { return mk(sign_of(d.x), sign_of(d.y), sign_of(d.z)); }
+
+__device__ __forceinline__ float cr_sin(float x) { return (float)sin((double)x); }
+__device__ __forceinline__ float cr_cos(float x) { return (float)cos((double)x); }
+__device__ __forceinline__ float cr_exp(float x) { return (float)exp((double)x); }
+__device__ __forceinline__ float cr_pow5(float x) { return (float)pow((double)x, 5.0); }
+
+// ---------------------------------------------------------------------------- RNG
+// WangHash / xorshift32 / RandomFloat: template/tmpl8math.cpp:20-27, 119-133.
+__host__ __device__ __forceinline__ uint32_t wang_hash(uint32_t s) {
+    s = (s ^ 61u) ^ (s >> 16);
+    s *= 9u;
+    s = s ^ (s >> 4);
+    s *= 0x27d4eb2du;
+    s = s ^ (s >> 15);
+    return s;
+}
+__host__ __device__ __forceinline__ uint32_t pixel_seed(uint32_t base, uint32_t frame, uint32_t w,
+                                                        uint32_t h, uint32_t x, uint32_t y) {
+    const uint32_t k = base + frame * (w * h) + y * w + x;
+    return 0x12345678u + wang_hash((k + 1u) * 17u);
+}
+
+struct Rng {
+    uint32_t s;
+    __device__ __forceinline__ float next() {
+        s ^= s << 13;
+        s ^= s >> 17;
+        s ^= s << 5;
+        return (float)s * 2.3283064365387e-10f;
+    }
+};
+
+// --------------------------------------------------------------------- transforms
+// TransformPosition_SSEM / TransformVector_SSEM (tmpl8math.cpp:369-402): pairwise sums.
+__device__ __forceinline__ f3 xform_pos_ssem(f3 a, const float* m) {
+    return mk((a.x * m[0] + a.y * m[1]) + (a.z * m[2] + m[3]),
+              (a.x * m[4] + a.y * m[5]) + (a.z * m[6] + m[7]),
+              (a.x * m[8] + a.y * m[9]) + (a.z * m[10] + m[11]));
+}
+__device__ __forceinline__ f3 xform_vec_ssem(f3 a, const float* m) {
+    return mk((a.x * m[0] + a.y * m[1]) + a.z * m[2], (a.x * m[4] + a.y * m[5]) + a.z * m[6],
+              (a.x * m[8] + a.y * m[9]) + a.z * m[10]);
+}
+// TransformPosition / TransformVector (tmpl8math.cpp:345-353): left-to-right sums.
+__device__ __forceinline__ f3 xform_pos(f3 a, const float* m) {
+    return mk(m[0] * a.x + m[1] * a.y + m[2] * a.z + m[3] * 1.0f,
+              m[4] * a.x + m[5] * a.y + m[6] * a.z + m[7] * 1.0f,
+              m[8] * a.x + m[9] * a.y + m[10] * a.z + m[11] * 1.0f);
+}
+__device__ __forceinline__ f3 xform_vec(f3 a, const float* m) {
+    return mk(m[0] * a.x + m[1] * a.y + m[2] * a.z + m[3] * 0.0f,
+              m[4] * a.x + m[5] * a.y + m[6] * a.z + m[7] * 0.0f,
+              m[8] * a.x + m[9] * a.y + m[10] * a.z + m[11] * 0.0f);
+}
+
+// OffsetRay (tmpl8math.cpp:473-487): integer ULP nudge, float nudge near the origin.
+__device__ __forceinline__ float offset1(float p, float n) {
+    const int o = trunc_i32(256.0f * n);
+    const float pi = __uint_as_float(__float_as_uint(p) + (uint32_t)((p < 0) ? -o : o));
+    return fabsf(p) < (1.0f / 32.0f) ? p + (1.0f / 65536.0f) * n : pi;
+}
+__device__ __forceinline__ f3 offset_ray(f3 p, f3 n) {
+    return mk(offset1(p.x, n.x), offset1(p.y, n.y), offset1(p.z, n.z));
+}
+
+// --------------------------------------------------------------------------- rays
+// World-space ray.  Dsign and rD are always derivable from D where the reference
+// reads them (they are recomputed per volume in object space), so only O/D are kept.
+struct Ray {
+    f3 O, D, N;
+    float t;
+    uint32_t mat;
+    bool inside;
+};
+
+// Ray::Ray(origin, direction), template/scene.cpp:83-93.
+__device__ __forceinline__ Ray make_ray(f3 o, f3 dir) {
+    Ray r;
+    r.O = o;
+    r.D = normalize(dir);
+    r.N = mk(0.f, 0.f, 0.f);
+    r.t = kBig;
+    r.mat = kNone;
+    r.inside = false;
+    return r;
+}
+__device__ __forceinline__ f3 ray_point(const Ray& r) { return r.O + r.D * r.t; }
+
+// Object-space ray inside one volume visit (Ray fields after the per-volume transform).
+struct ORay {
+    f3 O, D, rD;
+};
+
+// ------------------------------------------------------------------------ the DDA
+struct Dda {
+    uint32_t X, Y, Z;
+    int sx, sy, sz;
+    float t;
+    f3 tdelta, tmax;
+};
+
+// Cube::Intersect, template/scene.cpp:166-202.
+__device__ __forceinline__ float cube_intersect(f3 b0, f3 b1, const ORay& r) {
+    const bool sgx = r.D.x < 0, sgy = r.D.y < 0, sgz = r.D.z < 0;
+    float tmin_x = ((sgx ? b1.x : b0.x) - r.O.x) * r.rD.x;
+    float tmax_x = ((sgx ? b0.x : b1.x) - r.O.x) * r.rD.x;
+    const float tmin_y = ((sgy ? b1.y : b0.y) - r.O.y) * r.rD.y;
+    const float tmax_y = ((sgy ? b0.y : b1.y) - r.O.y) * r.rD.y;
+    if (tmin_x > tmax_y || tmin_y > tmax_x) return kBig;
+    tmin_x = smax(tmin_x, tmin_y);
+    tmax_x = smin(tmax_x, tmax_y);
+    const float tmin_z = ((sgz ? b1.z : b0.z) - r.O.z) * r.rD.z;
+    const float tmax_z = ((sgz ? b0.z : b1.z) - r.O.z) * r.rD.z;
+    if (tmin_x > tmax_z || tmin_z > tmax_x) return kBig;
+    tmin_x = smax(tmin_x, tmin_z);
+    return tmin_x > 0 ? tmin_x : kBig;
+}
+
+// Scene::Setup3DDDA, template/scene.cpp:719-749.
+__device__ __forceinline__ bool dda_setup(const vpx_volume& vol, uint32_t n, const ORay& r, Dda& s) {
+    const f3 b0 = ld3(vol.b0), b1 = ld3(vol.b1);
+    s.t = 0;
+    const bool contains = r.O.x >= b0.x && r.O.y >= b0.y && r.O.z >= b0.z && r.O.x <= b1.x &&
+                          r.O.y <= b1.y && r.O.z <= b1.z;
+    if (!contains) {
+        s.t = cube_intersect(b0, b1, r);
+        if (s.t > 1e33f) return false;
+    }
+    const f3 vmax = b1 - b0;
+    const float g = (float)n;
+    const float cell = __fdiv_rn(1.0f, g);
+    const f3 ds = dsign(r.D);
+    s.sx = trunc_i32(1.0f - ds.x * 2.0f);
+    s.sy = trunc_i32(1.0f - ds.y * 2.0f);
+    s.sz = trunc_i32(1.0f - ds.z * 2.0f);
+    const f3 pos = (((r.O - b0) + r.D * (s.t + 0.00005f)) * g) / vmax;
+    const f3 planes = (mk(ceilf(pos.x), ceilf(pos.y), ceilf(pos.z)) - ds) * cell;
+    const int hi = (int)(n - 1);
+    int px = trunc_i32(pos.x), py = trunc_i32(pos.y), pz = trunc_i32(pos.z);
+    px = px < 0 ? 0 : (px > hi ? hi : px);
+    py = py < 0 ? 0 : (py > hi ? hi : py);
+    pz = pz < 0 ? 0 : (pz > hi ? hi : pz);
+    s.X = (uint32_t)px;
+    s.Y = (uint32_t)py;
+    s.Z = (uint32_t)pz;
+    s.tdelta = mk(cell * (float)s.sx, cell * (float)s.sy, cell * (float)s.sz) * r.rD;
+    s.tmax = ((planes * vmax) - (r.O - b0)) * r.rD;
+    return true;
+}
+
+// Ray::GetNormalVoxel, template/scene.cpp:121-148 (object-space O/D/t, Dsign of D).
+__device__ __forceinline__ f3 normal_voxel(const ORay& r, float t, uint32_t n, const float* matrix) {
+    const f3 i1 = (r.O + r.D * t) * (float)n;
+    const f3 fg = mk(i1.x - floorf(i1.x), i1.y - floorf(i1.y), i1.z - floorf(i1.z));
+    const f3 d = mk(smin(fg.x, 1.0f - fg.x), smin(fg.y, 1.0f - fg.y), smin(fg.z, 1.0f - fg.z));
+    const float mind = smin(smin(d.x, d.y), d.z);
+    const f3 sg = dsign(r.D) * 2.0f - mk(1.f, 1.f, 1.f);
+    const f3 nn = mk(mind == d.x ? sg.x : 0.0f, mind == d.y ? sg.y : 0.0f, mind == d.z ? sg.z : 0.0f);
+    return normalize(xform_vec(nn, matrix));
+}
+
+// Walk modes (all share the stepping of scene.cpp:773-802).
+enum WalkMode { kNearest = 0, kGlassExit = 1, kSmokeExit = 2, kOcclusion = 3 };
+
+struct WalkResult {
+    bool hit;     // nearest: found a cell with t < bound; exits: left the material; occl: occluded
+    float t;      // hit t (nearest / exits) or last s.t (exits leaving the grid)
+    uint32_t cell;
+};
+
+// The Amanatides-Woo march.  `bound` is Ray::t on entry.  Loads one byte per visited
+// cell (x + y*N + z*N^2, 64-bit index) and counts it in `cells`.
+template <int MODE>
+__device__ __forceinline__ WalkResult dda_walk(const DevGrid& g, Dda s, float bound, uint32_t& cells) {
+    WalkResult res{false, s.t, kNone};
+    const uint64_t n = g.n;
+    const uint64_t nn = n * n;
+    const uint8_t* __restrict__ grid = g.cells;
+    for (;;) {
+        if (MODE == kNearest || MODE == kOcclusion) {
+            if (!(s.t < bound)) break;
+        }
+        const uint32_t cell = grid[(uint64_t)s.X + (uint64_t)s.Y * n + (uint64_t)s.Z * nn];
+        ++cells;
+        if (MODE == kNearest) {
+            if (cell != kNone && s.t < bound) {
+                res.hit = true, res.t = s.t, res.cell = cell;
+                return res;
+            }
+        } else if (MODE == kOcclusion) {
+            if (cell != kNone) {
+                res.hit = s.t < bound;
+                return res;
+            }
+        } else {
+            const bool leave = (MODE == kGlassExit) ? (cell != VPX_MAT_GLASS)
+                                                    : (cell > VPX_MAT_SMOKE_PLAYER || cell < VPX_MAT_SMOKE_LOW_DENSITY);
+            if (leave) {
+                res.hit = true, res.t = s.t, res.cell = cell;
+                return res;
+            }
+        }
+        // Axis choice: x<y ? (x<z ? x : z) : (y<z ? y : z), strict compares (scene.cpp:773-802).
+        const bool xy = s.tmax.x < s.tmax.y, xz = s.tmax.x < s.tmax.z, yz = s.tmax.y < s.tmax.z;
+        const int axis = xy ? (xz ? 0 : 2) : (yz ? 1 : 2);
+        if (axis == 0) {
+            if (MODE != kOcclusion) s.t = s.tmax.x;
+            s.X += (uint32_t)s.sx;
+            if (s.X >= g.n) break;
+            if (MODE == kOcclusion) s.t = s.tmax.x;
+            s.tmax.x += s.tdelta.x;
+        } else if (axis == 1) {
+            if (MODE != kOcclusion) s.t = s.tmax.y;
+            s.Y += (uint32_t)s.sy;
+            if (s.Y >= g.n) break;
+            if (MODE == kOcclusion) s.t = s.tmax.y;
+            s.tmax.y += s.tdelta.y;
+        } else {
+            if (MODE != kOcclusion) s.t = s.tmax.z;
+            s.Z += (uint32_t)s.sz;
+            if (s.Z >= g.n) break;
+            if (MODE == kOcclusion) s.t = s.tmax.z;
+            s.tmax.z += s.tdelta.z;
+        }
+    }
+    res.t = s.t;  // exits: Scene::FindMaterialExit/FindSmokeExit set ray.t = s.t on leaving
+    return res;
+}
+
+// ------------------------------------------------------------------------ shapes
+// Sphere::Hit / IsHit, Triangle::Hit / IsHit — src/BVH/Shapes.h:12-139.
+__device__ __forceinline__ void sphere_hit(const vpx_sphere& sp, Ray& r) {
+    const f3 c = ld3(sp.center);
+    const f3 to = r.O - c;
+    const float b = dot(to, r.D);
+    const float cc = dot(to, to) - (sp.radius * sp.radius);
+    const float disc = b * b - cc;
+    if (cc > 0.0f && b > 0.0f) return;
+    if (disc < 0) return;
+    const float len = -b - __fsqrt_rn(disc);
+    if (len > r.t) return;
+    if (len < 0) return;
+    const f3 ip = r.O + r.D * len;
+    const f3 outn = (ip - c) / sp.radius;
+    const bool outside = dot(r.D, outn) < 0;
+    r.N = outside ? outn : -outn;
+    r.inside = !outside;
+    r.t = len;
+    r.mat = sp.material;
+}
+__device__ __forceinline__ bool sphere_is_hit(const vpx_sphere& sp, const Ray& r) {
+    const f3 c = ld3(sp.center);
+    const f3 to = r.O - c;
+    const float b = dot(to, r.D);
+    const float cc = dot(to, to) - (sp.radius * sp.radius);
+    const float disc = b * b - cc;
+    if (cc > 0.0f && b > 0.0f) return false;
+    if (disc < 0) return false;
+    const float len = -b - __fsqrt_rn(disc);
+    if (len < 0) return false;
+    if (len > r.t) return false;
+    return true;
+}
+__device__ __forceinline__ bool tri_core(const vpx_triangle& tr, const Ray& r, float& t, f3& e1o, f3& e2o) {
+    const f3 pos = ld3(tr.position);
+    const f3 p1 = pos + ld3(tr.v0), p2 = pos + ld3(tr.v1), p3 = pos + ld3(tr.v2);
+    const f3 e1 = p2 - p1, e2 = p3 - p1;
+    const f3 h = cross(r.D, e2);
+    const float a = dot(e1, h);
+    if (a > -0.0001f && a < 0.0001f) return false;
+    const float f = __fdiv_rn(1.0f, a);
+    const f3 s = r.O - p1;
+    const float u = f * dot(s, h);
+    if (u < 0 || u > 1) return false;
+    const f3 q = cross(s, e1);
+    const float v = f * dot(r.D, q);
+    if (v < 0 || u + v > 1) return false;
+    t = f * dot(e2, q);
+    e1o = e1;
+    e2o = e2;
+    return true;
+}
+__device__ __forceinline__ void tri_hit(const vpx_triangle& tr, Ray& r) {
+    float t;
+    f3 e1, e2;
+    if (!tri_core(tr, r, t, e1, e2)) return;
+    if (t > 0.0001f && r.t > t) {
+        r.t = t;
+        r.mat = tr.material;
+        const f3 nrm = normalize(cross(e1, e2));
+        r.N = dot(r.D, nrm) < 0 ? nrm : -nrm;
+    }
+}
+__device__ __forceinline__ bool tri_is_hit(const vpx_triangle& tr, const Ray& r) {
+    float t;
+    f3 e1, e2;
+    if (!tri_core(tr, r, t, e1, e2)) return false;
+    if (t < 0.0001f) return false;
+    if (t > r.t) return false;
+    return true;
+}
+
+// ---------------------------------------------------------------- renderer level
+struct Counters {
+    uint32_t cells;
+    uint32_t shadow;
+    uint32_t nearest;
+};
+
+// Renderer::FindNearest, renderer.cpp:946-1018.  Linear loop over the volumes with the
+// SSE transforms; a later volume wins only with a strictly smaller t (ties -> lowest index).
+__device__ __forceinline__ int32_t find_nearest(const SceneView& sv, Ray& r, Counters& k) {
+    int32_t vox = -2;
+    ++k.nearest;
+    for (uint32_t i = 0; i < sv.num_volumes; ++i) {
+        const vpx_volume& vol = sv.volumes[i];
+        ORay o;
+        o.O = xform_pos_ssem(r.O, vol.inv_matrix);
+        o.D = xform_vec_ssem(r.D, vol.inv_matrix);
+        o.rD = mk(__fdiv_rn(1.0f, o.D.x), __fdiv_rn(1.0f, o.D.y), __fdiv_rn(1.0f, o.D.z));
+        const DevGrid g = sv.grids[vol.grid_id];
+        Dda s;
+        if (!dda_setup(vol, g.n, o, s)) continue;
+        const WalkResult w = dda_walk<kNearest>(g, s, r.t, k.cells);
+        if (w.hit) {
+            r.t = w.t;
+            r.N = normal_voxel(o, w.t, g.n, vol.matrix);
+            r.mat = w.cell;
+            vox = (int32_t)i;
+        }
+    }
+    if (sv.num_spheres | sv.num_triangles) {
+        Ray sh = make_ray(r.O, r.D);
+        for (uint32_t i = 0; i < sv.num_spheres; ++i) sphere_hit(sv.spheres[i], sh);
+        for (uint32_t i = 0; i < sv.num_triangles; ++i) tri_hit(sv.triangles[i], sh);
+        if (r.t > sh.t) {
+            r.t = sh.t;
+            r.mat = sh.mat;
+            r.N = sh.N;
+            r.inside = sh.inside;
+            vox = -1;
+        }
+    }
+    return vox;
+}
+
+// Renderer::IsOccluded, renderer.cpp:209-243 (scalar transforms, exact 1/D).
+__device__ __forceinline__ bool is_occluded(const SceneView& sv, const Ray& r, Counters& k) {
+    for (uint32_t i = 0; i < sv.num_volumes; ++i) {
+        const vpx_volume& vol = sv.volumes[i];
+        ORay o;
+        o.O = xform_pos(r.O, vol.inv_matrix);
+        o.D = xform_vec(r.D, vol.inv_matrix);
+        o.rD = mk(__fdiv_rn(1.0f, o.D.x), __fdiv_rn(1.0f, o.D.y), __fdiv_rn(1.0f, o.D.z));
+        const DevGrid g = sv.grids[vol.grid_id];
+        Dda s;
+        if (!dda_setup(vol, g.n, o, s)) continue;
+        if (dda_walk<kOcclusion>(g, s, r.t, k.cells).hit) return true;
+    }
+    for (uint32_t i = 0; i < sv.num_spheres; ++i)
+        if (sphere_is_hit(sv.spheres[i], r)) return true;
+    for (uint32_t i = 0; i < sv.num_triangles; ++i)
+        if (tri_is_hit(sv.triangles[i], r)) return true;
+    return false;
+}
+
+__device__ __forceinline__ bool shadow(const SceneView& sv, const Ray& r, Counters& k) {
+    ++k.shadow;
+    return is_occluded(sv, r, k);
+}
+
+__device__ __forceinline__ f3 albedo(const SceneView& sv, uint32_t m) { return ld3(sv.materials[m].albedo); }
+
+// RandomDirection (tmpl8math.cpp:76-93), RandomSphereSample (tmpl8math.h:2502-2511),
+// DiffuseReflection (tmpl8math.h:2518-2528; argument order left to right).
+__device__ __forceinline__ f3 random_direction(Rng& g) {
+    for (;;) {
+        const float a = g.next(), b = g.next(), c = g.next();
+        const f3 p = mk(a, b, c);
+        if (dot(p, p) < 1) return normalize(p);
+    }
+}
+__device__ __forceinline__ f3 random_sphere_sample(Rng& g) {
+    const float theta = g.next() * 2.0f * kPi;
+    const float phi = g.next() * kPi;
+    const float r = g.next();
+    const float sp = cr_sin(phi);
+    return mk(r * sp * cr_cos(theta), r * sp * cr_sin(theta), r * cr_cos(phi));
+}
+__device__ __forceinline__ f3 diffuse_reflection(Rng& g, f3 n) {
+    f3 r;
+    do {
+        const float a = g.next() * 2.0f - 1.0f;
+        const float b = g.next() * 2.0f - 1.0f;
+        const float c = g.next() * 2.0f - 1.0f;
+        r = mk(a, b, c);
+    } while (dot(r, r) > 1);
+    if (dot(r, n) < 0) r = r * -1.0f;
+    return normalize(r);
+}
+
+// Reflect / Refract (renderer.cpp:913-925), Schlick (:1588-1594, :1611-1616).
+__device__ __forceinline__ f3 reflect(f3 d, f3 n) { return d - (n * 2.0f) * dot(n, d); }
+__device__ __forceinline__ f3 refract(f3 d, f3 n, float ratio) {
+    const float c = smin(dot(-d, n), 1.0f);
+    const f3 rper = (d + n * c) * ratio;
+    const f3 rpar = n * (-__fsqrt_rn(fabsf(1.0f - dot(rper, rper))));
+    return rper + rpar;
+}
+__device__ __forceinline__ float schlick(float cosine, float ior) {
+    float r0 = __fdiv_rn(1 - ior, 1 + ior);
+    r0 = r0 * r0;
+    return r0 + (1 - r0) * cr_pow5(1 - cosine);
+}
+__device__ __forceinline__ float schlick_nonmetal(float cosine) {
+    const float r0 = 0.04f;
+    return r0 + (1 - r0) * cr_pow5(1 - cosine);
+}
+
+// Light evaluation: PointLightEvaluate (renderer.cpp:102-131), AreaLightEvaluation
+// (:161-207), SpotLightEvaluate (:133-159), DirectionalLightEvaluate (:315-338),
+// Illumination (:738-764).
+__device__ __noinline__ f3 illumination(const SceneView& sv, const Ray& r, Rng& g, Counters& k) {
+    const uint64_t pc = sv.num_points, scn = sv.num_spots, ac = sv.num_areas;
+    const uint64_t lc = pc + scn + ac + 1;
+    const uint64_t idx = (uint64_t)(g.next() * (float)lc);
+    const f3 ip = ray_point(r);
+    const f3 n = r.N;
+    const f3 kd = albedo(sv, r.mat);
+    f3 inc = mk(0.f, 0.f, 0.f);
+    if (idx < pc) {
+        const vpx_point_light& l = sv.points[idx];
+        const f3 dir = ld3(l.position) - ip;
+        const float dst = length(dir);
+        const f3 dn = dir * __fdiv_rn(1.0f, dst);
+        const float c = dot(dn, n);
+        if (!(c <= 0.0f)) {  // `if (cosTheta <= 0) return 0` (NaN continues)
+            const f3 li = (ld3(l.color) * smax(0.0f, c)) * __fdiv_rn(1.0f, dst * dst);
+            Ray sh = make_ray(offset_ray(ip, n), dn);
+            sh.t = dst;
+            if (!shadow(sv, sh, k)) inc = li * kd;
+        }
+    } else if (idx < ac + pc) {
+        const vpx_area_light& l = sv.areas[idx - pc];
+        const f3 center = ld3(l.position);
+        const float radius = l.radius;
+        const f3 point = offset_ray(ip, n);
+        f3 acc = mk(0.f, 0.f, 0.f);
+        for (int i = 0; i < sv.area_samples; ++i) {
+            f3 rp = random_direction(g);
+            rp = rp * radius;
+            rp = rp + center;
+            const f3 dir = rp - ip;
+            const float dst = length(dir);
+            const f3 dn = dir * __fdiv_rn(1.0f, dst);
+            const float c = dot(dn, n);
+            if (c <= 0) continue;
+            Ray sh = make_ray(point, dn);
+            sh.t = dst;
+            if (shadow(sv, sh, k)) continue;
+            f3 li = ld3(l.color) * c;
+            li = li * l.color_multiplier;
+            li = li * (radius * radius);
+            li = li * kPi;
+            li = li * 4.0f;
+            li = li / (dst * dst);
+            acc = acc + li;
+        }
+        acc = acc / (float)sv.area_samples;
+        inc = acc * kd;
+    } else if (idx < ac + scn + pc) {
+        const vpx_spot_light& l = sv.spots[idx - ac - pc];
+        const f3 dir = ld3(l.position) - ip;
+        const float dst = length(dir);
+        const f3 dn = dir / dst;
+        const float c = dot(dn, ld3(l.direction));
+        if (!(c <= l.angle)) {
+            const float alpha = 1.0f - __fdiv_rn((1.0f - c) * 1.0f, 1.0f - l.angle);
+            const f3 li = (ld3(l.color) * smax(0.0f, c)) / (dst * dst);
+            Ray sh = make_ray(offset_ray(ip, n), dn);
+            sh.t = dst;
+            if (!shadow(sv, sh, k)) inc = (li * kd) * alpha;
+        }
+    } else {
+        const f3 dir = -ld3(sv.dir.direction);
+        const float c = dot(dir, n);
+        if (!(c <= 0)) {
+            const f3 li = ld3(sv.dir.color) * smax(0.0f, c);
+            Ray sh = make_ray(offset_ray(ip, n), dir);
+            if (!shadow(sv, sh, k)) inc = li * kd;
+        }
+    }
+    return inc * (float)lc;
+}
+
+// Glass/smoke interior march in object space (renderer.cpp:1160-1173, 1266-1279).
+template <int MODE>
+__device__ __forceinline__ bool exit_march(const SceneView& sv, Ray& r, int32_t vox, Counters& k) {
+    const vpx_volume& vol = sv.volumes[vox];
+    ORay o;
+    o.O = xform_pos(r.O, vol.inv_matrix);
+    o.D = xform_vec(r.D, vol.inv_matrix);
+    o.rD = mk(__fdiv_rn(1.0f, o.D.x), __fdiv_rn(1.0f, o.D.y), __fdiv_rn(1.0f, o.D.z));
+    const DevGrid g = sv.grids[vol.grid_id];
+    Dda s;
+    if (!dda_setup(vol, g.n, o, s)) return false;
+    const WalkResult w = dda_walk<MODE>(g, s, 0.0f, k.cells);
+    r.t = w.t;
+    if (w.hit) {
+        r.N = normal_voxel(o, w.t, g.n, vol.matrix);
+        r.mat = w.cell;
+    }
+    return w.hit;
+}
+
+// One combine record per Trace level, folded bottom-up in trace_path():
+//   kFormMulAdd:  v*a + b   (non-metal diffuse: incLight + Trace*albedo)
+//   kFormAddMul:  (v + b)*a (model materials: (Trace + incLight)*albedo)
+//   kFormMul:     v*a       (metal, glass, smoke)
+//   kFormPass:    v         (non-metal specular)
+enum { kFormMulAdd = 0, kFormAddMul = 1, kFormMul = 2, kFormPass = 3 };
+
+struct Level {
+    f3 a, b;
+};
+
+// Renderer::Trace(ray, depth) — renderer.cpp:1076-1328, recursion unrolled to a loop.
+template <int LEVELS>
+__device__ __forceinline__ f3 trace_path(const SceneView& sv, Ray ray, int depth, Rng& g, Counters& k) {
+    Level lv[LEVELS];
+    uint32_t forms = 0;
+    int nl = 0;
+    f3 leaf = mk(0.f, 0.f, 0.f);
+    for (;;) {
+        if (depth < 0) break;  // Trace(depth < 0) returns 0
+        const int32_t vox = find_nearest(sv, ray, k);
+        if (ray.mat == kNone) {
+            leaf = ld3(sv.sky);
+            break;
+        }
+        const uint32_t m = ray.mat;
+        const vpx_material& mat = sv.materials[m];
+        f3 a = mk(1.f, 1.f, 1.f), b = mk(0.f, 0.f, 0.f);
+        uint32_t form;
+        Ray next;
+        if (m >= VPX_MAT_METAL_HIGH && m <= VPX_MAT_METAL_LOW) {  // :1103-1114
+            const f3 refl = reflect(ray.D, ray.N);
+            const f3 o = offset_ray(ray_point(ray), ray.N);
+            next = make_ray(o, refl + random_sphere_sample(g) * mat.roughness);
+            a = albedo(sv, m);
+            form = kFormMul;
+        } else if (m <= VPX_MAT_NON_METAL_PINK) {  // :1117-1144
+            if (g.next() > schlick_nonmetal(dot(-ray.D, ray.N))) {
+                const f3 rdir = ray.N + random_sphere_sample(g);
+                b = illumination(sv, ray, g, k);
+                next = make_ray(offset_ray(ray_point(ray), ray.N), rdir);
+                a = albedo(sv, m);
+                form = kFormMulAdd;
+            } else {
+                const f3 refl = reflect(ray.D, ray.N);
+                const f3 o = offset_ray(ray_point(ray), ray.N);
+                next = make_ray(o, refl + random_sphere_sample(g) * mat.roughness);
+                form = kFormPass;
+            }
+        } else if (m == VPX_MAT_GLASS) {  // :1146-1209
+            bool in_glass = ray.inside;
+            const float ior = mat.ior;
+            const float ratio = in_glass ? ior : __fdiv_rn(1.0f, ior);
+            bool inside_volume = true;
+            if (in_glass) {
+                a = albedo(sv, m);
+                if (vox >= 0) inside_volume = exit_march<kGlassExit>(sv, ray, vox, k);
+            }
+            if (!inside_volume) {
+                ray.O = ray.O + ray.D * ray.t;
+                ray.t = 0;
+            }
+            const float c = smin(dot(-ray.D, ray.N), 1.0f);
+            const float s = __fsqrt_rn(1.0f - c * c);
+            const bool cannot = ratio * s > 1.0f;
+            f3 rdir, rn;
+            if (cannot || schlick(c, ratio) > g.next()) {
+                rdir = reflect(ray.D, ray.N);
+                rn = ray.N;
+            } else {
+                rdir = refract(ray.D, ray.N, ratio);
+                in_glass = !in_glass;
+                rn = -ray.N;
+            }
+            next = make_ray(offset_ray(ray_point(ray), rn), rdir);
+            next.inside = in_glass;
+            form = kFormMul;
+        } else if (m <= VPX_MAT_SMOKE_PLAYER) {  // smoke :1210-1314
+            f3 color = mk(1.f, 1.f, 1.f);
+            bool in_glass = ray.inside;
+            bool inside_volume = true;
+            float intensity = 0.f, dist = 0.f;
+            if (vox == 0) (void)illumination(sv, ray, g, k);  // player light probe :1228-1240
+            if (in_glass) {
+                intensity = mat.emissive;
+                color = albedo(sv, m);
+                if (vox >= 0) inside_volume = exit_march<kSmokeExit>(sv, ray, vox, k);
+                dist = ray.t;
+            }
+            const float threshold = g.next() * 100.0f - intensity;
+            if (g.next() * dist > threshold) {
+                const float lo = ray.t * .45f, hi = ray.t;
+                const float tt = lo + g.next() * (hi - lo);
+                ray.O = ray.O + ray.D * tt;
+                ray.D = random_direction(g);
+                ray.t = 0;
+            }
+            const f3 flipped = mk(1.f, 1.f, 1.f) - color;
+            const f3 e = flipped * ((-dist) * intensity);
+            a = mk(cr_exp(e.x), cr_exp(e.y), cr_exp(e.z));
+            if (!inside_volume) {
+                ray.O = ray.O + ray.D * ray.t;
+                ray.t = 0;
+            }
+            const f3 rdir = refract(ray.D, ray.N, 1.0f);
+            next = make_ray(offset_ray(ray_point(ray), -ray.N), rdir);
+            next.inside = !in_glass;
+            form = kFormMul;
+        } else if (m == VPX_MAT_EMISSIVE) {  // :1315-1316
+            leaf = albedo(sv, m) * mat.emissive;
+            break;
+        } else {  // model materials :1319-1326
+            const f3 rdir = diffuse_reflection(g, ray.N);
+            b = illumination(sv, ray, g, k);
+            next = make_ray(offset_ray(ray_point(ray), ray.N), rdir);
+            a = albedo(sv, m);
+            form = kFormAddMul;
+        }
+        if (nl < LEVELS) {
+            lv[nl].a = a;
+            lv[nl].b = b;
+            forms |= form << (2 * nl);
+            ++nl;
+        }
+        ray = next;
+        --depth;
+    }
+    f3 v = leaf;
+    for (int i = nl - 1; i >= 0; --i) {
+        const uint32_t form = (forms >> (2 * i)) & 3u;
+        const f3 a = lv[i].a, b = lv[i].b;
+        if (form == kFormMulAdd)
+            v = b + v * a;
+        else if (form == kFormAddMul)
+            v = (v + b) * a;
+        else if (form == kFormMul)
+            v = v * a;
+    }
+    return v;
+}
+
+}  // namespace vpx

@@ -1,0 +1,302 @@
+"""Scene descriptions for the trace path: worlds, volumes, materials, lights, camera.
+
+Everything here is HOST-side input preparation restating the reference's scene setup:
+  - models: the ogt_vox-decoded .vox data (tests/golden/<name>.npz, produced by the
+    reference's own vendored decoder lib/ogt_vox.h — see tests/golden/make_golden.py);
+  - `load_model_grid`  Scene::LoadModel placement      template/scene.cpp:449-529
+  - `palette_materials` LoadModel's palette override    template/scene.cpp:516-520
+  - lights / materials / camera defaults                renderer.cpp:93-100,357-443; camera.h
+  - the build-defined tiled worlds of SURVEY.md §8(d) (C1/C2/C3/C4): the reference has no
+    world larger than 128^3 of its own (every .vox is <= 126 voxels a side).
+The device never sees this module's numpy arrays except through libvpx_hip.so uploads.
+"""
+import ctypes as C
+import dataclasses
+import math
+import os
+
+import numpy as np
+
+from . import abi
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+GOLDEN = os.path.join(REPO, "tests", "golden")
+NONE = abi.MAT_NONE
+
+
+# ----------------------------------------------------------------------------- models
+def load_model(name):
+    """(size[3], voxels uint8[sx*sy*sz], palette uint8[256,4]) as ogt_vox returns them."""
+    z = np.load(os.path.join(GOLDEN, name + ".npz"))
+    return z["size"].astype(np.int64), z["voxels"].astype(np.uint8), z["palette"].astype(np.uint8)
+
+
+def orient_model(size, voxels):
+    """Grid-oriented model (x, z, y) as LoadModel places it; empty -> NONE.
+    Returns (array[mz, my, mx], (mx, my, mz)) with index x + y*mx + z*mx*my."""
+    sx, sy, sz = (int(v) for v in size)
+    v = voxels.reshape(sz, sy, sx)
+    o = np.ascontiguousarray(v.transpose(1, 0, 2))  # [y_model][z_model][x] = [gz][gy][gx]
+    o = np.where(o == 0, np.uint8(NONE), o).astype(np.uint8)
+    return o, (sx, sz, sy)
+
+
+def load_model_grid(size, voxels, n, scale_model=(1.0, 1.0, 1.0)):
+    """Scene::LoadModel into an n^3 grid (template/scene.cpp:449-529): ResetGrid() to
+    NONE, downscale only when size_x > n, (x, y, z) -> (x*s.x, z*s.y, y*s.z)."""
+    sx, sy, sz = (int(v) for v in size)
+    scl = np.array(scale_model, np.float32)
+    if sx > n:
+        scl = scl * (np.float32(n) / np.array([sx, sy, sz], np.float32))
+    grid = np.full(n * n * n, NONE, np.uint8)
+    v = voxels.reshape(sz, sy, sx)
+    zz, yy, xx = np.nonzero(v)
+    vals = v[zz, yy, xx]
+    gx = (xx.astype(np.float32) * scl[0]).astype(np.int64)
+    gy = (zz.astype(np.float32) * scl[1]).astype(np.int64)
+    gz = (yy.astype(np.float32) * scl[2]).astype(np.int64)
+    ok = (gx >= 0) & (gy >= 0) & (gz >= 0) & (gx < n) & (gy < n) & (gz < n)
+    idx = gx[ok] + gy[ok] * n + gz[ok] * n * n
+    # later voxels (z-major, then y, then x) overwrite earlier ones, as the loop does
+    order = np.lexsort((xx[ok], yy[ok], zz[ok]))
+    grid[idx[order]] = vals[ok][order]
+    return grid
+
+
+def default_materials():
+    lib = abi.load_library()
+    mats = (abi.Material * 256)()
+    abi.check(lib, None, lib.vpx_default_materials(mats), "vpx_default_materials")
+    return mats
+
+
+def palette_materials(mats, voxels, palette):
+    """LoadModel's palette override (template/scene.cpp:516-520): every used index gets
+    albedo = rgb/255 and roughness 1."""
+    for i in np.unique(voxels[voxels > 0]):
+        c = palette[int(i)]
+        m = mats[int(i)]
+        for k in range(3):
+            m.albedo[k] = float(np.float32(c[k]) / np.float32(255.0))
+        m.roughness = 1.0
+    return mats
+
+
+# ------------------------------------------------------------------------------ grids
+@dataclasses.dataclass
+class GridSpec:
+    """A voxel grid: either dense host bytes or the build-defined tiled generator."""
+    n: int
+    dense: np.ndarray = None          # uint8[n^3], index x + y*n + z*n*n
+    model: np.ndarray = None          # grid-oriented model for the tiled generator
+    model_dims: tuple = None          # (mx, my, mz)
+    period: tuple = None              # (px, py, pz)
+    ground: int = 2
+
+    def host_cells(self):
+        if self.dense is not None:
+            return self.dense
+        from_oracle = _tiled_numpy(self)
+        return from_oracle
+
+    def upload(self, lib, ctx, grid_id):
+        if self.dense is not None:
+            arr = np.ascontiguousarray(self.dense, np.uint8)
+            abi.check(lib, ctx, lib.vpx_upload_grid(ctx, grid_id, arr.ctypes.data_as(C.c_void_p), self.n),
+                      "vpx_upload_grid")
+        else:
+            m = np.ascontiguousarray(self.model, np.uint8)
+            mx, my, mz = self.model_dims
+            px, py, pz = self.period
+            abi.check(lib, ctx, lib.vpx_generate_tiled_grid(ctx, grid_id, self.n, m.ctypes.data_as(C.c_void_p), mx,
+                                                            my, mz, px, py, pz, self.ground),
+                      "vpx_generate_tiled_grid")
+
+
+def _tiled_numpy(spec):
+    """Host-side tiled world (numpy), same contract as vpx_generate_tiled_grid."""
+    n = spec.n
+    mx, my, mz = spec.model_dims
+    px, py, pz = spec.period
+    m = spec.model.reshape(mz, my, mx)
+    x = np.arange(n)
+    lx = x % px
+    okx = lx < mx
+    out = np.empty((n, n, n), np.uint8)
+    for z in range(n):
+        lz = z % pz
+        sl = out[z]
+        if lz >= mz:
+            sl[:] = NONE
+        else:
+            ys = np.arange(n)
+            ly = (ys - spec.ground) % py
+            oky = (ys >= spec.ground) & (ly < my)
+            plane = m[lz][np.minimum(ly, my - 1)][:, np.minimum(lx, mx - 1)]
+            sl[:] = np.where(oky[:, None] & okx[None, :], plane, NONE)
+        sl[: spec.ground] = 0
+    return out.reshape(-1)
+
+
+def tiled_grid(model_name, n, ground=2, period_scale=2):
+    size, vox, pal = load_model(model_name)
+    o, dims = orient_model(size, vox)
+    period = tuple(int(period_scale * d) for d in dims)
+    return GridSpec(n=n, model=o.reshape(-1), model_dims=dims, period=period, ground=ground), vox, pal
+
+
+# ------------------------------------------------------------------------------ scene
+@dataclasses.dataclass
+class SceneDesc:
+    name: str
+    grids: list
+    volumes: object            # ctypes array of abi.Volume
+    materials: object          # ctypes array of 256 abi.Material
+    points: list
+    spots: list
+    areas: list
+    dir_light: abi.DirLight
+    camera: abi.Camera
+    width: int
+    height: int
+    max_bounces: int = 0
+    flags: int = 0
+    aa_strength: float = 1.0
+    area_samples: int = 3
+    sky: tuple = abi.SKY_DEFAULT
+    spheres: list = dataclasses.field(default_factory=list)
+    triangles: list = dataclasses.field(default_factory=list)
+    spp: int = 1
+
+    def frame_params(self, frame_index=0, seed_base=0, width=None, height=None):
+        p = abi.FrameParams()
+        p.width = width or self.width
+        p.height = height or self.height
+        p.max_bounces = self.max_bounces
+        p.frame_index = frame_index
+        p.seed_base = seed_base
+        p.flags = self.flags
+        p.aa_strength = self.aa_strength
+        p.area_samples = self.area_samples
+        p.sky = abi.vec3(self.sky)
+        return p
+
+    def with_size(self, width, height):
+        """Same scene at another resolution (camera ASPECT follows W/H, camera.h:183)."""
+        d = dataclasses.replace(self, width=width, height=height)
+        d.camera = look_at(self._cam_pos, self._cam_target, width, height)
+        d._cam_pos, d._cam_target = self._cam_pos, self._cam_target
+        return d
+
+
+def look_at(pos, target, width, height):
+    lib = abi.load_library()
+    cam = abi.Camera()
+    p = (C.c_float * 3)(*pos)
+    t = (C.c_float * 3)(*target)
+    abi.check(lib, None, lib.vpx_camera_look_at(p, t, width, height, C.byref(cam)), "vpx_camera_look_at")
+    return cam
+
+
+def volume(position=(0.0, 0.0, 0.0), scale=(1.0, 1.0, 1.0), rotation=(0.0, 0.0, 0.0), grid_id=0):
+    lib = abi.load_library()
+    v = abi.Volume()
+    f = lambda a: (C.c_float * 3)(*a)
+    abi.check(lib, None, lib.vpx_volume_set_transform(f(position), f(scale), f(rotation), C.byref(v)),
+              "vpx_volume_set_transform")
+    v.grid_id = grid_id
+    return v
+
+
+def point_light(position=(0.5, 0.5, 3.5), color=(1.0, 1.0, 1.0)):  # PointLight.h:13
+    return abi.PointLight(abi.vec3(position), abi.vec3(color))
+
+
+def spot_light(position=(-1.0, 0.5, -1.0), direction=(1.0, 0.0, 0.0), color=(1.5, 1.5, 1.5),
+               angle=None):  # SpotLight.h:23, angle = CosDegrees(45)
+    if angle is None:
+        angle = float(np.float32(math.cos(float(np.float32(45.0) * np.float32(math.pi) / np.float32(180.0)))))
+    return abi.SpotLight(abi.vec3(position), abi.vec3(direction), abi.vec3(color), angle)
+
+
+def area_light(position=(-0.0, 0.5, -3.5), color=(1.0, 1.0, 1.0), mult=1.2, radius=1.2):  # SphereAreaLight.h:13
+    return abi.AreaLight(abi.vec3(position), abi.vec3(color), mult, radius)
+
+
+def dir_light(direction=(1.0, 0.0, 0.0), color=(0.0, 0.0, 0.0)):  # DirectionalLight.h:12
+    return abi.DirLight(abi.vec3(direction), abi.vec3(color))
+
+
+def _scene(name, grids, vols, mats, points, spots, areas, dl, cam_pos, cam_target, w, h, **kw):
+    varr = (abi.Volume * len(vols))(*vols)
+    d = SceneDesc(name=name, grids=grids, volumes=varr, materials=mats, points=points, spots=spots, areas=areas,
+                  dir_light=dl, camera=look_at(cam_pos, cam_target, w, h), width=w, height=h, **kw)
+    d._cam_pos, d._cam_target = tuple(cam_pos), tuple(cam_target)
+    return d
+
+
+# ---------------------------------------------------------------------------- configs
+# BASELINE.json configs; worlds and cameras beyond the reference's own are build-defined
+# (SURVEY.md §8(d)).  C1 is the metric's workload.
+C0_CAM = ((0.5, 0.35, -0.6), (0.5, 0.2, 0.3))
+CITY_CAM = ((1.25, 0.9, -0.35), (0.45, 0.15, 0.55))
+CITY_LIGHTS = dict(points=[point_light((0.5, 1.5, 0.5), (1.0, 1.0, 1.0))],
+                   dir_light=dir_light((-0.3, -1.0, -0.2), (1.0, 1.0, 1.0)))
+
+
+def model_scene(model="teapot", n=128, width=640, height=360, max_bounces=0, cam=C0_CAM, city_lights=False):
+    """C0: the reference's own setup — Scene({0}, n) + LoadModel + SetTransform({0})."""
+    size, vox, pal = load_model(model)
+    grid = GridSpec(n=n, dense=load_model_grid(size, vox, n))
+    mats = palette_materials(default_materials(), vox, pal)
+    if city_lights:
+        pts, dl = CITY_LIGHTS["points"], CITY_LIGHTS["dir_light"]
+    else:
+        pts, dl = [point_light()], dir_light()
+    return _scene(f"{model}{n}", [grid], [volume()], mats, pts, [], [], dl, cam[0], cam[1], width, height,
+                  max_bounces=max_bounces)
+
+
+def city_scene(model="monu3", n=1024, width=1920, height=1080, max_bounces=0, areas=None, cam=CITY_CAM):
+    """C1/C2/C3: a .vox model tiled with a 2x period above a white ground slab."""
+    spec, vox, pal = tiled_grid(model, n)
+    mats = palette_materials(default_materials(), vox, pal)
+    pts = list(CITY_LIGHTS["points"]) if areas is None else []
+    dl = CITY_LIGHTS["dir_light"]
+    return _scene(f"{model}-city{n}", [spec], [volume()], mats, pts, [], list(areas or []), dl, cam[0], cam[1],
+                  width, height, max_bounces=max_bounces)
+
+
+C3_AREAS = [area_light((0.5, 2.0, 0.5)), area_light((-1.5, 1.5, 0.5)), area_light((2.5, 1.5, 0.5)),
+            area_light((0.5, 1.5, -1.5))]
+
+
+def instanced_scene(n=2048, inst_n=64, width=3840, height=2160, model="monu3", spp=16):
+    """C4: the city plus 64 transformed instances of one 64^3 model grid (4x4x4 lattice
+    floating above it, scale 0.1, fixed rotations).  The reference semantics are a linear
+    loop over 65 volumes (renderer.cpp:952-993)."""
+    spec, vox, pal = tiled_grid(model, n)
+    size, mv, _ = load_model(model)
+    inst = GridSpec(n=inst_n, dense=load_model_grid(size, mv, inst_n))
+    mats = palette_materials(default_materials(), vox, pal)
+    vols = [volume(grid_id=0)]
+    for k in range(4):
+        for j in range(4):
+            for i in range(4):
+                c = (0.125 + 0.25 * i, 1.125 + 0.25 * j, 0.125 + 0.25 * k)
+                pos = tuple(v - 0.5 for v in c)
+                rot = (0.0, 0.3 * (i + 4 * j + 16 * k), 0.1 * k)
+                vols.append(volume(pos, (0.1, 0.1, 0.1), rot, grid_id=1))
+    return _scene(f"{model}-inst{n}", [spec, inst], vols, mats, [], [], list(C3_AREAS),
+                  CITY_LIGHTS["dir_light"], (1.6, 1.9, -1.2), (0.5, 0.7, 0.5), width, height, spp=spp)
+
+
+CONFIGS = {
+    "C0": lambda: model_scene("teapot", 128, 640, 360, 0),
+    "C0m": lambda: model_scene("monu3", 128, 640, 360, 0),
+    "C1": lambda: city_scene("monu3", 1024, 1920, 1080, 0),
+    "C2": lambda: city_scene("roomGlass", 1024, 1920, 1080, 4),
+    "C3": lambda: city_scene("monu3", 2048, 3840, 2160, 0, areas=C3_AREAS),
+    "C4": lambda: instanced_scene(),
+}

@@ -1,0 +1,241 @@
+"""GPU parity: libvpx_hip.so (through the C-ABI) against the CPU restatement (oracle/).
+
+The bar is bit-exactness: t, normals, materials, occlusion, cells visited and every float
+of the radiance / accumulator, and every RGB8 byte.  The oracle itself is "parity
+unpinned" against the reference; these tests pin the GPU to the oracle.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():
+    pytest.skip("no GPU", allow_module_level=True)
+
+
+def bits(a):
+    return np.ascontiguousarray(a, np.float32).view(np.uint32)
+
+
+def random_rays(n, seed, inside_frac=0.3, axis_frac=0.1):
+    rng = np.random.default_rng(seed)
+    o = rng.uniform(-0.6, 1.6, (n, 3)).astype(np.float32)
+    k = int(n * inside_frac)
+    o[:k] = rng.uniform(0.0, 1.0, (k, 3)).astype(np.float32)
+    target = rng.uniform(0.1, 0.9, (n, 3)).astype(np.float32)
+    d = (target - o).astype(np.float32)
+    d[k:2 * k] = rng.normal(size=(k, 3)).astype(np.float32)
+    a = int(n * axis_frac)
+    if a:  # axis-aligned and zero-component directions (rD = +-inf)
+        axes = rng.integers(0, 3, a)
+        d[-a:] = 0
+        d[-a:][np.arange(a), axes] = rng.choice([-1.0, 1.0], a)
+    return o, d
+
+
+def make_ctx(pkg, desc):
+    ctx = pkg.context.Context(0)
+    ctx.load_scene(desc)
+    return ctx
+
+
+def cmp_hits(pkg, gh, oh, n):
+    g = pkg.context.hits_to_numpy(gh, n)
+    o = pkg.context.hits_to_numpy(oh, n)
+    for f in ("vox_index", "material", "cells", "inside_glass"):
+        assert np.array_equal(g[f], o[f]), f
+    assert np.array_equal(bits(g["t"]), bits(o["t"]))
+    assert np.array_equal(bits(g["normal"]), bits(o["normal"]))
+    return g
+
+
+SCENES = {
+    "teapot128": lambda sc: sc.model_scene("teapot", 128, 96, 64, 0),
+    "monu3_128": lambda sc: sc.model_scene("monu3", 128, 96, 64, 0),
+    "room128_d4": lambda sc: sc.model_scene("roomGlass", 128, 96, 64, 4, city_lights=True),
+    "city128_d0": lambda sc: sc.city_scene("monu3", 128, 96, 64, 0),
+    "cityglass128_d4": lambda sc: sc.city_scene("roomGlass", 256, 96, 64, 4),
+}
+
+
+@pytest.mark.parametrize("name", sorted(SCENES))
+def test_find_nearest_and_occlusion(pkg, orc, name):
+    desc = SCENES[name](pkg.scene)
+    ctx = make_ctx(pkg, desc)
+    o = orc.Oracle(pkg.abi, desc)
+    org, dirs = random_rays(4096, 7)
+    rays = pkg.context.make_rays(org, dirs)
+    g = cmp_hits(pkg, ctx.find_nearest(rays), o.find_nearest(rays), len(rays))
+    assert (g["vox_index"] >= 0).mean() > 0.1  # the test hits something
+    srays = pkg.context.make_rays(org, dirs, tmax=np.random.default_rng(3).uniform(0.05, 3.0, len(org)))
+    occ_g = ctx.is_occluded(srays)
+    occ_o, _ = o.is_occluded(srays)
+    assert np.array_equal(occ_g, occ_o)
+    ctx.close()
+
+
+@pytest.mark.parametrize("name", sorted(SCENES))
+@pytest.mark.parametrize("depth", [0, 4, 14])
+def test_trace_rays(pkg, orc, name, depth):
+    desc = SCENES[name](pkg.scene)
+    ctx = make_ctx(pkg, desc)
+    o = orc.Oracle(pkg.abi, desc)
+    org, dirs = random_rays(2048, 11 + depth)
+    rays = pkg.context.make_rays(org, dirs, inside=(np.arange(len(org)) % 5 == 0).astype(np.uint32))
+    seeds = np.random.default_rng(depth).integers(1, 2**32 - 1, len(org), dtype=np.uint64).astype(np.uint32)
+    rg = ctx.trace(rays, seeds, depth, desc.sky, desc.area_samples)
+    ro, _ = o.trace(rays, seeds, depth, desc.sky, desc.area_samples)
+    assert np.array_equal(bits(rg), bits(ro))
+    ctx.close()
+
+
+def render_gpu(pkg, desc, frames=1, flags=None):
+    r = pkg.renderer.Renderer(desc, 0)
+    if flags is not None:
+        desc.flags = flags
+    r.Init()
+    stats = []
+    for _ in range(frames):
+        stats.append(r.Tick(0.0, stats=True))
+    torch.cuda.synchronize()
+    acc, rgb = r.accumulator_host().reshape(-1, 4).copy(), r.screen_host().reshape(-1).copy()
+    r.ctx.close()
+    return acc, rgb, stats
+
+
+@pytest.mark.parametrize("name", sorted(SCENES))
+def test_render_frame_bit_exact(pkg, orc, name):
+    desc = SCENES[name](pkg.scene)
+    acc_g, rgb_g, st = render_gpu(pkg, desc)
+    o = orc.Oracle(pkg.abi, desc)
+    acc_o, rgb_o, ost = o.render(desc.frame_params(0))
+    assert np.array_equal(bits(acc_g), bits(acc_o))
+    assert np.array_equal(rgb_g, rgb_o)
+    s = st[0]
+    assert (s.primary_rays, s.shadow_rays, s.bounce_rays, s.dda_cells) == (
+        ost.primary_rays, ost.shadow_rays, ost.bounce_rays, ost.dda_cells)
+
+
+def test_progressive_accumulation_aa(pkg, orc):
+    """4 frames with AA jitter: running average w = 1/(n+1), seeds advance per frame."""
+    desc = pkg.scene.model_scene("monu3", 128, 80, 48, 1, city_lights=True)
+    desc.flags = pkg.abi.VPX_FLAG_AA
+    acc_g, rgb_g, _ = render_gpu(pkg, desc, frames=4)
+    o = orc.Oracle(pkg.abi, desc)
+    acc = None
+    for f in range(4):
+        acc, rgb, _ = o.render(desc.frame_params(f), accum=acc)
+    assert np.array_equal(bits(acc_g), bits(acc))
+    assert np.array_equal(rgb_g, rgb)
+
+
+def test_dof_focus(pkg, orc):
+    desc = pkg.scene.model_scene("monu3", 128, 64, 40, 0, city_lights=True)
+    desc.flags = pkg.abi.VPX_FLAG_AA | pkg.abi.VPX_FLAG_DOF
+    ctx = make_ctx(pkg, desc)
+    o = orc.Oracle(pkg.abi, desc)
+    fd = ctx.focus_distance(desc.width, desc.height)
+    assert np.float32(fd).view(np.uint32) == np.float32(o.focus_distance(desc.width, desc.height)).view(np.uint32)
+    ctx.close()
+    desc.camera.focal_distance = fd
+    acc_g, rgb_g, _ = render_gpu(pkg, desc)
+    o.set_camera(desc.camera)
+    acc_o, rgb_o, _ = o.render(desc.frame_params(0))
+    assert np.array_equal(bits(acc_g), bits(acc_o))
+
+
+@pytest.mark.parametrize("wh", [(1, 1), (17, 5), (33, 31)])
+def test_odd_frame_sizes(pkg, orc, wh):
+    desc = pkg.scene.model_scene("monu3", 128, wh[0], wh[1], 2, city_lights=True)
+    acc_g, rgb_g, _ = render_gpu(pkg, desc)
+    acc_o, rgb_o, _ = orc.Oracle(pkg.abi, desc).render(desc.frame_params(0))
+    assert np.array_equal(bits(acc_g), bits(acc_o)) and np.array_equal(rgb_g, rgb_o)
+
+
+def test_tiles_composite_equals_monolithic(pkg, orc):
+    """Multi-GPU layout on one device: R ranks' packed tiles -> composite == vpx_render."""
+    desc = pkg.scene.city_scene("monu3", 128, 100, 70, 0)
+    acc_ref, rgb_ref, _ = render_gpu(pkg, desc)
+    ctx = make_ctx(pkg, desc)
+    R = 3
+    L = ctx.packed_len(desc.width, desc.height, R)
+    gathered = torch.zeros(R * L * 4, dtype=torch.float32, device="cuda")
+    p = desc.frame_params(0)
+    for rank in range(R):
+        ctx.render_tiles(p, rank, R, gathered.data_ptr() + rank * L * 16)
+    acc = torch.zeros(desc.width * desc.height * 4, dtype=torch.float32, device="cuda")
+    rgb = torch.zeros(desc.width * desc.height, dtype=torch.int32, device="cuda")
+    ctx.composite_tiles(p, R, gathered.data_ptr(), acc.data_ptr(), rgb.data_ptr())
+    ctx.synchronize()
+    assert np.array_equal(bits(acc.cpu().numpy().reshape(-1, 4)), bits(acc_ref))
+    assert np.array_equal(rgb.cpu().numpy().view(np.uint32), rgb_ref)
+    ctx.close()
+
+
+def test_tiled_world_generator_matches_oracle(pkg, orc):
+    for model, n in (("monu3", 256), ("roomGlass", 320)):
+        spec, _, _ = pkg.scene.tiled_grid(model, n)
+        ctx = pkg.context.Context(0)
+        spec.upload(ctx.lib, ctx.h, 0)
+        o = orc.Oracle.__new__(orc.Oracle)
+        o.lib = orc._lib(pkg.abi)
+        cells = o.host_grid(spec)
+        assert ctx.grid_checksum(0) == o.lib.oracle_grid_checksum(cells.ctypes.data, cells.size)
+        ctx.close()
+
+
+def test_multi_volume_transforms_shapes(pkg, orc):
+    """Several transformed volumes sharing grids, plus spheres and triangles
+    (renderer.cpp:946-1018 linear loop, ties to the lowest index)."""
+    sc, abi = pkg.scene, pkg.abi
+    desc = sc.model_scene("monu3", 64, 64, 48, 3, city_lights=True)
+    size, vox, _ = sc.load_model("teapot")
+    desc.grids.append(sc.GridSpec(n=32, dense=sc.load_model_grid(size, vox, 32)))
+    vols = [sc.volume()]
+    vols.append(sc.volume((0.6, 0.0, 0.2), (0.5, 0.5, 0.5), (0.0, 0.7, 0.0), grid_id=1))
+    vols.append(sc.volume((-0.4, 0.1, 0.3), (1.0, 0.5, 2.0), (0.3, 0.2, 0.1), grid_id=0))
+    vols.append(sc.volume((0.0, 0.0, 0.0), (1.0, 1.0, 1.0), (0.0, 0.0, 0.0), grid_id=0))  # exact duplicate: tie
+    desc.volumes = (abi.Volume * len(vols))(*vols)
+    desc.spheres = [abi.Sphere(abi.vec3((0.3, 0.8, 0.4)), 0.15, 8), abi.Sphere(abi.vec3((0.8, 0.2, 0.1)), 0.1, 15)]
+    tri = abi.Triangle(abi.vec3((0.5, 0.6, 0.0)), abi.vec3((-0.25, 0, 0)), abi.vec3((0, 0.25, 0)),
+                       abi.vec3((0.25, 0, 0)), 5)
+    desc.triangles = [tri]
+    desc.spots = [sc.spot_light((0.5, 1.2, 0.5), (0.0, -1.0, 0.0), (2.0, 2.0, 2.0))]
+    desc.areas = [sc.area_light((0.5, 1.5, -0.5), radius=0.3)]
+    ctx = make_ctx(pkg, desc)
+    o = orc.Oracle(pkg.abi, desc)
+    org, dirs = random_rays(4096, 5)
+    rays = pkg.context.make_rays(org, dirs)
+    cmp_hits(pkg, ctx.find_nearest(rays), o.find_nearest(rays), len(rays))
+    ctx.close()
+    acc_g, rgb_g, _ = render_gpu(pkg, desc)
+    acc_o, rgb_o, _ = o.render(desc.frame_params(0))
+    assert np.array_equal(bits(acc_g), bits(acc_o)) and np.array_equal(rgb_g, rgb_o)
+
+
+def test_smoke_material_exits(pkg, orc):
+    """Smoke and glass volumes exercise FindSmokeExit / FindMaterialExit."""
+    sc = pkg.scene
+    desc = sc.model_scene("monu3", 64, 64, 48, 6, city_lights=True)
+    g = desc.grids[0].dense.reshape(64, 64, 64).copy()
+    g[20:40, 5:30, 20:44] = 11          # smoke block
+    g[40:50, 30:40, 10:30] = 8          # glass block
+    g[5:10, 40:45, 5:60] = 15           # emissive bar
+    desc.grids[0].dense = g.reshape(-1)
+    acc_g, rgb_g, _ = render_gpu(pkg, desc)
+    acc_o, rgb_o, _ = orc.Oracle(pkg.abi, desc).render(desc.frame_params(0))
+    assert np.array_equal(bits(acc_g), bits(acc_o)) and np.array_equal(rgb_g, rgb_o)
+
+
+@pytest.mark.parametrize("fill", [255, 0, 7])
+def test_degenerate_worlds(pkg, orc, fill):
+    """Empty world (all NONE), full diffuse world, full mirror world; camera inside."""
+    sc = pkg.scene
+    desc = sc.model_scene("monu3", 32, 40, 24, 4, cam=((0.5, 0.5, 0.5), (0.9, 0.2, 0.7)), city_lights=True)
+    desc.grids[0].dense = np.full(32 ** 3, fill, np.uint8)
+    acc_g, rgb_g, _ = render_gpu(pkg, desc)
+    acc_o, rgb_o, _ = orc.Oracle(pkg.abi, desc).render(desc.frame_params(0))
+    assert np.array_equal(bits(acc_g), bits(acc_o)) and np.array_equal(rgb_g, rgb_o)
