@@ -98,7 +98,8 @@ def run(args):
     desc = build_scene(pkg, args.config, W, H)
     if n == 1 and args.config != "C1":
         W, H = desc.width, desc.height
-    stream = torch.cuda.current_stream()
+    stream = torch.cuda.Stream()  # a real stream: the kernel and its HIP events share it
+    torch.cuda.set_stream(stream)
     ctx = pkg.context.Context(local)
     ctx.set_stream(stream.cuda_stream)
     ctx.load_scene(desc)

@@ -57,7 +57,7 @@ __device__ __forceinline__ Ray primary_ray(const FrameArgs& f, uint32_t x, uint3
     const f3 P = (tl + (tr - tl) * u) + (bl - tl) * v;
     const f3 cp = ld3(f.cam.cam_pos);
     if (f.flags & VPX_FLAG_DOF) {
-        const float rr = __fsqrt_rn(g.next());
+        const float rr = sqrtf(g.next());
         const float theta = g.next() * (2.0f * kPi);
         const float cx = cr_cos(theta) * rr, cy = cr_sin(theta) * rr;
         const float jx = __fdiv_rn(cx * f.cam.defocus_jitter, (float)f.width);

@@ -10,7 +10,9 @@
 // built with -ffp-contract=off and f32 denormal flush (template/template.cpp:130 sets
 // FTZ|DAZ); division and sqrt are correctly rounded (hipcc default); std::min/std::max
 // are spelled as the exact ternaries; sin/cos/pow/exp are the correctly rounded f32
-// values obtained through f64.  No approximations (rcp/rsq) are used anywhere.
+// values obtained through f64.  No approximations (rcp/rsq) are used anywhere; note that
+// HIP's __fsqrt_rn lowers to a 3-ulp sqrt (!fpmath 3.0), so plain sqrtf (correctly
+// rounded under hipcc's default -fhip-fp32-correctly-rounded-divide-sqrt) is used.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -61,9 +63,9 @@ __device__ __forceinline__ f3 operator*(f3 a, float s) { return mk(a.x * s, a.y 
 __device__ __forceinline__ f3 operator/(f3 a, float s) { return mk(a.x / s, a.y / s, a.z / s); }
 __device__ __forceinline__ f3 operator-(f3 a) { return mk(-a.x, -a.y, -a.z); }
 __device__ __forceinline__ float dot(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
-__device__ __forceinline__ float length(f3 a) { return __fsqrt_rn(dot(a, a)); }
+__device__ __forceinline__ float length(f3 a) { return sqrtf(dot(a, a)); }
 __device__ __forceinline__ f3 normalize(f3 v) {
-    const float inv = __fdiv_rn(1.0f, __fsqrt_rn(dot(v, v)));
+    const float inv = __fdiv_rn(1.0f, sqrtf(dot(v, v)));
     return v * inv;
 }
 __device__ __forceinline__ f3 cross(f3 a, f3 b) {
@@ -319,7 +321,7 @@ __device__ __forceinline__ void sphere_hit(const vpx_sphere& sp, Ray& r) {
     const float disc = b * b - cc;
     if (cc > 0.0f && b > 0.0f) return;
     if (disc < 0) return;
-    const float len = -b - __fsqrt_rn(disc);
+    const float len = -b - sqrtf(disc);
     if (len > r.t) return;
     if (len < 0) return;
     const f3 ip = r.O + r.D * len;
@@ -338,7 +340,7 @@ __device__ __forceinline__ bool sphere_is_hit(const vpx_sphere& sp, const Ray& r
     const float disc = b * b - cc;
     if (cc > 0.0f && b > 0.0f) return false;
     if (disc < 0) return false;
-    const float len = -b - __fsqrt_rn(disc);
+    const float len = -b - sqrtf(disc);
     if (len < 0) return false;
     if (len > r.t) return false;
     return true;
@@ -486,7 +488,7 @@ __device__ __forceinline__ f3 reflect(f3 d, f3 n) { return d - (n * 2.0f) * dot(
 __device__ __forceinline__ f3 refract(f3 d, f3 n, float ratio) {
     const float c = smin(dot(-d, n), 1.0f);
     const f3 rper = (d + n * c) * ratio;
-    const f3 rpar = n * (-__fsqrt_rn(fabsf(1.0f - dot(rper, rper))));
+    const f3 rpar = n * (-sqrtf(fabsf(1.0f - dot(rper, rper))));
     return rper + rpar;
 }
 __device__ __forceinline__ float schlick(float cosine, float ior) {
@@ -658,7 +660,7 @@ __device__ __forceinline__ f3 trace_path(const SceneView& sv, Ray ray, int depth
                 ray.t = 0;
             }
             const float c = smin(dot(-ray.D, ray.N), 1.0f);
-            const float s = __fsqrt_rn(1.0f - c * c);
+            const float s = sqrtf(1.0f - c * c);
             const bool cannot = ratio * s > 1.0f;
             f3 rdir, rn;
             if (cannot || schlick(c, ratio) > g.next()) {

@@ -32,7 +32,11 @@ class Renderer:
         w, h = self.scene.width, self.scene.height
         self.accumulator = torch.zeros(w * h * 4, dtype=torch.float32, device=self.device)
         self.screen = torch.zeros(w * h, dtype=torch.int32, device=self.device)
-        self.ctx.set_stream(torch.cuda.current_stream(self.device).cuda_stream)
+        torch.cuda.synchronize(self.device)
+        # the library launches on this torch stream (never the legacy NULL stream, whose
+        # handle 0 would select the context's own stream instead)
+        self.stream = torch.cuda.Stream(self.device)
+        self.ctx.set_stream(self.stream.cuda_stream)
         self.ctx.load_scene(self.scene)
         return self
 
@@ -56,8 +60,13 @@ class Renderer:
             return self.Update(stats=stats)
         raise NotImplementedError("static-camera reprojection path is out of scope (SURVEY.md §8(f) rank 1)")
 
+    def synchronize(self):
+        self.stream.synchronize()
+
     def screen_host(self):
+        self.synchronize()
         return self.screen.cpu().numpy().view("uint32").reshape(self.scene.height, self.scene.width)
 
     def accumulator_host(self):
+        self.synchronize()
         return self.accumulator.cpu().numpy().reshape(self.scene.height, self.scene.width, 4)

@@ -16,24 +16,7 @@ if not torch.cuda.is_available():
     pytest.skip("no GPU", allow_module_level=True)
 
 
-def bits(a):
-    return np.ascontiguousarray(a, np.float32).view(np.uint32)
-
-
-def random_rays(n, seed, inside_frac=0.3, axis_frac=0.1):
-    rng = np.random.default_rng(seed)
-    o = rng.uniform(-0.6, 1.6, (n, 3)).astype(np.float32)
-    k = int(n * inside_frac)
-    o[:k] = rng.uniform(0.0, 1.0, (k, 3)).astype(np.float32)
-    target = rng.uniform(0.1, 0.9, (n, 3)).astype(np.float32)
-    d = (target - o).astype(np.float32)
-    d[k:2 * k] = rng.normal(size=(k, 3)).astype(np.float32)
-    a = int(n * axis_frac)
-    if a:  # axis-aligned and zero-component directions (rD = +-inf)
-        axes = rng.integers(0, 3, a)
-        d[-a:] = 0
-        d[-a:][np.arange(a), axes] = rng.choice([-1.0, 1.0], a)
-    return o, d
+from cases import SCENES, bits, random_rays  # noqa: E402
 
 
 def make_ctx(pkg, desc):
@@ -50,15 +33,6 @@ def cmp_hits(pkg, gh, oh, n):
     assert np.array_equal(bits(g["t"]), bits(o["t"]))
     assert np.array_equal(bits(g["normal"]), bits(o["normal"]))
     return g
-
-
-SCENES = {
-    "teapot128": lambda sc: sc.model_scene("teapot", 128, 96, 64, 0),
-    "monu3_128": lambda sc: sc.model_scene("monu3", 128, 96, 64, 0),
-    "room128_d4": lambda sc: sc.model_scene("roomGlass", 128, 96, 64, 4, city_lights=True),
-    "city128_d0": lambda sc: sc.city_scene("monu3", 128, 96, 64, 0),
-    "cityglass128_d4": lambda sc: sc.city_scene("roomGlass", 256, 96, 64, 4),
-}
 
 
 @pytest.mark.parametrize("name", sorted(SCENES))
