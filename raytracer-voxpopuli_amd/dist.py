@@ -1,0 +1,105 @@
+"""Tile sharding of one frame across ranks (one process per GPU) with a gather to rank 0.
+
+Layout contract (shared with libvpx_hip.so's vpx_render_tiles / vpx_composite_tiles):
+  - the frame is cut into 16x16 tiles in row-major tile order, t = ty * tiles_x + tx;
+  - tile t belongs to rank t % R (round-robin: spatially uneven cost is spread evenly);
+  - a rank's packed buffer holds its tiles in increasing t, 256 float4 each (row-major
+    inside the tile), edge tiles zero-padded; every rank's buffer has the same length
+    ceil(num_tiles / R) * 256 so the gather is one fixed-size collective;
+  - rank 0 receives the R buffers back to back and composites them (unpack + running-
+    average accumulate + tonemap) into its accumulator and RGB8 screen.
+There is one exchange per frame (the gather); the world is replicated per GPU.  Over
+RCCL (torch.distributed backend "nccl") the gather is R-1 point-to-point transfers into
+rank 0, each on its own xGMI link on an MI355X node.
+"""
+import numpy as np
+
+TILE = 16
+
+
+def tiles_xy(width, height):
+    return (width + TILE - 1) // TILE, (height + TILE - 1) // TILE
+
+
+def packed_len(width, height, n_ranks):
+    """float4 elements per rank buffer (== vpx_tiles_packed_len)."""
+    tx, ty = tiles_xy(width, height)
+    return -(-(tx * ty) // n_ranks) * TILE * TILE
+
+
+def rank_pixel_ids(width, height, rank, n_ranks):
+    """Pixel ids (y*W + x) in packed order for one rank; -1 marks padding."""
+    tx, ty = tiles_xy(width, height)
+    tiles = np.arange(rank, tx * ty, n_ranks)
+    ly, lx = np.divmod(np.arange(TILE * TILE), TILE)
+    x = (tiles % tx)[:, None] * TILE + lx[None, :]
+    y = (tiles // tx)[:, None] * TILE + ly[None, :]
+    ids = np.where((x < width) & (y < height), y * width + x, -1).reshape(-1)
+    out = np.full(packed_len(width, height, n_ranks), -1, np.int64)
+    out[: ids.size] = ids
+    return out
+
+
+def pack(samples4, width, height, rank, n_ranks):
+    """Host reference of a rank's packed buffer from a full-frame float4 sample image."""
+    ids = rank_pixel_ids(width, height, rank, n_ranks)
+    out = np.zeros((ids.size, 4), np.float32)
+    ok = ids >= 0
+    out[ok] = np.asarray(samples4, np.float32).reshape(-1, 4)[ids[ok]]
+    return out
+
+
+def unpack(gathered, width, height, n_ranks):
+    """Host reference of vpx_composite_tiles' unpack step: R packed buffers -> image."""
+    L = packed_len(width, height, n_ranks)
+    g = np.asarray(gathered, np.float32).reshape(n_ranks, L, 4)
+    img = np.zeros((width * height, 4), np.float32)
+    for r in range(n_ranks):
+        ids = rank_pixel_ids(width, height, r, n_ranks)
+        ok = ids >= 0
+        img[ids[ok]] = g[r][ok]
+    return img
+
+
+def gather_tiles(packed, rank, n_ranks, out=None, group=None):
+    """Gather every rank's packed tensor to rank 0 (torch.distributed; RCCL on GPUs,
+    gloo on CPU).  Returns the concatenated [R*L*4] tensor on rank 0, None elsewhere."""
+    import torch
+    import torch.distributed as dist
+
+    if n_ranks == 1:
+        return packed
+    if rank == 0:
+        parts = [torch.empty_like(packed) for _ in range(n_ranks)]
+        dist.gather(packed, parts, dst=0, group=group)
+        if out is None:
+            return torch.cat(parts)
+        torch.cat(parts, out=out)
+        return out
+    dist.gather(packed, None, dst=0, group=group)
+    return None
+
+
+class ShardedFrame:
+    """One rank's share of the tile-sharded render (GPU path: libvpx_hip.so + RCCL)."""
+
+    def __init__(self, ctx, desc, rank, n_ranks, device):
+        import torch
+
+        self.ctx, self.desc, self.rank, self.n = ctx, desc, rank, n_ranks
+        w, h = desc.width, desc.height
+        self.L = ctx.packed_len(w, h, n_ranks)
+        assert self.L == packed_len(w, h, n_ranks)
+        self.packed = torch.zeros(self.L * 4, dtype=torch.float32, device=device)
+        self.gathered = torch.empty(n_ranks * self.L * 4, dtype=torch.float32, device=device) if rank == 0 else None
+        self.accum = torch.zeros(w * h * 4, dtype=torch.float32, device=device) if rank == 0 else None
+        self.screen = torch.zeros(w * h, dtype=torch.int32, device=device) if rank == 0 else None
+        self.frame = 0
+
+    def step(self):
+        p = self.desc.frame_params(frame_index=self.frame)
+        self.ctx.render_tiles(p, self.rank, self.n, self.packed.data_ptr())
+        g = gather_tiles(self.packed, self.rank, self.n, out=self.gathered)
+        if self.rank == 0:
+            self.ctx.composite_tiles(p, self.n, g.data_ptr(), self.accum.data_ptr(), self.screen.data_ptr())
+        self.frame += 1

@@ -1,0 +1,55 @@
+"""The C-ABI library loads without a GPU and exports every symbol include/vpx.h declares."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_symbols():
+    text = open(os.path.join(REPO, "include", "vpx.h")).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(vpx_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_header_symbols_exported(pkg):
+    lib = pkg.load_library()
+    syms = declared_symbols()
+    assert len(syms) >= 25
+    for s in syms:
+        assert hasattr(lib, s), s
+    assert set(syms) == set(pkg.abi.SIGNATURES), set(syms) ^ set(pkg.abi.SIGNATURES)
+    out = subprocess.run(["nm", "-D", "--defined-only", pkg.abi.LIB_PATH], capture_output=True, text=True).stdout
+    exported = set(re.findall(r" T (vpx_\w+)", out))
+    assert set(syms) <= exported
+
+
+def test_library_is_gfx950_code_object(pkg):
+    data = open(pkg.abi.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in data  # embedded offload bundle target
+
+
+def test_struct_layouts(pkg):
+    for s, size in pkg.abi.STRUCT_SIZES.items():
+        assert C.sizeof(s) == size, s
+
+
+def test_create_without_gpu_fails_cleanly(pkg):
+    torch = pytest.importorskip("torch")
+    if torch.cuda.device_count() > 0:
+        pytest.skip("a GPU is present")
+    lib = pkg.load_library()
+    h = C.c_void_p()
+    assert lib.vpx_create(0, C.byref(h)) == -2  # VPX_E_DEVICE, no abort
+    assert lib.vpx_destroy(None) == -1
+
+
+def test_host_helpers_reject_bad_arguments(pkg):
+    lib = pkg.load_library()
+    assert lib.vpx_camera_look_at(None, None, 0, 0, None) == -1
+    assert lib.vpx_default_materials(None) == -1
+    assert lib.vpx_tiles_packed_len(0, 10, 16, 16, 1) == 0
+    assert lib.vpx_tiles_packed_len(33, 17, 16, 16, 2) == 3 * 256  # 6 tiles over 2 ranks

@@ -1,0 +1,260 @@
+"""CPU suite: the oracle against known answers and golden fixtures, and the host logic.
+
+No GPU is needed.  Known answers come from (a) the published xorshift32 vector
+(Marsaglia 2003, seed 2463534242 -> 723471715), (b) the reference's own .vox decoder
+output (tests/golden/*.npz via lib/ogt_vox.h) and the per-asset histograms recorded in
+SURVEY.md §8(c), and (c) hand-derived DDA / slab / OffsetRay cases worked out from the
+reference formulas in the docstrings.  The trace path as a whole is "parity unpinned"
+against the reference: there is no reference output to pin it to.
+"""
+import ctypes as C
+import os
+import subprocess
+import tempfile
+
+import numpy as np
+import pytest
+
+from cases import bits
+
+REF = "/root/reference"
+
+
+def f32(x):
+    return np.float32(x)
+
+
+# ------------------------------------------------------------------------------ RNG
+def test_xorshift32_published_vector(orc, abi):
+    lib = orc._lib(abi)
+    s = C.c_uint32(2463534242)
+    assert lib.oracle_xorshift32(C.byref(s)) == 723471715
+
+
+def test_random_float_range_quirk(orc, abi):
+    """RandomFloat = u * 2.3283064365387e-10f reaches exactly 1.0 for u >= 2^32-128
+    (tmpl8math.cpp:130-133), so Rand(lightCount) can return lightCount -> directional."""
+    lib = orc._lib(abi)
+    s = C.c_uint32(0)
+    # find a state whose next output is 0xFFFFFFFF: invert xorshift is unnecessary — check
+    # the conversion directly
+    assert f32(np.float32(0xFFFFFFFF) * f32(2.3283064365387e-10)) == f32(1.0)
+    s = C.c_uint32(1)
+    vals = [lib.oracle_random_float(C.byref(s)) for _ in range(1000)]
+    assert min(vals) >= 0.0 and max(vals) <= 1.0
+
+
+def wang_py(s):
+    m = 0xFFFFFFFF
+    s = (s ^ 61) ^ (s >> 16)
+    s = (s * 9) & m
+    s = s ^ (s >> 4)
+    s = (s * 0x27D4EB2D) & m
+    return s ^ (s >> 15)
+
+
+def test_wang_hash_and_pixel_seed(orc, pkg, abi):
+    lib = orc._lib(abi)
+    vlib = pkg.load_library()
+    rng = np.random.default_rng(0)
+    for s in rng.integers(0, 2**32, 2000, dtype=np.uint64):
+        assert lib.oracle_wang_hash(int(s)) == wang_py(int(s))
+    for _ in range(500):
+        b, f, w, h = (int(v) for v in rng.integers(0, 4000, 4))
+        w, h = w + 1, h + 1
+        x, y = int(rng.integers(0, w)), int(rng.integers(0, h))
+        k = (b + f * (w * h) + y * w + x) & 0xFFFFFFFF
+        want = (0x12345678 + wang_py(((k + 1) * 17) & 0xFFFFFFFF)) & 0xFFFFFFFF
+        assert lib.oracle_pixel_seed(b, f, w, h, x, y) == want
+        assert vlib.vpx_pixel_seed(b, f, w, h, x, y) == want  # the library's host copy
+
+
+# ---------------------------------------------------------------------- geometry KATs
+def test_cube_intersect_known_answers(orc, abi):
+    lib = orc._lib(abi)
+    F = lambda *v: (C.c_float * 3)(*v)
+    b0, b1 = F(0, 0, 0), F(1, 1, 1)
+    # from (-1, .5, .5) along +x: enters at t = 1
+    assert lib.oracle_cube_intersect(b0, b1, F(-1, .5, .5), F(1, 0, 0), F(1, np.inf, np.inf)) == 1.0
+    # missing ray
+    assert lib.oracle_cube_intersect(b0, b1, F(-1, 2, .5), F(1, 0, 0), F(1, np.inf, np.inf)) == f32(1e34)
+    # origin inside: tmin < 0 -> 1e34 (scene.cpp:198-201)
+    assert lib.oracle_cube_intersect(b0, b1, F(.5, .5, .5), F(1, 0, 0), F(1, np.inf, np.inf)) == f32(1e34)
+    # pointing away
+    assert lib.oracle_cube_intersect(b0, b1, F(2, .5, .5), F(1, 0, 0), F(1, np.inf, np.inf)) == f32(1e34)
+
+
+def test_offset_ray_known_answers(orc, abi):
+    lib = orc._lib(abi)
+    out = (C.c_float * 3)()
+    p, n = np.array([1.0, 2.0, -3.0], np.float32), np.array([0.0, 1.0, -1.0], np.float32)
+    lib.oracle_offset_ray((C.c_float * 3)(*p), (C.c_float * 3)(*n), out)
+    o = np.array(out[:], np.float32)
+    # |p| >= 1/32: integer nudge by int(256*n) ulps away from zero along n's sign
+    assert o[0] == p[0]
+    assert o.view(np.int32)[1] == p.view(np.int32)[1] + 256
+    assert o.view(np.int32)[2] == p.view(np.int32)[2] + 256  # p<0 and n<0: -(-256)
+    p2 = np.array([0.01, -0.02, 0.0], np.float32)
+    lib.oracle_offset_ray((C.c_float * 3)(*p2), (C.c_float * 3)(*n), out)
+    o2 = np.array(out[:], np.float32)
+    assert o2[1] == f32(p2[1] + f32(1 / 65536) * n[1]) and o2[2] == f32(p2[2] + f32(1 / 65536) * n[2])
+
+
+def single_voxel_scene(pkg, n=8, at=(5, 3, 3), mat=20):
+    sc = pkg.scene
+    desc = sc.model_scene("monu3", 8, 8, 8, 0)
+    g = np.full(n ** 3, 255, np.uint8)
+    g[at[0] + at[1] * n + at[2] * n * n] = mat
+    desc.grids = [sc.GridSpec(n=n, dense=g)]
+    return desc
+
+
+def test_dda_single_voxel_known_answer(pkg, orc):
+    """N=8 grid, one voxel at (5,3,3).  Ray from (-0.5, 3.5/8, 3.5/8) along +x enters the
+    cube at t=0.5, steps x-cells 0..5 (6 cells) and hits cell 5 at its entry plane,
+    t = 0.5 + 5/8 = 1.125, normal (-1,0,0) (GetNormalVoxel: I.x = 5 exactly)."""
+    desc = single_voxel_scene(pkg)
+    o = orc.Oracle(pkg.abi, desc)
+    rays = pkg.context.make_rays([[-0.5, 3.5 / 8, 3.5 / 8]], [[1, 0, 0]])
+    h = pkg.context.hits_to_numpy(o.find_nearest(rays), 1)[0]
+    assert h["t"] == f32(1.125) and h["cells"] == 6 and h["material"] == 20 and h["vox_index"] == 0
+    assert tuple(h["normal"]) == (-1.0, 0.0, 0.0)
+    # the same ray bounded before the voxel does not hit; occlusion respects the bound
+    r2 = pkg.context.make_rays([[-0.5, 3.5 / 8, 3.5 / 8]], [[1, 0, 0]], tmax=1.0)
+    assert pkg.context.hits_to_numpy(o.find_nearest(r2), 1)[0]["material"] == 255
+    occ, cells = o.is_occluded(r2)
+    assert occ[0] == 0
+    occ, cells = o.is_occluded(pkg.context.make_rays([[-0.5, 3.5 / 8, 3.5 / 8]], [[1, 0, 0]], tmax=2.0))
+    assert occ[0] == 1 and cells[0] == 6
+    # negative direction from the far side: enters at x=1 (t=0.5), cells 7,6,5 -> t=0.5+2/8
+    r3 = pkg.context.make_rays([[1.5, 3.5 / 8, 3.5 / 8]], [[-1, 0, 0]])
+    h3 = pkg.context.hits_to_numpy(o.find_nearest(r3), 1)[0]
+    assert h3["t"] == f32(0.75) and h3["cells"] == 3 and tuple(h3["normal"]) == (1.0, 0.0, 0.0)
+
+
+def test_dda_tie_and_diagonal(pkg, orc):
+    """A diagonal ray through cell corners: ties in tmax pick z over x/y (x<y ? (x<z ? x
+    : z) : (y<z ? y : z), scene.cpp:773-802); the walk must still terminate and agree on
+    a second evaluation (determinism)."""
+    desc = single_voxel_scene(pkg, at=(4, 4, 4))
+    o = orc.Oracle(pkg.abi, desc)
+    rays = pkg.context.make_rays([[0.0, 0.0, 0.0]] * 2, [[1, 1, 1]] * 2)
+    h = pkg.context.hits_to_numpy(o.find_nearest(rays), 2)
+    assert h[0]["material"] == 20 and bits(h["t"])[0] == bits(h["t"])[1]
+
+
+# ---------------------------------------------------------------- worlds / fixtures
+SURVEY_HIST = {  # SURVEY.md §8(c)(i), recorded from ogt_vox in the survey container
+    "teapot": {8: 28411},
+    "monu3": {1: 31, 31: 271, 41: 9, 45: 4096, 57: 2695, 59: 7149, 63: 16},
+    "roomGlass": {1: 79548, 8: 453, 246: 627, 254: 42, 255: 12},
+}
+
+
+@pytest.mark.parametrize("name", sorted(SURVEY_HIST))
+def test_golden_models_match_survey_histograms(pkg, name):
+    size, vox, pal = pkg.scene.load_model(name)
+    assert vox.size == int(np.prod(size)) and pal.shape == (256, 4)
+    vals, counts = np.unique(vox[vox > 0], return_counts=True)
+    assert dict(zip(vals.tolist(), counts.tolist())) == SURVEY_HIST[name]
+
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(REF, "lib", "ogt_vox.h")), reason="reference tree absent")
+@pytest.mark.parametrize("name", sorted(SURVEY_HIST))
+def test_golden_models_regenerate_from_reference_decoder(pkg, name):
+    """Re-decode with the reference's own ogt_vox (oracle/_ref) and compare to the fixture."""
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    tool = os.path.join(repo, "oracle", "_ref", "ogt_ref_dump")
+    if not os.path.exists(tool):
+        subprocess.run(["make", "-s", "-C", os.path.join(repo, "oracle"), "ref"], check=True)
+    with tempfile.TemporaryDirectory() as td:
+        out = os.path.join(td, "m.bin")
+        subprocess.run([tool, os.path.join(REF, "assets", name + ".vox"), out], check=True)
+        raw = open(out, "rb").read()
+    size, vox, pal = pkg.scene.load_model(name)
+    assert np.array_equal(np.frombuffer(raw, np.uint32, 3, 4), size)
+    assert np.array_equal(np.frombuffer(raw, np.uint8, 1024, 16).reshape(256, 4), pal)
+    assert np.array_equal(np.frombuffer(raw, np.uint8, -1, 16 + 1024), vox)
+
+
+@pytest.mark.parametrize("name,n", [("teapot", 128), ("teapot", 64), ("roomGlass", 128), ("monu3", 48)])
+def test_load_model_placement_two_restatements(pkg, orc, name, n):
+    """scene.load_model_grid (numpy, product host code) == oracle_load_model (C)."""
+    size, vox, _ = pkg.scene.load_model(name)
+    a = pkg.scene.load_model_grid(size, vox, n)
+    lib = orc._lib(pkg.abi)
+    b = np.empty(n ** 3, np.uint8)
+    one = (C.c_float * 3)(1, 1, 1)
+    lib.oracle_load_model(np.ascontiguousarray(vox).ctypes.data, int(size[0]), int(size[1]), int(size[2]), n, one,
+                          b.ctypes.data)
+    assert np.array_equal(a, b)
+    if size[0] <= n and max(size) <= n:  # no downscale, no clipping: every voxel placed
+        assert np.count_nonzero(a != 255) == np.count_nonzero((vox > 0) & (vox < 255))  # 255 == NONE
+
+
+@pytest.mark.parametrize("name,n", [("monu3", 96), ("roomGlass", 130)])
+def test_tiled_world_two_restatements(pkg, orc, name, n):
+    spec, _, _ = pkg.scene.tiled_grid(name, n)
+    a = pkg.scene._tiled_numpy(spec)
+    o = orc.Oracle.__new__(orc.Oracle)
+    o.lib = orc._lib(pkg.abi)
+    b = o.host_grid(spec)
+    assert np.array_equal(a, b)
+    assert (b.reshape(n, n, n)[:, :2, :] == 0).all()  # ground slab
+    lib = o.lib
+    cs = lib.oracle_grid_checksum(b.ctypes.data, b.size)
+    ref = 0
+    idx = np.arange(b.size, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        x = idx + np.uint64(0x9E3779B97F4A7C15)
+        x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        x = x ^ (x >> np.uint64(31))
+        ref = int(np.sum((b.astype(np.uint64) + np.uint64(1)) * x, dtype=np.uint64))
+    assert cs == ref
+
+
+# --------------------------------------------------------------- oracle behaviour
+def test_oracle_thread_count_invariance(pkg, orc):
+    desc = pkg.scene.model_scene("roomGlass", 64, 48, 32, 4, city_lights=True)
+    o = orc.Oracle(pkg.abi, desc)
+    a1, r1, s1 = o.render(desc.frame_params(0), threads=1)
+    a8, r8, s8 = o.render(desc.frame_params(0), threads=7)
+    assert np.array_equal(bits(a1), bits(a8)) and np.array_equal(r1, r8)
+    assert (s1.shadow_rays, s1.dda_cells) == (s8.shadow_rays, s8.dda_cells)
+    ids = np.arange(5 * 48, 9 * 48)
+    sub, _ = o.render_pixels(desc.frame_params(0), ids, threads=3)
+    assert np.array_equal(bits(sub), bits(a1[ids]))
+
+
+def test_depth0_glass_is_black_and_casts_no_shadow(pkg, orc):
+    """C0's teapot is palette index 8 = GLASS: at depth 0 every hit returns
+    Trace(-1) * color = 0 and no shadow ray is cast."""
+    desc = pkg.scene.model_scene("teapot", 128, 64, 36, 0)
+    acc, rgb, st = orc.Oracle(pkg.abi, desc).render(desc.frame_params(0))
+    sky = np.array(pkg.abi.SKY_DEFAULT, np.float32)
+    hit = ~(acc[:, :3] == sky).all(1)
+    assert hit.any() and (acc[hit, :3] == 0).all() and st.shadow_rays == 0
+
+
+def test_camera_and_transform_helpers(pkg):
+    sc = pkg.scene
+    cam = sc.look_at((0.5, 0.35, -0.6), (0.5, 0.2, 0.3), 640, 360)
+    r, u = np.array(cam.right[:]), np.array(cam.up[:])
+    assert abs(np.dot(r, u)) < 1e-6 and abs(np.linalg.norm(r) - 1) < 1e-6
+    tl, tr = np.array(cam.top_left[:]), np.array(cam.top_right[:])
+    assert np.allclose(np.linalg.norm(tr - tl), 2 * 640 / 360, atol=1e-5)
+    v = sc.volume()
+    assert np.array_equal(np.array(v.matrix[:]), np.eye(4, dtype=np.float32).reshape(-1))
+    assert np.array_equal(np.array(v.inv_matrix[:]), np.eye(4, dtype=np.float32).reshape(-1))
+    v2 = sc.volume((0.2, 0.1, 0.0), (0.5, 0.5, 0.5), (0.3, 0.2, 0.1))
+    m = np.array(v2.matrix[:], np.float64).reshape(4, 4)
+    inv = np.array(v2.inv_matrix[:], np.float64).reshape(4, 4)
+    assert np.allclose(m @ inv, np.eye(4), atol=1e-5)  # uniform scale: inverse is exact-ish
+
+
+def test_default_materials_table(pkg):
+    m = pkg.scene.default_materials()
+    assert tuple(m[8].albedo) == (1.0, 0.5, 1.0) and m[8].ior == np.float32(1.45)
+    assert [m[i].emissive for i in range(9, 15)] == [3, 8, 12, 15, 16, 22]
+    assert m[15].emissive == 5 and m[2].roughness == np.float32(0.25) and m[100].roughness == 1.0
