@@ -1,11 +1,9 @@
 // vpx_kernels.hip — gfx950 kernels and the C-ABI of libvpx_hip.so (include/vpx.h).
 //
 // Kernels:
-//   render_tiles<LEVELS, PACKED>  one lane per pixel, 16x16-pixel tiles per 256-thread
-//                                 workgroup (four 16x4 wave strips), XCD-grouped tile order;
-//                                 primary ray -> Trace -> accumulate -> tonemap -> RGB8 in one
-//                                 pass (PACKED=false) or the raw sample into a rank's packed
-//                                 tile buffer (PACKED=true, multi-GPU).
+//   k_nearest / k_shade / k_shadow / k_finish   the frame as a wavefront of small kernels
+//                                 per bounce level (vpx_wavefront.hpp); one lane per pixel,
+//                                 16x16-pixel tiles per 256-thread workgroup (16x4 wave strips)
 //   composite_tiles               rank-0 unpack + accumulate + tonemap of gathered tiles.
 //   find_nearest_k / is_occluded_k / trace_k   per-ray unit entries.
 //   tiled_world_k / checksum_k    world generator and grid checksum.
@@ -13,147 +11,19 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
 
-#include "vpx_trace.hpp"
+#include "vpx_persist.hpp"
 
 using namespace vpx;
 
 namespace {
 
-constexpr int kTile = 16;  // 16x16 pixels per workgroup
+constexpr int kTile = 16;  // 16x16 pixels per tile / 256-thread workgroup
 constexpr int kThreads = 256;
-
-struct FrameArgs {
-    vpx_camera cam;
-    uint32_t width, height;
-    int32_t max_bounces;
-    uint32_t frame_index;
-    uint32_t seed_base;
-    uint32_t flags;
-    float aa;
-    float weight;      // 1/(n+1)
-    float inv_weight;  // 1 - weight
-    uint32_t tiles_x, tiles_y, num_tiles;
-    uint32_t rank, n_ranks;
-    uint32_t tiles_per_rank;
-};
-
-// --------------------------------------------------------------- primary rays
-// Camera::GetPrimaryRayNoDOF (camera.h:103-110) / GetPrimaryRay + thin lens (:68-83);
-// AA jitter as the AVX path: fma(rand, aa, x) (renderer.cpp:1699-1708).
-__device__ __forceinline__ Ray primary_ray(const FrameArgs& f, uint32_t x, uint32_t y, Rng& g) {
-    float fx = (float)x, fy = (float)y;
-    if (f.flags & VPX_FLAG_AA) {
-        const float rx = g.next(), ry = g.next();
-        fx = fmaf(rx, f.aa, fx);
-        fy = fmaf(ry, f.aa, fy);
-    }
-    const float u = fx * __fdiv_rn(1.0f, (float)f.width);
-    const float v = fy * __fdiv_rn(1.0f, (float)f.height);
-    const f3 tl = ld3(f.cam.top_left), tr = ld3(f.cam.top_right), bl = ld3(f.cam.bottom_left);
-    const f3 P = (tl + (tr - tl) * u) + (bl - tl) * v;
-    const f3 cp = ld3(f.cam.cam_pos);
-    if (f.flags & VPX_FLAG_DOF) {
-        const float rr = sqrtf(g.next());
-        const float theta = g.next() * (2.0f * kPi);
-        const float cx = cr_cos(theta) * rr, cy = cr_sin(theta) * rr;
-        const float jx = __fdiv_rn(cx * f.cam.defocus_jitter, (float)f.width);
-        const float jy = __fdiv_rn(cy * f.cam.defocus_jitter, (float)f.width);
-        const f3 focal = cp + normalize(P - cp) * f.cam.focal_distance;
-        const f3 o = (cp + ld3(f.cam.right) * jx) + ld3(f.cam.up) * jy;
-        return make_ray(o, focal - o);
-    }
-    return make_ray(cp, P - cp);
-}
-
-// GetLuminance / ApplyReinhardJodie / RGBF32_to_RGB8 (renderer.cpp:2222-2240,
-// template/precomp.h:372-388).
-__device__ __forceinline__ uint32_t tonemap_pack(float4 a) {
-    const f3 c = mk(a.x, a.y, a.z);
-    const float lum = dot(c, mk(0.2126f, 0.7152f, 0.0722f));
-    const f3 rh = c / mk(1.0f + c.x, 1.0f + c.y, 1.0f + c.z);
-    const f3 la = c / (1.0f + lum);
-    const float o0 = la.x + rh.x * (rh.x - la.x);
-    const float o1 = la.y + rh.y * (rh.y - la.y);
-    const float o2 = la.z + rh.z * (rh.z - la.z);
-    const uint32_t r = (uint32_t)(int64_t)(255.0f * smin(1.0f, o0));
-    const uint32_t gg = (uint32_t)(int64_t)(255.0f * smin(1.0f, o1));
-    const uint32_t b = (uint32_t)(int64_t)(255.0f * smin(1.0f, o2));
-    return (r << 16) + (gg << 8) + b;
-}
-
-// Running-average blend of the AVX path: fma(1-w, acc, px*w) (renderer.cpp:1797-1828).
-__device__ __forceinline__ float4 blend(float4 acc, f3 px, float w, float iw) {
-    return make_float4(fmaf(iw, acc.x, px.x * w), fmaf(iw, acc.y, px.y * w), fmaf(iw, acc.z, px.z * w),
-                       fmaf(iw, acc.w, 0.0f * w));
-}
-
-__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
-
-// One 64-bit atomic per counter per wave: [0] shadow rays, [1] FindNearest calls,
-// [2] DDA cells, [3] primary rays.
-__device__ __forceinline__ void flush_counters(Counters k, uint32_t primary, unsigned long long* ctr) {
-    const uint32_t sh = wave_sum(k.shadow), ne = wave_sum(k.nearest), ce = wave_sum(k.cells);
-    const uint32_t pr = wave_sum(primary);
-    if ((threadIdx.x & 63) == 0) {
-        atomicAdd(&ctr[0], (unsigned long long)sh);
-        atomicAdd(&ctr[1], (unsigned long long)ne);
-        atomicAdd(&ctr[2], (unsigned long long)ce);
-        atomicAdd(&ctr[3], (unsigned long long)pr);
-    }
-}
-
-// XCD-grouped workgroup order: hardware deals consecutive workgroups round-robin over the
-// 8 XCDs; hand each XCD a contiguous run of tiles so neighbouring tiles (which walk the
-// same voxels) share that XCD's L2.  Speed only — any mapping is correct.
-__device__ __forceinline__ uint32_t xcd_remap(uint32_t b, uint32_t nb) {
-    const uint32_t full = nb & ~7u;
-    if (b >= full) return b;
-    const uint32_t per = full >> 3;
-    return (b & 7u) * per + (b >> 3);
-}
-
-template <int LEVELS, bool PACKED>
-__global__ __launch_bounds__(kThreads) void render_tiles(SceneView sv, FrameArgs f, float4* __restrict__ accum,
-                                                         uint32_t* __restrict__ rgb8, float4* __restrict__ packed,
-                                                         unsigned long long* __restrict__ ctr) {
-    const uint32_t nb = gridDim.x;
-    const uint32_t j = xcd_remap(blockIdx.x, nb);  // this rank's j-th tile
-    const uint32_t tile = PACKED ? f.rank + j * f.n_ranks : j;
-    Counters k{0u, 0u, 0u};
-    // wave w of the workgroup takes rows 4w..4w+3 of the 16x16 tile (16x4 strip)
-    const uint32_t lx = threadIdx.x & 15u, ly = threadIdx.x >> 4;
-    const uint32_t x = (tile % f.tiles_x) * kTile + lx;
-    const uint32_t y = (tile / f.tiles_x) * kTile + ly;
-    const bool valid = tile < f.num_tiles && x < f.width && y < f.height;
-    f3 v = mk(0.f, 0.f, 0.f);
-    if (valid) {
-        Rng g{pixel_seed(f.seed_base, f.frame_index, f.width, f.height, x, y)};
-        const Ray r = primary_ray(f, x, y, g);
-        v = trace_path<LEVELS>(sv, r, f.max_bounces, g, k);
-    }
-    if (PACKED) {
-        if (j < f.tiles_per_rank)
-            packed[(uint64_t)j * (kTile * kTile) + threadIdx.x] = make_float4(v.x, v.y, v.z, 0.0f);
-    } else if (valid) {
-        const uint64_t p = (uint64_t)y * f.width + x;
-        if (f.flags & VPX_FLAG_NO_TONEMAP) {
-            accum[p] = make_float4(v.x, v.y, v.z, 0.0f);
-        } else {
-            const float4 a = blend(accum[p], v, f.weight, f.inv_weight);
-            accum[p] = a;
-            if (rgb8) rgb8[p] = tonemap_pack(a);
-        }
-    }
-    flush_counters(k, valid ? 1u : 0u, ctr);
-}
 
 __global__ __launch_bounds__(kThreads) void composite_tiles(FrameArgs f, const float4* __restrict__ gathered,
                                                             float4* __restrict__ accum, uint32_t* __restrict__ rgb8) {
@@ -230,8 +100,8 @@ __global__ void focus_k(SceneView sv, FrameArgs f, float* out) {
         const DevGrid g = sv.grids[vol.grid_id];
         Dda s;
         if (!dda_setup(vol, g.n, o, s)) continue;
-        const WalkResult w = dda_walk<kNearest>(g, s, r.t, cells);
-        if (w.hit) r.t = w.t;
+        skip::Walk w = to_walk(s);
+        if (skip::walk_skip(grid_view(g), w, r.t, cells)) r.t = w.t;
     }
     *out = smax(-1.0f, smin(r.t, 1e4f));
 }
@@ -271,6 +141,45 @@ __global__ void tiled_world_k(uint8_t* __restrict__ out, uint32_t n, const uint8
     }
 }
 
+// ------------------------------------------------------------- occupancy masks
+// l1: one thread per 4x4x4 brick reads its 64 cells (16 rows of 4 bytes).
+__global__ void build_l1_k(const uint8_t* __restrict__ cells, uint32_t n, uint32_t nb1, uint64_t* __restrict__ l1) {
+    const uint64_t total = (uint64_t)nb1 * nb1 * nb1;
+    const uint64_t n64 = n;
+    for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b < total; b += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t bx = (uint32_t)(b % nb1), by = (uint32_t)((b / nb1) % nb1), bz = (uint32_t)(b / ((uint64_t)nb1 * nb1));
+        uint64_t m = 0;
+        for (uint32_t lz = 0; lz < 4; ++lz)
+            for (uint32_t ly = 0; ly < 4; ++ly) {
+                const uint32_t y = by * 4 + ly, z = bz * 4 + lz;
+                if (y >= n || z >= n) continue;
+                const uint8_t* row = cells + (uint64_t)y * n64 + (uint64_t)z * n64 * n64;
+                for (uint32_t lx = 0; lx < 4; ++lx) {
+                    const uint32_t x = bx * 4 + lx;
+                    if (x < n && row[x] != kNone) m |= 1ull << (lx + 4 * ly + 16 * lz);
+                }
+            }
+        l1[b] = m;
+    }
+}
+
+// l2: one thread per 16^3 macro ORs its 64 child brick masks into one bit each.
+__global__ void build_l2_k(const uint64_t* __restrict__ l1, uint32_t nb1, uint32_t nb2, uint64_t* __restrict__ l2) {
+    const uint64_t total = (uint64_t)nb2 * nb2 * nb2;
+    for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < total; c += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t cx = (uint32_t)(c % nb2), cy = (uint32_t)((c / nb2) % nb2), cz = (uint32_t)(c / ((uint64_t)nb2 * nb2));
+        uint64_t m = 0;
+        for (uint32_t lz = 0; lz < 4; ++lz)
+            for (uint32_t ly = 0; ly < 4; ++ly)
+                for (uint32_t lx = 0; lx < 4; ++lx) {
+                    const uint32_t bx = cx * 4 + lx, by = cy * 4 + ly, bz = cz * 4 + lz;
+                    if (bx >= nb1 || by >= nb1 || bz >= nb1) continue;
+                    if (l1[(uint64_t)bx + (uint64_t)by * nb1 + (uint64_t)bz * nb1 * nb1]) m |= 1ull << (lx + 4 * ly + 16 * lz);
+                }
+        l2[c] = m;
+    }
+}
+
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
     x += 0x9e3779b97f4a7c15ull;
     x = (x ^ (x >> 30)) * 0xbf58476d1ce4e5b9ull;
@@ -298,7 +207,10 @@ struct vpx_ctx {
     std::string err;
     struct GridBuf {
         uint8_t* ptr = nullptr;
-        uint32_t n = 0;
+        uint64_t* l1 = nullptr;
+        uint64_t* l2 = nullptr;
+        uint64_t* l3 = nullptr;
+        uint32_t n = 0, nb1 = 0, nb2 = 0, nb3 = 0;
     };
     std::vector<GridBuf> grids;
     DevGrid* d_grids = nullptr;
@@ -321,6 +233,16 @@ struct vpx_ctx {
     void* d_scratch = nullptr;
     size_t scratch_bytes = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
+    // wavefront path state (vpx_wavefront.hpp), grown on demand
+    void* d_wave = nullptr;
+    size_t wave_bytes = 0;
+    WaveBufs wave{};
+    uint32_t* shadow_list = nullptr;  // [S*P] compact shadow work list
+    uint32_t* next_list = nullptr;    // [P] next level's active paths
+    uint32_t* ctl = nullptr;          // [4 + 4*L] work-list lengths / counters, zeroed per frame
+    uint32_t ctl_words = 0;
+    int persist_blocks = 0;           // resident 256-thread workgroups for persistent kernels
+    bool persistent = false;          // single-volume scenes: persistent DDA kernels (VPX_PERSIST=1 enables)
 };
 
 namespace {
@@ -380,7 +302,10 @@ int sync_grids(vpx_ctx* c) {
         c->d_grids_cap = n;
     }
     std::vector<DevGrid> h(n);
-    for (uint32_t i = 0; i < n; ++i) h[i] = DevGrid{c->grids[i].ptr, c->grids[i].n, 0};
+    for (uint32_t i = 0; i < n; ++i) {
+        const auto& g = c->grids[i];
+        h[i] = DevGrid{g.ptr, g.l1, g.l2, g.l3, g.n, g.nb1, g.nb2, g.nb3};
+    }
     if (n) VPX_HIP(c, hipMemcpy(c->d_grids, h.data(), sizeof(DevGrid) * n, hipMemcpyHostToDevice));
     return VPX_OK;
 }
@@ -434,22 +359,119 @@ int validate_frame(vpx_ctx* c, const vpx_frame_params* p) {
         return fail(c, VPX_E_INVALID, "frame size out of range");
     if (p->max_bounces < -1 || p->max_bounces > kMaxLevels - 2)
         return fail(c, VPX_E_INVALID, "max_bounces must be in [-1, 14]");
-    if (p->area_samples < 0 || p->area_samples > 1024) return fail(c, VPX_E_INVALID, "area_samples out of range");
+    if (p->area_samples < 0 || p->area_samples > 15) return fail(c, VPX_E_INVALID, "area_samples must be in [0, 15]");
     if (!c->have_camera) return fail(c, VPX_E_STATE, "no camera set (vpx_set_camera)");
     return check_ready(c);
 }
 
+// Carve the wavefront buffers for P paths, L levels and S shadow slots out of one
+// device allocation (grown on demand; never inside a capture).
+int ensure_wave(vpx_ctx* c, uint32_t P, uint32_t L, uint32_t S) {
+    const size_t f4 = sizeof(float4);
+    const size_t bytes = (size_t)P * (f4 * (5 + 2 * (size_t)L + 3 * (size_t)S + 1) + 3 * sizeof(uint32_t)) +
+                         sizeof(uint32_t) * ((size_t)S * P + P + 4 + 4 * (size_t)L) + 16 * 256;
+    if (bytes > c->wave_bytes) {
+        if (c->d_wave) {
+            VPX_HIP(c, hipStreamSynchronize(c->stream));
+            (void)hipFree(c->d_wave);
+        }
+        c->d_wave = nullptr;
+        c->wave_bytes = 0;
+        VPX_HIP(c, hipMalloc(&c->d_wave, bytes));
+        c->wave_bytes = bytes;
+    }
+    char* q = (char*)c->d_wave;
+    auto take = [&](size_t n) {
+        char* r = q;
+        q += (n + 255) & ~(size_t)255;
+        return (void*)r;
+    };
+    WaveBufs& w = c->wave;
+    w.P = P;
+    w.S = S;
+    w.O = (float4*)take(f4 * P);
+    w.D = (float4*)take(f4 * P);
+    w.H = (float4*)take(f4 * P);
+    w.leaf = (float4*)take(f4 * P);
+    w.SM = (float4*)take(f4 * P);
+    w.LA = (float4*)take(f4 * P * (size_t)L);
+    w.LB = (float4*)take(f4 * P * (size_t)L);
+    w.SO = (float4*)take(f4 * P * (size_t)S);
+    w.SD = (float4*)take(f4 * P * (size_t)S);
+    w.SL = (float4*)take(f4 * P * (size_t)S);
+    w.HM = (uint32_t*)take(4 * (size_t)P);
+    w.depth = (int32_t*)take(4 * (size_t)P);
+    w.forms = (uint32_t*)take(4 * (size_t)P);
+    c->shadow_list = (uint32_t*)take(4 * (size_t)S * P);
+    c->next_list = (uint32_t*)take(4 * (size_t)P);
+    c->ctl_words = 4 + 4 * L;
+    c->ctl = (uint32_t*)take(4 * (size_t)c->ctl_words);
+    return VPX_OK;
+}
+
+// Workgroups of the persistent kernels: what the occupancy calculator admits per CU x CUs.
+int persist_grid(vpx_ctx* c) {
+    if (c->persist_blocks) return c->persist_blocks;
+    int per_cu = 0, cus = 0;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, c->device) == hipSuccess) cus = prop.multiProcessorCount;
+    int a = 0, b = 0, d = 0;
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, reinterpret_cast<const void*>(&k_nearest1<true>), kThreads, 0);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, reinterpret_cast<const void*>(&k_nearest1<false>), kThreads, 0);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&d, reinterpret_cast<const void*>(&k_shadow1), kThreads, 0);
+    per_cu = std::max(1, std::min(a, std::min(b, d)));
+    c->persist_blocks = std::max(1, per_cu * std::max(1, cus));
+    return c->persist_blocks;
+}
+
+// The frame: nearest(first) -> [shade -> shadow (-> resolve) -> nearest]* -> finish, all
+// on c->stream.  Single-volume scenes take the persistent lane-refilling DDA kernels fed
+// by compact work lists; N-volume scenes the per-path kernels of vpx_wavefront.hpp.
 template <bool PACKED>
-void launch_render(vpx_ctx* c, const SceneView& sv, const FrameArgs& f, uint32_t blocks, float4* accum,
-                   uint32_t* rgb8, float4* packed) {
-    const dim3 grid(blocks), block(kThreads);
-    if (f.max_bounces <= 0)
-        hipLaunchKernelGGL((render_tiles<1, PACKED>), grid, block, 0, c->stream, sv, f, accum, rgb8, packed, c->d_ctr);
-    else if (f.max_bounces <= 4)
-        hipLaunchKernelGGL((render_tiles<5, PACKED>), grid, block, 0, c->stream, sv, f, accum, rgb8, packed, c->d_ctr);
-    else
-        hipLaunchKernelGGL((render_tiles<kMaxLevels, PACKED>), grid, block, 0, c->stream, sv, f, accum, rgb8, packed,
+int launch_render(vpx_ctx* c, const SceneView& sv, const FrameArgs& f, uint32_t tiles, float4* accum, uint32_t* rgb8,
+                  float4* packed) {
+    const uint32_t P = tiles * (uint32_t)kTilePix;
+    const uint32_t L = (uint32_t)std::max(1, f.max_bounces + 1);
+    const uint32_t S = (uint32_t)std::max(1, sv.area_samples);
+    int rc = ensure_wave(c, P, L, S);
+    if (rc) return rc;
+    const WaveBufs w = c->wave;
+    const dim3 grid(tiles), block(kThreads);
+    if (sv.num_volumes == 1 && c->persistent) {
+        OneVolume ov;
+        ov.vol = c->volumes[0];
+        const auto& gb = c->grids[ov.vol.grid_id];
+        ov.g = DevGrid{gb.ptr, gb.l1, gb.l2, gb.l3, gb.n, gb.nb1, gb.nb2, gb.nb3};
+        const dim3 pgrid(persist_grid(c));
+        uint32_t* ctl = c->ctl;
+        VPX_HIP(c, hipMemsetAsync(ctl, 0, sizeof(uint32_t) * c->ctl_words, c->stream));
+        hipLaunchKernelGGL((k_nearest1<true>), pgrid, block, 0, c->stream, sv, ov, f, w, nullptr, nullptr, ctl,
                            c->d_ctr);
+        for (int level = 0; level <= f.max_bounces; ++level) {
+            uint32_t* lc = ctl + 4 + 4 * level;  // [0] shadow len [1] shadow ctr [2] next len [3] next ctr
+            const bool more = level < f.max_bounces;
+            hipLaunchKernelGGL(k_shade, grid, block, 0, c->stream, sv, f, w, level, c->d_ctr, c->shadow_list, lc + 0,
+                               more ? c->next_list : nullptr, lc + 2);
+            hipLaunchKernelGGL(k_shadow1, pgrid, block, 0, c->stream, sv, ov, w, c->shadow_list, lc + 0, lc + 1,
+                               c->d_ctr);
+            hipLaunchKernelGGL(k_resolve, grid, block, 0, c->stream, sv, w);
+            if (more)
+                hipLaunchKernelGGL((k_nearest1<false>), pgrid, block, 0, c->stream, sv, ov, f, w, c->next_list,
+                                   lc + 2, lc + 3, c->d_ctr);
+        }
+    } else {
+        hipLaunchKernelGGL((k_nearest<true>), grid, block, 0, c->stream, sv, f, w, c->d_ctr);
+        for (int level = 0; level <= f.max_bounces; ++level) {
+            hipLaunchKernelGGL(k_shade, grid, block, 0, c->stream, sv, f, w, level, c->d_ctr, nullptr, nullptr,
+                               nullptr, nullptr);
+            hipLaunchKernelGGL(k_shadow, grid, block, 0, c->stream, sv, w, c->d_ctr);
+            if (level < f.max_bounces)
+                hipLaunchKernelGGL((k_nearest<false>), grid, block, 0, c->stream, sv, f, w, c->d_ctr);
+        }
+    }
+    hipLaunchKernelGGL((k_finish<PACKED>), grid, block, 0, c->stream, f, w, accum, rgb8, packed);
+    VPX_HIP(c, hipGetLastError());
+    return VPX_OK;
 }
 
 int snapshot_counters(vpx_ctx* c, unsigned long long out[4]) {
@@ -492,6 +514,7 @@ int vpx_create(int device, vpx_ctx** out) {
     }
     c->stream = c->own_stream;
     (void)hipMemset(c->d_ctr, 0, 4 * sizeof(unsigned long long));
+    if (const char* e = std::getenv("VPX_PERSIST")) c->persistent = std::atoi(e) != 0;
     *out = c;
     return VPX_OK;
 }
@@ -500,10 +523,14 @@ int vpx_destroy(vpx_ctx* c) {
     if (!c) return VPX_E_INVALID;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    for (auto& g : c->grids)
+    for (auto& g : c->grids) {
         if (g.ptr) (void)hipFree(g.ptr);
+        if (g.l1) (void)hipFree(g.l1);
+        if (g.l2) (void)hipFree(g.l2);
+        if (g.l3) (void)hipFree(g.l3);
+    }
     void* ptrs[] = {c->d_grids, c->d_volumes, c->d_materials, c->d_points, c->d_spots, c->d_areas,
-                    c->d_spheres, c->d_triangles, c->d_ctr, c->d_sum, c->d_scratch};
+                    c->d_spheres, c->d_triangles, c->d_ctr, c->d_sum, c->d_scratch, c->d_wave};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -538,11 +565,35 @@ static int alloc_grid(vpx_ctx* c, uint32_t id, uint32_t n) {
     if (g.ptr && g.n != n) {
         VPX_HIP(c, hipStreamSynchronize(c->stream));
         (void)hipFree(g.ptr);
-        g.ptr = nullptr;
+        (void)hipFree(g.l1);
+        (void)hipFree(g.l2);
+        (void)hipFree(g.l3);
+        g.ptr = nullptr, g.l1 = nullptr, g.l2 = nullptr, g.l3 = nullptr;
     }
-    if (!g.ptr) VPX_HIP(c, hipMalloc(&g.ptr, bytes));
     g.n = n;
+    g.nb1 = (n + 3) / 4;
+    g.nb2 = (g.nb1 + 3) / 4;
+    g.nb3 = (g.nb2 + 3) / 4;
+    if (!g.ptr) {
+        VPX_HIP(c, hipMalloc(&g.ptr, bytes));
+        VPX_HIP(c, hipMalloc(&g.l1, sizeof(uint64_t) * (size_t)g.nb1 * g.nb1 * g.nb1));
+        VPX_HIP(c, hipMalloc(&g.l2, sizeof(uint64_t) * (size_t)g.nb2 * g.nb2 * g.nb2));
+        VPX_HIP(c, hipMalloc(&g.l3, sizeof(uint64_t) * (size_t)g.nb3 * g.nb3 * g.nb3));
+    }
     return sync_grids(c);
+}
+
+// Rebuild the occupancy hierarchy after the grid bytes changed.
+static int build_masks(vpx_ctx* c, uint32_t id) {
+    auto& g = c->grids[id];
+    hipLaunchKernelGGL(build_l1_k, dim3(2048), dim3(256), 0, c->stream, g.ptr, g.n, g.nb1, g.l1);
+    VPX_HIP(c, hipGetLastError());
+    hipLaunchKernelGGL(build_l2_k, dim3(512), dim3(256), 0, c->stream, g.l1, g.nb1, g.nb2, g.l2);
+    VPX_HIP(c, hipGetLastError());
+    hipLaunchKernelGGL(build_l2_k, dim3(64), dim3(256), 0, c->stream, g.l2, g.nb2, g.nb3, g.l3);  // same OR-reduction one level up
+    VPX_HIP(c, hipGetLastError());
+    VPX_HIP(c, hipStreamSynchronize(c->stream));
+    return VPX_OK;
 }
 
 int vpx_upload_grid(vpx_ctx* c, uint32_t id, const uint8_t* cells, uint32_t n) {
@@ -550,7 +601,7 @@ int vpx_upload_grid(vpx_ctx* c, uint32_t id, const uint8_t* cells, uint32_t n) {
     int rc = alloc_grid(c, id, n);
     if (rc) return rc;
     VPX_HIP(c, hipMemcpy(c->grids[id].ptr, cells, (size_t)n * n * n, hipMemcpyHostToDevice));
-    return VPX_OK;
+    return build_masks(c, id);
 }
 
 int vpx_generate_tiled_grid(vpx_ctx* c, uint32_t id, uint32_t n, const uint8_t* model, uint32_t mx, uint32_t my,
@@ -568,7 +619,7 @@ int vpx_generate_tiled_grid(vpx_ctx* c, uint32_t id, uint32_t n, const uint8_t* 
     VPX_HIP(c, hipGetLastError());
     VPX_HIP(c, hipStreamSynchronize(c->stream));
     (void)hipFree(dm);
-    return VPX_OK;
+    return build_masks(c, id);
 }
 
 int vpx_grid_checksum(vpx_ctx* c, uint32_t id, uint64_t* out) {
@@ -658,8 +709,7 @@ int vpx_render(vpx_ctx* c, const vpx_frame_params* p, float* accum, uint32_t* rg
     const SceneView sv = view_of(c, p->sky, p->area_samples);
     const FrameArgs f = frame_of(c, p, 0, 1);
     if (stats) VPX_HIP(c, hipEventRecord(c->ev0, c->stream));
-    launch_render<false>(c, sv, f, f.num_tiles, reinterpret_cast<float4*>(accum), rgb8, nullptr);
-    VPX_HIP(c, hipGetLastError());
+    if ((rc = launch_render<false>(c, sv, f, f.num_tiles, reinterpret_cast<float4*>(accum), rgb8, nullptr))) return rc;
     if (stats) {
         VPX_HIP(c, hipEventRecord(c->ev1, c->stream));
         unsigned long long after[4];
@@ -693,8 +743,8 @@ int vpx_render_tiles(vpx_ctx* c, const vpx_frame_params* p, uint32_t tile_w, uin
     const SceneView sv = view_of(c, p->sky, p->area_samples);
     const FrameArgs f = frame_of(c, p, rank, n_ranks);
     if (stats) VPX_HIP(c, hipEventRecord(c->ev0, c->stream));
-    launch_render<true>(c, sv, f, f.tiles_per_rank, nullptr, nullptr, reinterpret_cast<float4*>(packed));
-    VPX_HIP(c, hipGetLastError());
+    if ((rc = launch_render<true>(c, sv, f, f.tiles_per_rank, nullptr, nullptr, reinterpret_cast<float4*>(packed))))
+        return rc;
     if (stats) {
         VPX_HIP(c, hipEventRecord(c->ev1, c->stream));
         unsigned long long after[4];

@@ -1,0 +1,415 @@
+// vpx_skip.hpp — exact empty-space skipping for the reference DDA (host + device).
+//
+// The reference march (Scene::FindNearest / IsOccluded, template/scene.cpp:751-811,
+// 1009-1047) advances three float accumulators tmax.{x,y,z} += tdelta one cell at a time
+// and always steps the axis with the smallest head (ties: z, then y, then x —
+// `x<y ? (x<z ? x : z) : (y<z ? y : z)`).  The visited cells, the t of the first solid
+// cell and the number of cells visited are therefore a pure function of the three
+// sequences A(i+1) = fl(A(i) + d) and of their merge in (value, z>y>x) order.
+//
+// Inside one binade [2^E, 2^(E+1)) every A(i) is a multiple of u = 2^(E-23), and as long
+// as the exact sum stays below 2^(E+1), fl(A + d) = A + c*u with c = d/u rounded to the
+// nearest integer (no tie).  So A(k) and "how many A(i) lie below T" are O(1) per binade
+// instead of O(k) — exactly, bit for bit.  Ties, stagnation, non-positive or non-finite
+// values fall back to single IEEE additions (or to the cell-by-cell march).
+//
+// walk_skip() uses that to cross boxes of empty cells (empty 16^3 macros and 64^3
+// super-bricks of the occupancy hierarchy) in one jump: it finds the merged event that
+// leaves the box, counts the events before it per axis, and lands on the reference state
+// just before that event, adding the skipped cells to the count.  Cells in non-empty
+// macros are marched one by one.  Results equal the cell-by-cell march exactly.
+#pragma once
+
+#include <stdint.h>
+
+#ifndef __HIP_DEVICE_COMPILE__
+#include <cstring>
+#endif
+
+#if defined(__HIPCC__)
+#define VPX_HD __host__ __device__ __forceinline__
+#else
+#define VPX_HD inline
+#endif
+
+namespace vpx {
+namespace skip {
+
+VPX_HD uint32_t fbits(float f) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __float_as_uint(f);
+#else
+    uint32_t u;
+    std::memcpy(&u, &f, 4);
+    return u;
+#endif
+}
+VPX_HD float bitsf(uint32_t u) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __uint_as_float(u);
+#else
+    float f;
+    std::memcpy(&f, &u, 4);
+    return f;
+#endif
+}
+
+// Exact a / b for a, b < 2^26, b >= 1, given rb ~ 1/b within 2^-20 relative.  The device
+// has no integer divider: two reciprocal-multiply estimates plus one integer correction.
+VPX_HD uint32_t udiv_rcp(uint32_t a, uint32_t b, float rb) {
+    int32_t q = (int32_t)((float)a * rb);
+    int32_t r = (int32_t)a - q * (int32_t)b;  // |r| < 16 b
+    q += (int32_t)((float)r * rb);
+    r = (int32_t)a - q * (int32_t)b;  // |r| < 2 b
+    if (r < 0) q -= 1, r += (int32_t)b;
+    if (r < 0) q -= 1, r += (int32_t)b;
+    if (r >= (int32_t)b) q += 1, r -= (int32_t)b;
+    if (r >= (int32_t)b) q += 1;
+    return (uint32_t)q;
+}
+
+VPX_HD uint32_t udiv(uint32_t a, uint32_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return udiv_rcp(a, b, __builtin_amdgcn_rcpf((float)b));
+#else
+    return a / b;
+#endif
+}
+
+// Closed-form segment of A(i+1) = fl(A(i) + d) starting at A > 0 (normal, finite):
+// A = b*2^(E-23) with b in [2^23, 2^24).  ok=false: this step must be a plain addition.
+struct Seg {
+    uint32_t b;      // integer significand of A
+    uint32_t c;      // increment in ulps
+    uint32_t m;      // closed-form steps available in this binade (>= 1 when ok)
+    uint32_t ebits;  // biased exponent of A
+    bool ok;
+    bool stuck;      // fl(A + d) == A forever
+};
+
+VPX_HD Seg segment(float a, float d) {
+    Seg s{0u, 0u, 0u, 0u, false, false};
+    const uint32_t ab = fbits(a), db = fbits(d);
+    const uint32_t ea = ab >> 23, ed = db >> 23;  // sign bits are 0 (callers ensure a,d > 0)
+    if (ea == 0 || ea >= 255 || ed == 0 || ed >= 255) return s;  // zero/denormal/inf/nan: single step
+    s.ebits = ea;
+    s.b = (ab & 0x7fffffu) | 0x800000u;
+    const uint32_t md = (db & 0x7fffffu) | 0x800000u;
+    if (ed >= ea) return s;  // d >= 2^E: at most a few steps per binade, do them one by one
+    const uint32_t sh = ea - ed;  // >= 1
+    if (sh > 25) {                // d < u/2: A + d rounds back to A (md < 2^24 <= 2^(sh-1))
+        s.ok = true;
+        s.stuck = true;
+        return s;
+    }
+    uint32_t c = md >> sh;
+    const uint32_t rem = md & ((1u << sh) - 1u), half = 1u << (sh - 1);
+    if (rem == half) return s;  // exact tie: rounding alternates with parity -> single step
+    if (rem > half) ++c;
+    if (c == 0) {
+        s.ok = true;
+        s.stuck = true;
+        return s;
+    }
+    // step i -> i+1 is closed-form while b + (i+1)*c <= 2^24 - 1 (exact sum < 2^(E+1))
+    const uint32_t room = 0xffffffu - s.b;
+    s.m = udiv(room, c);
+    if (s.m == 0) return s;
+    s.c = c;
+    s.ok = true;
+    return s;
+}
+
+VPX_HD float seg_value(uint32_t b, uint32_t ebits) {
+    // b may have reached 2^24 only through an exact closed-form landing below 2^24 - 1,
+    // so it is still a valid significand of this binade.
+    return bitsf((ebits << 23) | (b & 0x7fffffu));
+}
+
+// A(k): k accumulations of d onto a (a, d > 0).  Exact.  With a cap, returns early with
+// some A(j) > cap (j <= k) once the sequence exceeds it (then A(k) > cap too).
+VPX_HD float jump(float a, float d, uint32_t k, float cap = 3.4e38f) {
+    float A = a;
+    while (k > 0) {
+        if (!(A < 3.0e38f) || A > cap) return A;  // inf stays inf; beyond the cap
+        const Seg s = segment(A, d);
+        if (!s.ok) {
+            A = A + d;
+            --k;
+            continue;
+        }
+        if (s.stuck) return A;
+        const uint32_t st = k < s.m ? k : s.m;
+        A = seg_value(s.b + st * s.c, s.ebits);
+        k -= st;
+    }
+    return A;
+}
+
+// #{ i in [0, kmax) : A(i) < T }  (strict)  or  A(i) <= T  (!strict).  Exact.
+VPX_HD uint32_t count_below(float a, float d, float T, bool strict, uint32_t kmax) {
+    float A = a;
+    uint32_t i = 0;
+    while (i < kmax) {
+        const bool below = strict ? (A < T) : (A <= T);
+        if (!below) return i;
+        if (!(A < 3.0e38f)) return kmax;  // A = inf <= T = inf: every later term equal
+        const Seg s = segment(A, d);
+        if (!s.ok) {
+            A = A + d;
+            ++i;
+            continue;
+        }
+        if (s.stuck) return kmax;  // constant and below T forever
+        // A(i+j) = (b + j c) u for j = 0..m.  Smallest j >= 1 with A(i+j) not below T.
+        const uint32_t left = kmax - i;
+        const uint32_t lim = left < s.m ? left : s.m;
+        const uint32_t tb = fbits(T);
+        uint32_t jj = 0xffffffffu;
+        if ((tb >> 23) == s.ebits) {  // T in the same binade: T = t*u with integer t
+            const uint32_t t = (tb & 0x7fffffu) | 0x800000u;  // t > b (A < T) or t >= b
+            // strict: b + j c >= t ; non-strict: b + j c > t
+            const uint32_t need = strict ? udiv(t - s.b + s.c - 1u, s.c) : udiv(t - s.b, s.c) + 1u;
+            jj = need;
+        } else if ((tb >> 23) < s.ebits || (tb >> 31)) {
+            jj = 1;  // cannot happen (A below T), kept for safety
+        }
+        if (jj <= lim) return i + jj;
+        A = seg_value(s.b + lim * s.c, s.ebits);
+        i += lim;
+    }
+    return kmax;
+}
+
+// count_below plus the sequence values around the stop: returns n, sets Aend = A(n) and
+// Aprev = A(n-1) (Aprev unspecified when n == 0).
+VPX_HD uint32_t count_below2(float a, float d, float T, bool strict, uint32_t kmax, float& Aend, float& Aprev) {
+    float A = a, P = a;
+    uint32_t i = 0;
+    while (i < kmax) {
+        const bool below = strict ? (A < T) : (A <= T);
+        if (!below) break;
+        if (!(A < 3.0e38f)) {  // inf: constant from here on
+            P = A;
+            i = kmax;
+            break;
+        }
+        const Seg s = segment(A, d);
+        if (!s.ok) {
+            P = A;
+            A = A + d;
+            ++i;
+            continue;
+        }
+        if (s.stuck) {
+            P = A;
+            i = kmax;
+            break;
+        }
+        const uint32_t left = kmax - i;
+        const uint32_t lim = left < s.m ? left : s.m;
+        const uint32_t tb = fbits(T);
+        uint32_t jj = 0xffffffffu;
+        if ((tb >> 23) == s.ebits) {
+            const uint32_t t = (tb & 0x7fffffu) | 0x800000u;
+            jj = strict ? udiv(t - s.b + s.c - 1u, s.c) : udiv(t - s.b, s.c) + 1u;
+        }
+        const uint32_t st = jj <= lim ? jj : lim;  // st >= 1
+        P = seg_value(s.b + (st - 1u) * s.c, s.ebits);
+        A = seg_value(s.b + st * s.c, s.ebits);
+        i += st;
+        if (jj <= lim) break;
+    }
+    Aend = A;
+    Aprev = P;
+    return i;
+}
+
+}  // namespace skip
+}  // namespace vpx
+
+namespace vpx {
+namespace skip {
+
+// A grid as the skipping walker sees it: the MatType bytes and the occupancy hierarchy
+// l1 (4^3 bricks: cell bits), l2 (16^3 macros: brick bits), l3 (64^3 supers: macro bits).
+struct GridView {
+    const uint8_t* cells;
+    const uint64_t* l1;
+    const uint64_t* l2;
+    const uint64_t* l3;
+    uint32_t n, nb1, nb2, nb3;
+};
+
+struct Walk {
+    uint32_t X, Y, Z;
+    float t, tx, ty, tz;
+    float dx, dy, dz;
+    int32_t sx, sy, sz;
+    uint32_t k1, k2, k3;
+    uint64_t m1, m2, m3;
+};
+
+VPX_HD uint32_t pack3(uint32_t a, uint32_t b, uint32_t c) { return a | (b << 11) | (c << 22); }
+
+// 0: solid cell, 1: empty cell, 2: inside an empty 16^3 macro, 3: inside an empty 64^3 super.
+VPX_HD int classify(Walk& w, const GridView& g) {
+    const uint32_t X = w.X, Y = w.Y, Z = w.Z;
+    const uint32_t k3 = pack3(X >> 6, Y >> 6, Z >> 6);
+    if (k3 != w.k3) {
+        w.k3 = k3;
+        w.m3 = g.l3[(uint64_t)(X >> 6) + (uint64_t)(Y >> 6) * g.nb3 + (uint64_t)(Z >> 6) * ((uint64_t)g.nb3 * g.nb3)];
+    }
+    if (w.m3 == 0) return 3;
+    const uint32_t mb = ((X >> 4) & 3u) | (((Y >> 4) & 3u) << 2) | (((Z >> 4) & 3u) << 4);
+    if (!((w.m3 >> mb) & 1ull)) return 2;
+    const uint32_t k2 = pack3(X >> 4, Y >> 4, Z >> 4);
+    if (k2 != w.k2) {
+        w.k2 = k2;
+        w.m2 = g.l2[(uint64_t)(X >> 4) + (uint64_t)(Y >> 4) * g.nb2 + (uint64_t)(Z >> 4) * ((uint64_t)g.nb2 * g.nb2)];
+    }
+    const uint32_t bb = ((X >> 2) & 3u) | (((Y >> 2) & 3u) << 2) | (((Z >> 2) & 3u) << 4);
+    if (!((w.m2 >> bb) & 1ull)) return 1;
+    const uint32_t k1 = pack3(X >> 2, Y >> 2, Z >> 2);
+    if (k1 != w.k1) {
+        w.k1 = k1;
+        w.m1 = g.l1[(uint64_t)(X >> 2) + (uint64_t)(Y >> 2) * g.nb1 + (uint64_t)(Z >> 2) * ((uint64_t)g.nb1 * g.nb1)];
+    }
+    const uint32_t cb = (X & 3u) | ((Y & 3u) << 2) | ((Z & 3u) << 4);
+    return ((w.m1 >> cb) & 1ull) ? 0 : 1;
+}
+
+// One reference step (scene.cpp:773-802), branch-free; false = left the grid.
+VPX_HD bool step1(Walk& w, uint32_t n) {
+    const bool xy = w.tx < w.ty, xz = w.tx < w.tz, yz = w.ty < w.tz;
+    const bool ax = xy && xz;
+    const bool ay = !xy && yz;
+    const bool az = !(ax || ay);
+    w.t = ax ? w.tx : (ay ? w.ty : w.tz);
+    w.X += ax ? (uint32_t)w.sx : 0u;
+    w.Y += ay ? (uint32_t)w.sy : 0u;
+    w.Z += az ? (uint32_t)w.sz : 0u;
+    w.tx = ax ? w.tx + w.dx : w.tx;
+    w.ty = ay ? w.ty + w.dy : w.ty;
+    w.tz = az ? w.tz + w.dz : w.tz;
+    const uint32_t m = w.X > w.Y ? w.X : w.Y;
+    return (m > w.Z ? m : w.Z) < n;
+}
+
+// Cross the empty box [lo, hi] (per axis, inclusive) around the current cell.
+// 0: landed just before the event that leaves the box (cells += skipped visits);
+// 1: the walk ends inside the box (bound reached; cells += visits); 2: not applicable.
+VPX_HD int skip_box(Walk& w, const uint32_t lo[3], const uint32_t hi[3], float bound, uint32_t& cells) {
+    const float h[3] = {w.tx, w.ty, w.tz};
+    const float d[3] = {w.dx, w.dy, w.dz};
+    const int32_t s[3] = {w.sx, w.sy, w.sz};
+    const uint32_t c[3] = {w.X, w.Y, w.Z};
+    uint32_t e[3];
+    float approx[3];
+    for (int k = 0; k < 3; ++k) {
+        if (!(h[k] > 0.0f) || !(d[k] > 0.0f)) return 2;  // NaN, zero or negative: march instead
+        e[k] = s[k] > 0 ? hi[k] - c[k] + 1u : c[k] - lo[k] + 1u;
+        // A(e-1) ~ h + (e-1) d, relative error < (e+1) 2^-24 (<= 4e-6 for e <= 64)
+        approx[k] = e[k] > 1u ? h[k] + (float)(e[k] - 1u) * d[k] : h[k];
+    }
+    // leaving event = smallest A_k(e_k - 1), ties -> z, then y, then x.  Decide on the
+    // approximations when they are apart by more than their error; otherwise exactly.
+    float V[3], Vp[3];
+    bool exact[3] = {false, false, false};
+    int a = (approx[2] <= approx[0] && approx[2] <= approx[1]) ? 2 : (approx[1] <= approx[0] ? 1 : 0);
+    const float amin = approx[a];
+    bool close = false;
+    for (int k = 0; k < 3; ++k)
+        if (k != a && !(approx[k] > amin * 1.0001f)) close = true;
+    if (close) {
+        for (int k = 0; k < 3; ++k) {
+            count_below2(h[k], d[k], 3.4e38f, true, e[k] - 1u, V[k], Vp[k]);
+            exact[k] = true;
+        }
+        a = (V[2] <= V[0] && V[2] <= V[1]) ? 2 : (V[1] <= V[0] ? 1 : 0);
+    } else {
+        count_below2(h[a], d[a], 3.4e38f, true, e[a] - 1u, V[a], Vp[a]);
+        exact[a] = true;
+    }
+    const float vs = V[a];
+    uint32_t nk[3];
+    float head[3], prev[3];
+    for (int k = 0; k < 3; ++k) {
+        if (k == a) {
+            nk[k] = e[k] - 1u;
+            head[k] = V[k];
+            prev[k] = Vp[k];
+        } else {
+            // axis k precedes axis a on ties iff k > a (priority z=2 > y=1 > x=0)
+            nk[k] = count_below2(h[k], d[k], vs, k < a, e[k] - 1u, head[k], prev[k]);
+        }
+    }
+    if (vs < bound) {
+        float tl = w.t;
+        bool moved = false;
+        for (int k = 0; k < 3; ++k) {
+            if (nk[k] == 0) continue;
+            tl = moved ? (tl < prev[k] ? prev[k] : tl) : prev[k];
+            moved = true;
+        }
+        if (moved) w.t = tl;
+        w.tx = head[0], w.ty = head[1], w.tz = head[2];
+        w.X += nk[0] * (uint32_t)w.sx;
+        w.Y += nk[1] * (uint32_t)w.sy;
+        w.Z += nk[2] * (uint32_t)w.sz;
+        cells += nk[0] + nk[1] + nk[2];
+        return 0;
+    }
+    uint32_t v = 1u;
+    for (int k = 0; k < 3; ++k) v += count_below(h[k], d[k], bound, true, nk[k]);
+    cells += v;
+    return 1;
+}
+
+// Resumable form: at most `budget` loop iterations.  0 = not finished, 1 = solid cell
+// reached (w.t / w.X,Y,Z describe it), 2 = finished without a solid cell.
+VPX_HD int walk_skip_some(const GridView& g, Walk& w, float bound, uint32_t& cells, int budget) {
+    for (int it = 0; it < budget; ++it) {
+        if (!(w.t < bound)) return 2;
+        const int cls = classify(w, g);
+        if (cls == 0) {
+            ++cells;
+            return 1;
+        }
+        if (cls >= 2) {
+            const uint32_t m = cls == 3 ? 63u : 15u;
+            const uint32_t lo[3] = {w.X & ~m, w.Y & ~m, w.Z & ~m};
+            uint32_t hi[3] = {lo[0] + m, lo[1] + m, lo[2] + m};
+            for (int k = 0; k < 3; ++k) hi[k] = hi[k] < g.n - 1u ? hi[k] : g.n - 1u;
+            if (skip_box(w, lo, hi, bound, cells) == 1) return 2;
+        }
+        ++cells;
+        if (!step1(w, g.n)) return 2;
+    }
+    return 0;
+}
+
+// Scene::FindNearest (MODE nearest) / Scene::IsOccluded walk from an initialised state.
+// Returns true at the first solid cell (w.t / w.X,Y,Z describe it).  Exact.
+VPX_HD bool walk_skip(const GridView& g, Walk& w, float bound, uint32_t& cells) {
+    for (;;) {
+        if (!(w.t < bound)) return false;
+        const int cls = classify(w, g);
+        if (cls == 0) {
+            ++cells;
+            return true;
+        }
+        if (cls >= 2) {
+            const uint32_t m = cls == 3 ? 63u : 15u;
+            const uint32_t lo[3] = {w.X & ~m, w.Y & ~m, w.Z & ~m};
+            uint32_t hi[3] = {lo[0] + m, lo[1] + m, lo[2] + m};
+            for (int k = 0; k < 3; ++k) hi[k] = hi[k] < g.n - 1u ? hi[k] : g.n - 1u;
+            if (skip_box(w, lo, hi, bound, cells) == 1) return false;
+        }
+        ++cells;  // visit the (empty) current cell
+        if (!step1(w, g.n)) return false;
+    }
+}
+
+}  // namespace skip
+}  // namespace vpx

@@ -19,6 +19,7 @@
 #include <stdint.h>
 
 #include "../../include/vpx.h"
+#include "vpx_skip.hpp"
 
 namespace vpx {
 
@@ -28,10 +29,21 @@ constexpr float kBig = 1e34f;
 constexpr int kMaxLevels = 16;                     // max_bounces <= 14 -> 15 levels
 
 // ----------------------------------------------------------------------- device view
+// A voxel grid as the device walks it: the dense MatType bytes (x + y*N + z*N^2) plus a
+// two-level occupancy hierarchy built from them (build_masks): l1 = one 64-bit mask per
+// 4x4x4 brick (bit lx + 4ly + 16lz set <=> cell != NONE), l2 = one 64-bit mask per 16^3
+// macro brick (bit per child brick with a non-zero l1 mask).  The hierarchy only decides
+// WHETHER a cell must be read; the march still visits every cell in the reference order
+// with the reference float arithmetic, so t / cells / normals are unchanged.
 struct DevGrid {
     const uint8_t* cells;
+    const uint64_t* l1;
+    const uint64_t* l2;
+    const uint64_t* l3;
     uint32_t n;
-    uint32_t pad;
+    uint32_t nb1;  // bricks per axis  = ceil(n / 4)
+    uint32_t nb2;  // macros per axis  = ceil(nb1 / 4)
+    uint32_t nb3;  // supers per axis  = ceil(nb2 / 4)
 };
 
 struct SceneView {
@@ -243,6 +255,73 @@ __device__ __forceinline__ f3 normal_voxel(const ORay& r, float t, uint32_t n, c
     return normalize(xform_vec(nn, matrix));
 }
 
+__device__ __forceinline__ skip::GridView grid_view(const DevGrid& g) {
+    return skip::GridView{g.cells, g.l1, g.l2, g.l3, g.n, g.nb1, g.nb2, g.nb3};
+}
+__device__ __forceinline__ skip::Walk to_walk(const Dda& s) {
+    skip::Walk w;
+    w.X = s.X, w.Y = s.Y, w.Z = s.Z;
+    w.t = s.t;
+    w.tx = s.tmax.x, w.ty = s.tmax.y, w.tz = s.tmax.z;
+    w.dx = s.tdelta.x, w.dy = s.tdelta.y, w.dz = s.tdelta.z;
+    w.sx = s.sx, w.sy = s.sy, w.sz = s.sz;
+    w.k1 = w.k2 = w.k3 = 0xffffffffu;
+    w.m1 = w.m2 = w.m3 = 0ull;
+    return w;
+}
+
+// skip::walk_skip with wave-aware scheduling: each lane runs exactly the same sequence of
+// classify / skip_box / step1 as skip::walk_skip (so results are identical), but the long
+// skip_box is executed in batches — only when few lanes of the wave still want to take
+// plain cell steps — instead of inside every step iteration of the wave.
+constexpr uint32_t kStepThreshold = 16;
+
+__device__ __forceinline__ bool walk_wave(const skip::GridView& g, skip::Walk& w, float bound, uint32_t& cells) {
+    enum : int { kStep = 0, kSkip = 1, kMiss = 2, kHit = 3 };
+    int mode = kStep, pending = 0;
+    for (;;) {
+        for (;;) {
+            const uint64_t stepping = __ballot(mode == kStep);
+            if (!stepping) break;
+            if ((uint32_t)__popcll(stepping) < kStepThreshold && __ballot(mode == kSkip)) break;
+            if (mode == kStep) {
+                if (!(w.t < bound)) {
+                    mode = kMiss;
+                } else {
+                    const int cls = skip::classify(w, g);
+                    if (cls == 0) {
+                        ++cells;
+                        mode = kHit;
+                    } else if (cls >= 2) {
+                        mode = kSkip;
+                        pending = cls;
+                    } else {
+                        ++cells;
+                        if (!skip::step1(w, g.n)) mode = kMiss;
+                    }
+                }
+            }
+        }
+        if (!__ballot(mode == kSkip)) {
+            if (!__ballot(mode == kStep)) break;
+            continue;
+        }
+        if (mode == kSkip) {
+            const uint32_t m = pending == 3 ? 63u : 15u;
+            const uint32_t lo[3] = {w.X & ~m, w.Y & ~m, w.Z & ~m};
+            uint32_t hi[3] = {lo[0] + m, lo[1] + m, lo[2] + m};
+            for (int k = 0; k < 3; ++k) hi[k] = hi[k] < g.n - 1u ? hi[k] : g.n - 1u;
+            if (skip::skip_box(w, lo, hi, bound, cells) == 1) {
+                mode = kMiss;
+            } else {
+                ++cells;  // visit the landing cell, then take the leaving event
+                mode = skip::step1(w, g.n) ? kStep : kMiss;
+            }
+        }
+    }
+    return mode == kHit;
+}
+
 // Walk modes (all share the stepping of scene.cpp:773-802).
 enum WalkMode { kNearest = 0, kGlassExit = 1, kSmokeExit = 2, kOcclusion = 3 };
 
@@ -405,11 +484,11 @@ __device__ __forceinline__ int32_t find_nearest(const SceneView& sv, Ray& r, Cou
         const DevGrid g = sv.grids[vol.grid_id];
         Dda s;
         if (!dda_setup(vol, g.n, o, s)) continue;
-        const WalkResult w = dda_walk<kNearest>(g, s, r.t, k.cells);
-        if (w.hit) {
+        skip::Walk w = to_walk(s);
+        if (walk_wave(grid_view(g), w, r.t, k.cells)) {
             r.t = w.t;
             r.N = normal_voxel(o, w.t, g.n, vol.matrix);
-            r.mat = w.cell;
+            r.mat = g.cells[(uint64_t)w.X + (uint64_t)w.Y * g.n + (uint64_t)w.Z * ((uint64_t)g.n * g.n)];
             vox = (int32_t)i;
         }
     }
@@ -439,7 +518,8 @@ __device__ __forceinline__ bool is_occluded(const SceneView& sv, const Ray& r, C
         const DevGrid g = sv.grids[vol.grid_id];
         Dda s;
         if (!dda_setup(vol, g.n, o, s)) continue;
-        if (dda_walk<kOcclusion>(g, s, r.t, k.cells).hit) return true;
+        skip::Walk w = to_walk(s);
+        if (walk_wave(grid_view(g), w, r.t, k.cells)) return true;  // first solid cell, t < bound
     }
     for (uint32_t i = 0; i < sv.num_spheres; ++i)
         if (sphere_is_hit(sv.spheres[i], r)) return true;

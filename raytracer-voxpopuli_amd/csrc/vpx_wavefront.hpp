@@ -1,0 +1,609 @@
+// vpx_wavefront.hpp — the per-frame render as a wavefront of small kernels.
+//
+// Renderer::Trace (renderer.cpp:1076-1328) is one chain per pixel.  Instead of one big
+// kernel that carries the whole chain (VGPR-heavy, 2 waves/SIMD), each bounce level runs
+//   nearest  — primary/bounce ray -> Renderer::FindNearest               (DDA, lean)
+//   shade    — material dispatch: RNG, next ray, light choice, and the shadow rays the
+//              light evaluation would cast, with their unoccluded contributions
+//   shadow   — Renderer::IsOccluded for those rays, then the light's sum    (DDA, lean)
+// and a final `finish` folds the per-level (a, b, form) records bottom-up exactly as the
+// recursion does and accumulates / tonemaps (or packs tiles for the multi-GPU gather).
+// The RNG is consumed only in `shade`, in the reference order, and no RNG draw depends on
+// an occlusion result (renderer.cpp:102-207 draw before they test), so splitting the
+// chain changes no value: results stay bit-identical to the restatement.
+//
+// Path state lives in HBM as structure-of-arrays float4 streams (coalesced 16-B lanes).
+#pragma once
+
+#include "vpx_trace.hpp"
+
+namespace vpx {
+
+constexpr int kTileW = 16;
+constexpr int kTilePix = kTileW * kTileW;
+
+// flags word of a path (stored in D.w)
+constexpr uint32_t kActive = 1u;
+constexpr uint32_t kInside = 2u;
+
+// shadow-slot flags (stored in SH_D.w)
+constexpr uint32_t kSlotValid = 1u;
+constexpr uint32_t kSlotDiscard = 2u;  // smoke player probe: traced for the count, result unused
+
+// light kinds of a level's pending incLight
+constexpr uint32_t kLightNone = 0, kLightSingle = 1, kLightArea = 2;
+
+struct FrameArgs {
+    vpx_camera cam;
+    uint32_t width, height;
+    int32_t max_bounces;
+    uint32_t frame_index;
+    uint32_t seed_base;
+    uint32_t flags;
+    float aa;
+    float weight;      // 1/(n+1)
+    float inv_weight;  // 1 - weight
+    uint32_t tiles_x, tiles_y, num_tiles;
+    uint32_t rank, n_ranks;
+    uint32_t tiles_per_rank;
+};
+
+struct WaveBufs {
+    float4* O;     // [P] ray origin, w = rng state bits
+    float4* D;     // [P] ray direction, w = flags bits (kActive | kInside)
+    float4* H;     // [P] hit: t, normal
+    uint32_t* HM;  // [P] hit: material | (vox + 2) << 8
+    int32_t* depth;  // [P] remaining Trace depth
+    uint32_t* forms; // [P] 2 bits per level + level count in bits 27..31
+    float4* LA;    // [L][P] level multiplier a (xyz)
+    float4* LB;    // [L][P] level addend b (xyz)
+    float4* leaf;  // [P] leaf radiance (sky / emissive / 0)
+    float4* SO;    // [S][P] shadow origin, w = tmax
+    float4* SD;    // [S][P] shadow direction, w = slot flags bits
+    float4* SL;    // [S][P] unoccluded contribution of the slot
+    float4* SM;    // [P] pending light: xyz = kd (area), w = bits(kind | discard<<3 | count<<4 | level<<8 | lc<<16)
+    uint32_t P;    // paths (pixels) this call
+    uint32_t S;    // shadow slots per path
+};
+
+// ------------------------------------------------------------------ primary rays
+// Camera::GetPrimaryRayNoDOF (camera.h:103-110) / GetPrimaryRay + thin lens (:68-83);
+// AA jitter as the AVX path: fma(rand, aa, x) (renderer.cpp:1699-1708).
+__device__ __forceinline__ Ray primary_ray(const FrameArgs& f, uint32_t x, uint32_t y, Rng& g) {
+    float fx = (float)x, fy = (float)y;
+    if (f.flags & VPX_FLAG_AA) {
+        const float rx = g.next(), ry = g.next();
+        fx = fmaf(rx, f.aa, fx);
+        fy = fmaf(ry, f.aa, fy);
+    }
+    const float u = fx * (1.0f / (float)f.width);
+    const float v = fy * (1.0f / (float)f.height);
+    const f3 tl = ld3(f.cam.top_left), tr = ld3(f.cam.top_right), bl = ld3(f.cam.bottom_left);
+    const f3 P = (tl + (tr - tl) * u) + (bl - tl) * v;
+    const f3 cp = ld3(f.cam.cam_pos);
+    if (f.flags & VPX_FLAG_DOF) {
+        const float rr = sqrtf(g.next());
+        const float theta = g.next() * (2.0f * kPi);
+        const float cx = cr_cos(theta) * rr, cy = cr_sin(theta) * rr;
+        const float jx = (cx * f.cam.defocus_jitter) / (float)f.width;
+        const float jy = (cy * f.cam.defocus_jitter) / (float)f.width;
+        const f3 focal = cp + normalize(P - cp) * f.cam.focal_distance;
+        const f3 o = (cp + ld3(f.cam.right) * jx) + ld3(f.cam.up) * jy;
+        return make_ray(o, focal - o);
+    }
+    return make_ray(cp, P - cp);
+}
+
+// Path index -> pixel: path p = j*256 + lane covers the j-th tile of this rank
+// (tile = rank + j*n_ranks), lane in row-major order inside the 16x16 tile, so one
+// wave owns a 16x4 strip of neighbouring pixels.
+__device__ __forceinline__ bool path_pixel(const FrameArgs& f, uint32_t p, uint32_t& x, uint32_t& y) {
+    const uint32_t j = p >> 8, lane = p & 255u;
+    const uint32_t tile = f.rank + j * f.n_ranks;
+    x = (tile % f.tiles_x) * kTileW + (lane & 15u);
+    y = (tile / f.tiles_x) * kTileW + (lane >> 4);
+    return tile < f.num_tiles && x < f.width && y < f.height;
+}
+
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// One 64-bit atomic per counter per wave: [0] shadow rays, [1] FindNearest calls,
+// [2] DDA cells, [3] primary rays.
+__device__ __forceinline__ void flush_counters(const Counters& k, uint32_t primary, unsigned long long* ctr) {
+    const uint32_t sh = wave_sum(k.shadow), ne = wave_sum(k.nearest), ce = wave_sum(k.cells);
+    const uint32_t pr = wave_sum(primary);
+    if ((threadIdx.x & 63) == 0) {
+        if (sh) atomicAdd(&ctr[0], (unsigned long long)sh);
+        if (ne) atomicAdd(&ctr[1], (unsigned long long)ne);
+        if (ce) atomicAdd(&ctr[2], (unsigned long long)ce);
+        if (pr) atomicAdd(&ctr[3], (unsigned long long)pr);
+    }
+}
+
+// ------------------------------------------------------------------- stage 1
+// FIRST: generate the primary ray (and the pixel's RNG state) and mark the path active.
+template <bool FIRST>
+__global__ __launch_bounds__(256) void k_nearest(SceneView sv, FrameArgs f, WaveBufs w, unsigned long long* ctr) {
+    const uint32_t p = blockIdx.x * 256u + threadIdx.x;
+    Counters k{0u, 0u, 0u};
+    uint32_t prim = 0;
+    if (p < w.P) {
+        Ray r;
+        uint32_t rng, flags;
+        bool go;
+        if (FIRST) {
+            uint32_t x, y;
+            go = path_pixel(f, p, x, y);
+            flags = go ? kActive : 0u;
+            w.depth[p] = f.max_bounces;
+            w.forms[p] = 0u;
+            if (go) {
+                Rng g{pixel_seed(f.seed_base, f.frame_index, f.width, f.height, x, y)};
+                r = primary_ray(f, x, y, g);
+                rng = g.s;
+                prim = 1;
+            } else {
+                rng = 0;
+                r.O = r.D = mk(0.f, 0.f, 0.f);
+                r.inside = false;
+            }
+            w.leaf[p] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (f.max_bounces < 0) {  // Trace(ray, -1) returns 0 without a lookup
+                flags = 0u;
+                go = false;
+            }
+        } else {
+            const float4 o = w.O[p], d = w.D[p];
+            flags = __float_as_uint(d.w);
+            go = (flags & kActive) != 0u;
+            r.O = mk(o.x, o.y, o.z);
+            r.D = mk(d.x, d.y, d.z);
+            r.inside = (flags & kInside) != 0u;
+            rng = __float_as_uint(o.w);
+        }
+        if (go) {
+            r.t = kBig;
+            r.mat = kNone;
+            r.N = mk(0.f, 0.f, 0.f);
+            const int32_t vox = find_nearest(sv, r, k);
+            w.H[p] = make_float4(r.t, r.N.x, r.N.y, r.N.z);
+            w.HM[p] = r.mat | ((uint32_t)(vox + 2) << 8) | (r.inside ? 0x80000000u : 0u);
+        }
+        if (FIRST) {
+            w.O[p] = make_float4(r.O.x, r.O.y, r.O.z, __uint_as_float(rng));
+            w.D[p] = make_float4(r.D.x, r.D.y, r.D.z, __uint_as_float(flags));
+        }
+    }
+    flush_counters(k, prim, ctr);
+}
+
+// ------------------------------------------------------------------- stage 2
+__device__ __forceinline__ void put_slot(const WaveBufs& w, uint32_t s, uint32_t p, f3 o, f3 d, float tmax, f3 val,
+                                         uint32_t fl) {
+    const uint64_t i = (uint64_t)s * w.P + p;
+    w.SO[i] = make_float4(o.x, o.y, o.z, tmax);
+    w.SD[i] = make_float4(d.x, d.y, d.z, __uint_as_float(fl));
+    w.SL[i] = make_float4(val.x, val.y, val.z, 0.f);
+}
+
+// Renderer::Illumination (renderer.cpp:738-764) up to the IsOccluded calls: draws the
+// light index (and the area-light sample directions), computes each shadow ray exactly as
+// the evaluators build it, and the contribution it adds when unoccluded.  Returns the
+// pending-light word; discard = the smoke player probe (result thrown away).
+__device__ __forceinline__ uint32_t emit_illumination(const SceneView& sv, const Ray& r, Rng& g, const WaveBufs& w,
+                                                      uint32_t p, bool discard, f3& kd_out, uint32_t& slots) {
+    const uint64_t pc = sv.num_points, scn = sv.num_spots, ac = sv.num_areas;
+    const uint64_t lc = pc + scn + ac + 1;
+    const uint64_t idx = (uint64_t)(g.next() * (float)lc);
+    const f3 ip = ray_point(r);
+    const f3 n = r.N;
+    const f3 kd = albedo(sv, r.mat);
+    kd_out = kd;
+    const uint32_t extra = discard ? kSlotDiscard : 0u;
+    uint32_t kind = kLightSingle, count = 0;
+    if (idx < pc) {  // PointLightEvaluate :102-131
+        const vpx_point_light& l = sv.points[idx];
+        const f3 dir = ld3(l.position) - ip;
+        const float dst = length(dir);
+        const f3 dn = dir * (1.0f / dst);
+        const float c = dot(dn, n);
+        if (!(c <= 0.0f)) {
+            const f3 li = (ld3(l.color) * smax(0.0f, c)) * (1.0f / (dst * dst));
+            const Ray sh = make_ray(offset_ray(ip, n), dn);
+            put_slot(w, 0, p, sh.O, sh.D, dst, li * kd, kSlotValid | extra);
+            count = 1;
+            slots |= 1u;
+        }
+    } else if (idx < ac + pc) {  // AreaLightEvaluation :161-207
+        const vpx_area_light& l = sv.areas[idx - pc];
+        const f3 center = ld3(l.position);
+        const float radius = l.radius;
+        const f3 point = offset_ray(ip, n);
+        kind = kLightArea;
+        count = (uint32_t)sv.area_samples;
+        for (int i = 0; i < sv.area_samples; ++i) {  // count <= 15 slots (API caps area_samples)
+            f3 rp = random_direction(g);
+            rp = rp * radius;
+            rp = rp + center;
+            const f3 dir = rp - ip;
+            const float dst = length(dir);
+            const f3 dn = dir * (1.0f / dst);
+            const float c = dot(dn, n);
+            if (c <= 0) {
+                put_slot(w, i, p, mk(0.f, 0.f, 0.f), mk(0.f, 0.f, 0.f), 0.f, mk(0.f, 0.f, 0.f), 0u);
+                continue;
+            }
+            f3 li = ld3(l.color) * c;
+            li = li * l.color_multiplier;
+            li = li * (radius * radius);
+            li = li * kPi;
+            li = li * 4.0f;
+            li = li / (dst * dst);
+            const Ray sh = make_ray(point, dn);
+            put_slot(w, i, p, sh.O, sh.D, dst, li, kSlotValid | extra);
+            slots |= 1u << i;
+        }
+    } else if (idx < ac + scn + pc) {  // SpotLightEvaluate :133-159
+        const vpx_spot_light& l = sv.spots[idx - ac - pc];
+        const f3 dir = ld3(l.position) - ip;
+        const float dst = length(dir);
+        const f3 dn = dir / dst;
+        const float c = dot(dn, ld3(l.direction));
+        if (!(c <= l.angle)) {
+            const float alpha = 1.0f - ((1.0f - c) * 1.0f) / (1.0f - l.angle);
+            const f3 li = (ld3(l.color) * smax(0.0f, c)) / (dst * dst);
+            const Ray sh = make_ray(offset_ray(ip, n), dn);
+            put_slot(w, 0, p, sh.O, sh.D, dst, (li * kd) * alpha, kSlotValid | extra);
+            count = 1;
+            slots |= 1u;
+        }
+    } else {  // DirectionalLightEvaluate :315-338
+        const f3 dir = -ld3(sv.dir.direction);
+        const float c = dot(dir, n);
+        if (!(c <= 0)) {
+            const f3 li = ld3(sv.dir.color) * smax(0.0f, c);
+            const Ray sh = make_ray(offset_ray(ip, n), dir);
+            put_slot(w, 0, p, sh.O, sh.D, kBig, li * kd, kSlotValid | extra);
+            count = 1;
+            slots |= 1u;
+        }
+    }
+    return kind | (discard ? 8u : 0u) | (count << 4) | ((uint32_t)lc << 16);
+}
+
+// One Trace level of the material switch (renderer.cpp:1100-1327) for an active path.
+// Exclusive wave prefix sum (inclusive scan by shuffles, minus self).
+__device__ __forceinline__ uint32_t wave_prefix(uint32_t v, uint32_t& total) {
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= (uint32_t)o) x += y;
+    }
+    total = __shfl(x, 63, 64);
+    return x - v;
+}
+
+// Append `cnt` entries per lane to a device list with one atomic per wave.
+__device__ __forceinline__ uint32_t wave_append(uint32_t cnt, uint32_t* len) {
+    uint32_t total;
+    const uint32_t off = wave_prefix(cnt, total);
+    uint32_t base = 0;
+    if ((threadIdx.x & 63u) == 0 && total) base = atomicAdd(len, total);
+    base = __shfl(base, 0, 64);
+    return base + off;
+}
+
+// shadow_list / next_list (optional): compact work lists for the persistent DDA kernels
+// (entry = slot << 27 | path for shadows, path for the next level's FindNearest).
+__global__ __launch_bounds__(256) void k_shade(SceneView sv, FrameArgs f, WaveBufs w, int level,
+                                               unsigned long long* ctr, uint32_t* shadow_list, uint32_t* shadow_len,
+                                               uint32_t* next_list, uint32_t* next_len) {
+    const uint32_t p = blockIdx.x * 256u + threadIdx.x;
+    Counters k{0u, 0u, 0u};
+    uint32_t slots = 0;
+    bool next_active = false;
+    if (p < w.P) {
+        float4 od = w.D[p];
+        uint32_t flags = __float_as_uint(od.w);
+        uint32_t pending = 0;  // SM word; 0 = no light sample this level
+        if (flags & kActive) {
+            const float4 oo = w.O[p];
+            const float4 hh = w.H[p];
+            const uint32_t hm = w.HM[p];
+            Ray ray;
+            ray.O = mk(oo.x, oo.y, oo.z);
+            ray.D = mk(od.x, od.y, od.z);
+            ray.t = hh.x;
+            ray.N = mk(hh.y, hh.z, hh.w);
+            ray.mat = hm & 0xffu;
+            ray.inside = (hm & 0x80000000u) != 0u;
+            const int32_t vox = (int32_t)((hm >> 8) & 0xffffu) - 2;
+            Rng g{__float_as_uint(oo.w)};
+            int depth = w.depth[p];
+            uint32_t forms = w.forms[p];
+            const uint32_t nl = forms >> 27;
+            bool done = false;
+            f3 leaf = mk(0.f, 0.f, 0.f);
+            if (ray.mat == kNone) {  // SampleSky (activateSky == false), :1092-1095
+                leaf = ld3(sv.sky);
+                done = true;
+            } else if (ray.mat == VPX_MAT_EMISSIVE) {  // :1315-1316
+                leaf = albedo(sv, ray.mat) * sv.materials[ray.mat].emissive;
+                done = true;
+            } else {
+                const uint32_t m = ray.mat;
+                const vpx_material& mat = sv.materials[m];
+                f3 a = mk(1.f, 1.f, 1.f);
+                uint32_t form;
+                Ray next;
+                f3 kd;
+                if (m >= VPX_MAT_METAL_HIGH && m <= VPX_MAT_METAL_LOW) {  // :1103-1114
+                    const f3 refl = reflect(ray.D, ray.N);
+                    const f3 o = offset_ray(ray_point(ray), ray.N);
+                    next = make_ray(o, refl + random_sphere_sample(g) * mat.roughness);
+                    a = albedo(sv, m);
+                    form = kFormMul;
+                } else if (m <= VPX_MAT_NON_METAL_PINK) {  // :1117-1144
+                    if (g.next() > schlick_nonmetal(dot(-ray.D, ray.N))) {
+                        const f3 rdir = ray.N + random_sphere_sample(g);
+                        pending = emit_illumination(sv, ray, g, w, p, false, kd, slots);
+                        next = make_ray(offset_ray(ray_point(ray), ray.N), rdir);
+                        a = albedo(sv, m);
+                        form = kFormMulAdd;
+                    } else {
+                        const f3 refl = reflect(ray.D, ray.N);
+                        const f3 o = offset_ray(ray_point(ray), ray.N);
+                        next = make_ray(o, refl + random_sphere_sample(g) * mat.roughness);
+                        form = kFormPass;
+                    }
+                } else if (m == VPX_MAT_GLASS) {  // :1146-1209
+                    bool in_glass = ray.inside;
+                    const float ior = mat.ior;
+                    const float ratio = in_glass ? ior : 1.0f / ior;
+                    bool inside_volume = true;
+                    if (in_glass) {
+                        a = albedo(sv, m);
+                        if (vox >= 0) inside_volume = exit_march<kGlassExit>(sv, ray, vox, k);
+                    }
+                    if (!inside_volume) {
+                        ray.O = ray.O + ray.D * ray.t;
+                        ray.t = 0;
+                    }
+                    const float c = smin(dot(-ray.D, ray.N), 1.0f);
+                    const float s = sqrtf(1.0f - c * c);
+                    const bool cannot = ratio * s > 1.0f;
+                    f3 rdir, rn;
+                    if (cannot || schlick(c, ratio) > g.next()) {
+                        rdir = reflect(ray.D, ray.N);
+                        rn = ray.N;
+                    } else {
+                        rdir = refract(ray.D, ray.N, ratio);
+                        in_glass = !in_glass;
+                        rn = -ray.N;
+                    }
+                    next = make_ray(offset_ray(ray_point(ray), rn), rdir);
+                    next.inside = in_glass;
+                    form = kFormMul;
+                } else if (m <= VPX_MAT_SMOKE_PLAYER) {  // smoke :1210-1314
+                    f3 color = mk(1.f, 1.f, 1.f);
+                    const bool in_glass = ray.inside;
+                    bool inside_volume = true;
+                    float intensity = 0.f, dist = 0.f;
+                    if (vox == 0) {  // player light probe :1228-1240 (rays cast, result unused)
+                        pending = emit_illumination(sv, ray, g, w, p, true, kd, slots);
+                    }
+                    if (in_glass) {
+                        intensity = mat.emissive;
+                        color = albedo(sv, m);
+                        if (vox >= 0) inside_volume = exit_march<kSmokeExit>(sv, ray, vox, k);
+                        dist = ray.t;
+                    }
+                    const float threshold = g.next() * 100.0f - intensity;
+                    if (g.next() * dist > threshold) {
+                        const float lo = ray.t * .45f, hi = ray.t;
+                        const float tt = lo + g.next() * (hi - lo);
+                        ray.O = ray.O + ray.D * tt;
+                        ray.D = random_direction(g);
+                        ray.t = 0;
+                    }
+                    const f3 flipped = mk(1.f, 1.f, 1.f) - color;
+                    const f3 e = flipped * ((-dist) * intensity);
+                    a = mk(cr_exp(e.x), cr_exp(e.y), cr_exp(e.z));
+                    if (!inside_volume) {
+                        ray.O = ray.O + ray.D * ray.t;
+                        ray.t = 0;
+                    }
+                    const f3 rdir = refract(ray.D, ray.N, 1.0f);
+                    next = make_ray(offset_ray(ray_point(ray), -ray.N), rdir);
+                    next.inside = !in_glass;
+                    form = kFormMul;
+                } else {  // model materials :1319-1326
+                    const f3 rdir = diffuse_reflection(g, ray.N);
+                    pending = emit_illumination(sv, ray, g, w, p, false, kd, slots);
+                    next = make_ray(offset_ray(ray_point(ray), ray.N), rdir);
+                    a = albedo(sv, m);
+                    form = kFormAddMul;
+                }
+                const uint64_t li = (uint64_t)nl * w.P + p;
+                w.LA[li] = make_float4(a.x, a.y, a.z, 0.f);
+                w.LB[li] = make_float4(0.f, 0.f, 0.f, 0.f);
+                forms = (forms & 0x07ffffffu) | (form << (2 * nl)) | ((nl + 1u) << 27);
+                if (pending) {
+                    pending |= (nl << 8);
+                    w.SM[p] = make_float4(kd.x, kd.y, kd.z, __uint_as_float(pending));
+                }
+                --depth;
+                if (depth < 0) done = true;  // the child Trace(depth < 0) returns 0
+                flags = (next.inside ? kInside : 0u) | (done ? 0u : kActive);
+                w.O[p] = make_float4(next.O.x, next.O.y, next.O.z, __uint_as_float(g.s));
+                w.D[p] = make_float4(next.D.x, next.D.y, next.D.z, __uint_as_float(flags));
+                w.depth[p] = depth;
+                w.forms[p] = forms;
+                next_active = !done;
+            }
+            if (done) {
+                w.leaf[p] = make_float4(leaf.x, leaf.y, leaf.z, 0.f);
+                if (ray.mat == kNone || ray.mat == VPX_MAT_EMISSIVE) {
+                    w.D[p] = make_float4(od.x, od.y, od.z, __uint_as_float(0u));
+                }
+            }
+        }
+        if (!pending) w.SM[p] = make_float4(0.f, 0.f, 0.f, __uint_as_float(0u));
+    }
+    if (shadow_list) {  // wave-uniform
+        const uint32_t c = (uint32_t)__popc(slots);
+        uint32_t at = wave_append(c, shadow_len);
+        for (uint32_t m = slots; m; m &= m - 1u) shadow_list[at++] = ((uint32_t)__ffs(m) - 1u) << 27 | p;
+    }
+    if (next_list) {
+        const uint32_t at = wave_append(next_active ? 1u : 0u, next_len);
+        if (next_active) next_list[at] = p;
+    }
+    flush_counters(k, 0u, ctr);
+}
+
+// Light sum of a level once its shadow rays are resolved (kSlotOcc set by k_shadow1):
+// the evaluators' accumulation (renderer.cpp:102-207) and Illumination's *lightCount.
+__global__ __launch_bounds__(256) void k_resolve(SceneView sv, WaveBufs w) {
+    const uint32_t p = blockIdx.x * 256u + threadIdx.x;
+    if (p >= w.P) return;
+    const float4 sm = w.SM[p];
+    const uint32_t pend = __float_as_uint(sm.w);
+    if (!pend) return;
+    const uint32_t kind = pend & 7u, count = (pend >> 4) & 15u, lvl = (pend >> 8) & 31u, lc = pend >> 16;
+    w.SM[p] = make_float4(0.f, 0.f, 0.f, __uint_as_float(0u));
+    if (pend & 8u) return;  // discarded probe
+    f3 acc = mk(0.f, 0.f, 0.f);
+    for (uint32_t s = 0; s < count; ++s) {
+        const uint64_t i = (uint64_t)s * w.P + p;
+        const uint32_t fl = __float_as_uint(w.SD[i].w);
+        if (!(fl & kSlotValid) || (fl & 4u /* kSlotOcc */)) continue;
+        const float4 v = w.SL[i];
+        if (kind == kLightArea)
+            acc = acc + mk(v.x, v.y, v.z);
+        else
+            acc = mk(v.x, v.y, v.z);
+    }
+    f3 inc = acc;
+    if (kind == kLightArea) inc = (acc / (float)sv.area_samples) * mk(sm.x, sm.y, sm.z);
+    inc = inc * (float)lc;
+    w.LB[(uint64_t)lvl * w.P + p] = make_float4(inc.x, inc.y, inc.z, 0.f);
+}
+
+// ------------------------------------------------------------------- stage 3
+// Renderer::IsOccluded for the level's shadow rays, in the evaluator's order, then the
+// light sum exactly as the evaluators and Illumination form it.
+__global__ __launch_bounds__(256) void k_shadow(SceneView sv, WaveBufs w, unsigned long long* ctr) {
+    const uint32_t p = blockIdx.x * 256u + threadIdx.x;
+    Counters k{0u, 0u, 0u};
+    if (p < w.P) {
+        const float4 sm = w.SM[p];
+        const uint32_t pend = __float_as_uint(sm.w);
+        if (pend) {
+            const uint32_t kind = pend & 7u, count = (pend >> 4) & 15u, lvl = (pend >> 8) & 31u;
+            const uint32_t lc = pend >> 16;
+            const bool discard = (pend & 8u) != 0u;
+            f3 acc = mk(0.f, 0.f, 0.f);
+            for (uint32_t s = 0; s < count; ++s) {
+                const uint64_t i = (uint64_t)s * w.P + p;
+                const float4 sd = w.SD[i];
+                const uint32_t fl = __float_as_uint(sd.w);
+                if (!(fl & kSlotValid)) continue;
+                const float4 so = w.SO[i];
+                Ray r;
+                r.O = mk(so.x, so.y, so.z);
+                r.D = mk(sd.x, sd.y, sd.z);
+                r.t = so.w;
+                const bool occ = shadow(sv, r, k);
+                if (occ) continue;
+                const float4 v = w.SL[i];
+                if (kind == kLightArea)
+                    acc = acc + mk(v.x, v.y, v.z);
+                else
+                    acc = mk(v.x, v.y, v.z);
+            }
+            if (!discard) {
+                f3 inc = acc;
+                if (kind == kLightArea) inc = (acc / (float)sv.area_samples) * mk(sm.x, sm.y, sm.z);
+                inc = inc * (float)lc;
+                w.LB[(uint64_t)lvl * w.P + p] = make_float4(inc.x, inc.y, inc.z, 0.f);
+            }
+        }
+    }
+    flush_counters(k, 0u, ctr);
+}
+
+// ------------------------------------------------------------------- stage 4
+// GetLuminance / ApplyReinhardJodie / RGBF32_to_RGB8 (renderer.cpp:2222-2240,
+// template/precomp.h:372-388).
+__device__ __forceinline__ uint32_t tonemap_pack(float4 a) {
+    const f3 c = mk(a.x, a.y, a.z);
+    const float lum = dot(c, mk(0.2126f, 0.7152f, 0.0722f));
+    const f3 rh = c / mk(1.0f + c.x, 1.0f + c.y, 1.0f + c.z);
+    const f3 la = c / (1.0f + lum);
+    const float o0 = la.x + rh.x * (rh.x - la.x);
+    const float o1 = la.y + rh.y * (rh.y - la.y);
+    const float o2 = la.z + rh.z * (rh.z - la.z);
+    const uint32_t r = (uint32_t)(int64_t)(255.0f * smin(1.0f, o0));
+    const uint32_t gg = (uint32_t)(int64_t)(255.0f * smin(1.0f, o1));
+    const uint32_t b = (uint32_t)(int64_t)(255.0f * smin(1.0f, o2));
+    return (r << 16) + (gg << 8) + b;
+}
+
+// Running-average blend of the AVX path: fma(1-w, acc, px*w) (renderer.cpp:1797-1828).
+__device__ __forceinline__ float4 blend(float4 acc, f3 px, float w, float iw) {
+    return make_float4(fmaf(iw, acc.x, px.x * w), fmaf(iw, acc.y, px.y * w), fmaf(iw, acc.z, px.z * w),
+                       fmaf(iw, acc.w, 0.0f * w));
+}
+
+// Fold the level records bottom-up (the recursion's rounding order) and either
+// accumulate + tonemap in place (PACKED = false) or write the raw sample (PACKED = true).
+template <bool PACKED>
+__global__ __launch_bounds__(256) void k_finish(FrameArgs f, WaveBufs w, float4* __restrict__ accum,
+                                                uint32_t* __restrict__ rgb8, float4* __restrict__ packed) {
+    const uint32_t p = blockIdx.x * 256u + threadIdx.x;
+    if (p >= w.P) return;
+    uint32_t x, y;
+    const bool valid = path_pixel(f, p, x, y);
+    f3 v = mk(0.f, 0.f, 0.f);
+    if (valid) {
+        const float4 lf = w.leaf[p];
+        v = mk(lf.x, lf.y, lf.z);
+        const uint32_t forms = w.forms[p];
+        for (int i = (int)(forms >> 27) - 1; i >= 0; --i) {
+            const uint32_t form = (forms >> (2 * i)) & 3u;
+            const uint64_t li = (uint64_t)i * w.P + p;
+            const float4 a4 = w.LA[li];
+            const f3 a = mk(a4.x, a4.y, a4.z);
+            if (form == kFormMulAdd) {
+                const float4 b4 = w.LB[li];
+                v = mk(b4.x, b4.y, b4.z) + v * a;
+            } else if (form == kFormAddMul) {
+                const float4 b4 = w.LB[li];
+                v = (v + mk(b4.x, b4.y, b4.z)) * a;
+            } else if (form == kFormMul) {
+                v = v * a;
+            }
+        }
+    }
+    if (PACKED) {
+        packed[p] = make_float4(v.x, v.y, v.z, 0.0f);
+    } else if (valid) {
+        const uint64_t px = (uint64_t)y * f.width + x;
+        if (f.flags & VPX_FLAG_NO_TONEMAP) {
+            accum[px] = make_float4(v.x, v.y, v.z, 0.0f);
+        } else {
+            const float4 a = blend(accum[px], v, f.weight, f.inv_weight);
+            accum[px] = a;
+            if (rgb8) rgb8[px] = tonemap_pack(a);
+        }
+    }
+}
+
+}  // namespace vpx

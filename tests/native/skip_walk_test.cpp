@@ -1,0 +1,171 @@
+// Randomised equivalence test: vpx::skip::walk_skip (occupancy hierarchy + exact binade
+// jumps) against the plain cell-by-cell reference march (template/scene.cpp:751-811).
+// Build: g++ -O2 -std=c++17 -ffp-contract=off -I raytracer-voxpopuli_amd/csrc tests/native/skip_walk_test.cpp
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <vector>
+#include <xmmintrin.h>
+#include "vpx_skip.hpp"
+
+using namespace vpx::skip;
+
+struct World {
+    uint32_t n, nb1, nb2, nb3;
+    std::vector<uint8_t> cells;
+    std::vector<uint64_t> l1, l2, l3;
+    GridView view() const { return GridView{cells.data(), l1.data(), l2.data(), l3.data(), n, nb1, nb2, nb3}; }
+};
+
+static World make_world(uint32_t n, uint64_t seed, double density) {
+    World w;
+    w.n = n;
+    w.cells.assign((size_t)n * n * n, 255);
+    std::mt19937_64 r(seed);
+    // clustered boxes of solid voxels with holes
+    const int boxes = (int)(density * 400);
+    for (int b = 0; b < boxes; ++b) {
+        uint32_t x0 = r() % n, y0 = r() % n, z0 = r() % n, sx = 1 + r() % (n / 6 + 1), sy = 1 + r() % (n / 6 + 1), sz = 1 + r() % (n / 6 + 1);
+        for (uint32_t z = z0; z < std::min(n, z0 + sz); ++z)
+            for (uint32_t y = y0; y < std::min(n, y0 + sy); ++y)
+                for (uint32_t x = x0; x < std::min(n, x0 + sx); ++x)
+                    if (r() % 5) w.cells[x + (size_t)y * n + (size_t)z * n * n] = (uint8_t)(r() % 200);
+    }
+    w.nb1 = (n + 3) / 4, w.nb2 = (w.nb1 + 3) / 4, w.nb3 = (w.nb2 + 3) / 4;
+    w.l1.assign((size_t)w.nb1 * w.nb1 * w.nb1, 0);
+    for (uint32_t z = 0; z < n; ++z)
+        for (uint32_t y = 0; y < n; ++y)
+            for (uint32_t x = 0; x < n; ++x)
+                if (w.cells[x + (size_t)y * n + (size_t)z * n * n] != 255)
+                    w.l1[(x >> 2) + (size_t)(y >> 2) * w.nb1 + (size_t)(z >> 2) * w.nb1 * w.nb1] |= 1ull << ((x & 3) + 4 * (y & 3) + 16 * (z & 3));
+    w.l2.assign((size_t)w.nb2 * w.nb2 * w.nb2, 0);
+    for (uint32_t z = 0; z < w.nb1; ++z)
+        for (uint32_t y = 0; y < w.nb1; ++y)
+            for (uint32_t x = 0; x < w.nb1; ++x)
+                if (w.l1[x + (size_t)y * w.nb1 + (size_t)z * w.nb1 * w.nb1])
+                    w.l2[(x >> 2) + (size_t)(y >> 2) * w.nb2 + (size_t)(z >> 2) * w.nb2 * w.nb2] |= 1ull << ((x & 3) + 4 * (y & 3) + 16 * (z & 3));
+    w.l3.assign((size_t)w.nb3 * w.nb3 * w.nb3, 0);
+    for (uint32_t z = 0; z < w.nb2; ++z)
+        for (uint32_t y = 0; y < w.nb2; ++y)
+            for (uint32_t x = 0; x < w.nb2; ++x)
+                if (w.l2[x + (size_t)y * w.nb2 + (size_t)z * w.nb2 * w.nb2])
+                    w.l3[(x >> 2) + (size_t)(y >> 2) * w.nb3 + (size_t)(z >> 2) * w.nb3 * w.nb3] |= 1ull << ((x & 3) + 4 * (y & 3) + 16 * (z & 3));
+    return w;
+}
+
+// Setup3DDDA for the unit cube (template/scene.cpp:719-749); false = misses the cube.
+static bool setup(uint32_t n, const float O[3], const float D[3], Walk& w) {
+    float rD[3], ds[3];
+    for (int k = 0; k < 3; ++k) {
+        rD[k] = 1.0f / D[k];
+        uint32_t b;
+        std::memcpy(&b, &D[k], 4);
+        ds[k] = (float)(b >> 31);
+    }
+    float t = 0;
+    const bool inside = O[0] >= 0 && O[1] >= 0 && O[2] >= 0 && O[0] <= 1 && O[1] <= 1 && O[2] <= 1;
+    if (!inside) {
+        float tmin = -1e30f, tmax = 1e30f;
+        for (int k = 0; k < 3; ++k) {
+            const int sg = D[k] < 0;
+            float a = ((sg ? 1.f : 0.f) - O[k]) * rD[k], b = ((sg ? 0.f : 1.f) - O[k]) * rD[k];
+            if (k == 0) { tmin = a, tmax = b; continue; }
+            if (tmin > b || a > tmax) return false;
+            tmin = tmin < a ? a : tmin;
+            tmax = b < tmax ? b : tmax;
+        }
+        if (!(tmin > 0)) return false;
+        t = tmin;
+    }
+    const float g = (float)n, cell = 1.0f / g;
+    int P[3], st[3];
+    float tm[3], td[3];
+    for (int k = 0; k < 3; ++k) {
+        st[k] = (int)(1.0f - ds[k] * 2.0f);
+        const float pos = ((O[k] - 0.0f) + D[k] * (t + 0.00005f)) * g / 1.0f;
+        const float plane = (std::ceil(pos) - ds[k]) * cell;
+        int p = (pos > -2147483904.0f && pos < 2147483648.0f) ? (int)pos : (int)0x80000000u;
+        P[k] = p < 0 ? 0 : (p > (int)n - 1 ? (int)n - 1 : p);
+        td[k] = cell * (float)st[k] * rD[k];
+        tm[k] = ((plane * 1.0f) - (O[k] - 0.0f)) * rD[k];
+    }
+    w = Walk{};
+    w.X = P[0], w.Y = P[1], w.Z = P[2];
+    w.t = t;
+    w.tx = tm[0], w.ty = tm[1], w.tz = tm[2];
+    w.dx = td[0], w.dy = td[1], w.dz = td[2];
+    w.sx = st[0], w.sy = st[1], w.sz = st[2];
+    w.k1 = w.k2 = w.k3 = 0xffffffffu;
+    return true;
+}
+
+// Scene::FindNearest's loop, cell by cell.
+static bool walk_naive(const World& W, Walk s, float bound, uint32_t& cells, Walk& out) {
+    const uint32_t n = W.n;
+    while (s.t < bound) {
+        const uint8_t c = W.cells[s.X + (size_t)s.Y * n + (size_t)s.Z * n * n];
+        ++cells;
+        if (c != 255 && s.t < bound) { out = s; return true; }
+        if (s.tx < s.ty) {
+            if (s.tx < s.tz) { s.t = s.tx; s.X += s.sx; if (s.X >= n) break; s.tx += s.dx; }
+            else { s.t = s.tz; s.Z += s.sz; if (s.Z >= n) break; s.tz += s.dz; }
+        } else {
+            if (s.ty < s.tz) { s.t = s.ty; s.Y += s.sy; if (s.Y >= n) break; s.ty += s.dy; }
+            else { s.t = s.tz; s.Z += s.sz; if (s.Z >= n) break; s.tz += s.dz; }
+        }
+    }
+    return false;
+}
+
+int main(int argc, char** argv) {
+    _mm_setcsr(_mm_getcsr() | 0x8040u);
+    const long rays = argc > 1 ? atol(argv[1]) : 20000;
+    long bad = 0, total = 0;
+    uint64_t cells_all = 0;
+    const uint32_t sizes[] = {64, 100, 128, 256};
+    for (uint32_t n : sizes) {
+        for (double dens : {0.02, 0.2, 1.0}) {
+            World W = make_world(n, n * 31 + (uint64_t)(dens * 100), dens);
+            std::mt19937_64 r(n + 7);
+            std::uniform_real_distribution<float> U(0.f, 1.f);
+            for (long i = 0; i < rays; ++i) {
+                float O[3], T[3], D[3];
+                const int kind = i % 4;
+                for (int k = 0; k < 3; ++k) {
+                    O[k] = kind == 0 ? U(r) : -0.6f + 2.2f * U(r);
+                    T[k] = 0.05f + 0.9f * U(r);
+                    D[k] = T[k] - O[k];
+                }
+                if (kind == 3) {  // axis-aligned / grid-aligned directions and origins on planes
+                    const int ax = r() % 3;
+                    for (int k = 0; k < 3; ++k) if (k != ax) D[k] = (r() % 2) ? 0.0f : D[k];
+                    O[r() % 3] = (float)(r() % n) / (float)n;
+                }
+                const float len = std::sqrt(D[0] * D[0] + D[1] * D[1] + D[2] * D[2]);
+                if (!(len > 0)) continue;
+                for (int k = 0; k < 3; ++k) D[k] = D[k] * (1.0f / len);
+                Walk s;
+                if (!setup(n, O, D, s)) continue;
+                const float bound = (i % 3 == 0) ? 1e34f : 0.2f + 2.0f * U(r);
+                uint32_t c0 = 0, c1 = 0;
+                Walk h0{}, h1 = s;
+                const bool r0 = walk_naive(W, s, bound, c0, h0);
+                const bool r1 = walk_skip(W.view(), h1, bound, c1);
+                ++total;
+                cells_all += c0;
+                bool ok = r0 == r1 && c0 == c1;
+                if (ok && r0) ok = std::memcmp(&h0.t, &h1.t, 4) == 0 && h0.X == h1.X && h0.Y == h1.Y && h0.Z == h1.Z;
+                if (!ok) {
+                    if (bad < 10)
+                        printf("n=%u dens=%.2f ray %ld: hit %d/%d cells %u/%u t %a/%a cell (%u,%u,%u)/(%u,%u,%u)\n", n, dens, i, r0, r1, c0, c1,
+                               h0.t, h1.t, h0.X, h0.Y, h0.Z, h1.X, h1.Y, h1.Z);
+                    ++bad;
+                }
+            }
+        }
+    }
+    printf("rays=%ld cells=%llu bad=%ld\n", total, (unsigned long long)cells_all, bad);
+    return bad ? 1 : 0;
+}
