@@ -150,7 +150,7 @@ def load_library(path=None):
     global _LIB
     if _LIB is not None and path is None:
         return _LIB
-    p = path or LIB_PATH
+    p = path or os.environ.get("VPX_LIB") or LIB_PATH
     if not os.path.exists(p):
         raise VpxError(f"{p} is missing: run __graft_entry__.build() (hipcc --offload-arch=gfx950)")
     lib = C.CDLL(p)

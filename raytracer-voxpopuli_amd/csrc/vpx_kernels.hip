@@ -16,7 +16,7 @@
 #include <string>
 #include <vector>
 
-#include "vpx_persist.hpp"
+#include "vpx_wavefront.hpp"
 
 using namespace vpx;
 
@@ -237,12 +237,6 @@ struct vpx_ctx {
     void* d_wave = nullptr;
     size_t wave_bytes = 0;
     WaveBufs wave{};
-    uint32_t* shadow_list = nullptr;  // [S*P] compact shadow work list
-    uint32_t* next_list = nullptr;    // [P] next level's active paths
-    uint32_t* ctl = nullptr;          // [4 + 4*L] work-list lengths / counters, zeroed per frame
-    uint32_t ctl_words = 0;
-    int persist_blocks = 0;           // resident 256-thread workgroups for persistent kernels
-    bool persistent = false;          // single-volume scenes: persistent DDA kernels (VPX_PERSIST=1 enables)
 };
 
 namespace {
@@ -369,7 +363,7 @@ int validate_frame(vpx_ctx* c, const vpx_frame_params* p) {
 int ensure_wave(vpx_ctx* c, uint32_t P, uint32_t L, uint32_t S) {
     const size_t f4 = sizeof(float4);
     const size_t bytes = (size_t)P * (f4 * (5 + 2 * (size_t)L + 3 * (size_t)S + 1) + 3 * sizeof(uint32_t)) +
-                         sizeof(uint32_t) * ((size_t)S * P + P + 4 + 4 * (size_t)L) + 16 * 256;
+                         sizeof(uint32_t) * (size_t)P + 16 * 256;
     if (bytes > c->wave_bytes) {
         if (c->d_wave) {
             VPX_HIP(c, hipStreamSynchronize(c->stream));
@@ -402,31 +396,12 @@ int ensure_wave(vpx_ctx* c, uint32_t P, uint32_t L, uint32_t S) {
     w.HM = (uint32_t*)take(4 * (size_t)P);
     w.depth = (int32_t*)take(4 * (size_t)P);
     w.forms = (uint32_t*)take(4 * (size_t)P);
-    c->shadow_list = (uint32_t*)take(4 * (size_t)S * P);
-    c->next_list = (uint32_t*)take(4 * (size_t)P);
-    c->ctl_words = 4 + 4 * L;
-    c->ctl = (uint32_t*)take(4 * (size_t)c->ctl_words);
+    w.smask = (uint32_t*)take(4 * (size_t)P);
     return VPX_OK;
 }
 
-// Workgroups of the persistent kernels: what the occupancy calculator admits per CU x CUs.
-int persist_grid(vpx_ctx* c) {
-    if (c->persist_blocks) return c->persist_blocks;
-    int per_cu = 0, cus = 0;
-    hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, c->device) == hipSuccess) cus = prop.multiProcessorCount;
-    int a = 0, b = 0, d = 0;
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, reinterpret_cast<const void*>(&k_nearest1<true>), kThreads, 0);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, reinterpret_cast<const void*>(&k_nearest1<false>), kThreads, 0);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&d, reinterpret_cast<const void*>(&k_shadow1), kThreads, 0);
-    per_cu = std::max(1, std::min(a, std::min(b, d)));
-    c->persist_blocks = std::max(1, per_cu * std::max(1, cus));
-    return c->persist_blocks;
-}
-
-// The frame: nearest(first) -> [shade -> shadow (-> resolve) -> nearest]* -> finish, all
-// on c->stream.  Single-volume scenes take the persistent lane-refilling DDA kernels fed
-// by compact work lists; N-volume scenes the per-path kernels of vpx_wavefront.hpp.
+// The frame: primary -> [shade -> shadow -> resolve -> nearest]* -> finish, all on
+// c->stream, one 256-thread workgroup per 16x16 tile in every kernel.
 template <bool PACKED>
 int launch_render(vpx_ctx* c, const SceneView& sv, const FrameArgs& f, uint32_t tiles, float4* accum, uint32_t* rgb8,
                   float4* packed) {
@@ -437,37 +412,13 @@ int launch_render(vpx_ctx* c, const SceneView& sv, const FrameArgs& f, uint32_t 
     if (rc) return rc;
     const WaveBufs w = c->wave;
     const dim3 grid(tiles), block(kThreads);
-    if (sv.num_volumes == 1 && c->persistent) {
-        OneVolume ov;
-        ov.vol = c->volumes[0];
-        const auto& gb = c->grids[ov.vol.grid_id];
-        ov.g = DevGrid{gb.ptr, gb.l1, gb.l2, gb.l3, gb.n, gb.nb1, gb.nb2, gb.nb3};
-        const dim3 pgrid(persist_grid(c));
-        uint32_t* ctl = c->ctl;
-        VPX_HIP(c, hipMemsetAsync(ctl, 0, sizeof(uint32_t) * c->ctl_words, c->stream));
-        hipLaunchKernelGGL((k_nearest1<true>), pgrid, block, 0, c->stream, sv, ov, f, w, nullptr, nullptr, ctl,
-                           c->d_ctr);
-        for (int level = 0; level <= f.max_bounces; ++level) {
-            uint32_t* lc = ctl + 4 + 4 * level;  // [0] shadow len [1] shadow ctr [2] next len [3] next ctr
-            const bool more = level < f.max_bounces;
-            hipLaunchKernelGGL(k_shade, grid, block, 0, c->stream, sv, f, w, level, c->d_ctr, c->shadow_list, lc + 0,
-                               more ? c->next_list : nullptr, lc + 2);
-            hipLaunchKernelGGL(k_shadow1, pgrid, block, 0, c->stream, sv, ov, w, c->shadow_list, lc + 0, lc + 1,
-                               c->d_ctr);
-            hipLaunchKernelGGL(k_resolve, grid, block, 0, c->stream, sv, w);
-            if (more)
-                hipLaunchKernelGGL((k_nearest1<false>), pgrid, block, 0, c->stream, sv, ov, f, w, c->next_list,
-                                   lc + 2, lc + 3, c->d_ctr);
-        }
-    } else {
-        hipLaunchKernelGGL((k_nearest<true>), grid, block, 0, c->stream, sv, f, w, c->d_ctr);
-        for (int level = 0; level <= f.max_bounces; ++level) {
-            hipLaunchKernelGGL(k_shade, grid, block, 0, c->stream, sv, f, w, level, c->d_ctr, nullptr, nullptr,
-                               nullptr, nullptr);
-            hipLaunchKernelGGL(k_shadow, grid, block, 0, c->stream, sv, w, c->d_ctr);
-            if (level < f.max_bounces)
-                hipLaunchKernelGGL((k_nearest<false>), grid, block, 0, c->stream, sv, f, w, c->d_ctr);
-        }
+    const size_t slds = sizeof(uint32_t) * S * kThreads;
+    hipLaunchKernelGGL(k_primary, grid, block, 0, c->stream, sv, f, w, c->d_ctr);
+    for (int level = 0; level <= f.max_bounces; ++level) {
+        hipLaunchKernelGGL(k_shade, grid, block, 0, c->stream, sv, f, w, level, c->d_ctr);
+        hipLaunchKernelGGL(k_shadow_tile, grid, block, slds, c->stream, sv, w, c->d_ctr);
+        hipLaunchKernelGGL(k_resolve, grid, block, 0, c->stream, sv, w);
+        if (level < f.max_bounces) hipLaunchKernelGGL(k_nearest_tile, grid, block, 0, c->stream, sv, w, c->d_ctr);
     }
     hipLaunchKernelGGL((k_finish<PACKED>), grid, block, 0, c->stream, f, w, accum, rgb8, packed);
     VPX_HIP(c, hipGetLastError());
@@ -514,7 +465,6 @@ int vpx_create(int device, vpx_ctx** out) {
     }
     c->stream = c->own_stream;
     (void)hipMemset(c->d_ctr, 0, 4 * sizeof(unsigned long long));
-    if (const char* e = std::getenv("VPX_PERSIST")) c->persistent = std::atoi(e) != 0;
     *out = c;
     return VPX_OK;
 }
@@ -873,3 +823,15 @@ uint32_t vpx_pixel_seed(uint32_t base, uint32_t frame, uint32_t w, uint32_t h, u
 }
 
 }  // extern "C"
+
+#ifdef VPX_PHASE_PROF
+extern "C" int vpx_debug_phase(unsigned long long* out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(vpx::g_phase), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
+    if (reset) {
+        const unsigned long long z[16] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(vpx::g_phase), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif
+

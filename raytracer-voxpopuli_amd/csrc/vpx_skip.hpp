@@ -252,13 +252,24 @@ struct Walk {
 
 VPX_HD uint32_t pack3(uint32_t a, uint32_t b, uint32_t c) { return a | (b << 11) | (c << 22); }
 
+// Mask word of block (bx, by, bz) in a level with nb blocks per axis.  nb <= 1024 (grids up
+// to 4096^3), so the index fits 32 bits and every product fits the 24-bit multiplier.
+VPX_HD uint64_t mask_at(const uint64_t* p, uint32_t nb, uint32_t bx, uint32_t by, uint32_t bz) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const uint32_t i = __umul24(bz, __umul24(nb, nb)) + __umul24(by, nb) + bx;
+    return ((const __attribute__((address_space(1))) uint64_t*)p)[i];
+#else
+    return p[(uint64_t)bx + (uint64_t)by * nb + (uint64_t)bz * nb * nb];
+#endif
+}
+
 // 0: solid cell, 1: empty cell, 2: inside an empty 16^3 macro, 3: inside an empty 64^3 super.
 VPX_HD int classify(Walk& w, const GridView& g) {
     const uint32_t X = w.X, Y = w.Y, Z = w.Z;
     const uint32_t k3 = pack3(X >> 6, Y >> 6, Z >> 6);
     if (k3 != w.k3) {
         w.k3 = k3;
-        w.m3 = g.l3[(uint64_t)(X >> 6) + (uint64_t)(Y >> 6) * g.nb3 + (uint64_t)(Z >> 6) * ((uint64_t)g.nb3 * g.nb3)];
+        w.m3 = mask_at(g.l3, g.nb3, X >> 6, Y >> 6, Z >> 6);
     }
     if (w.m3 == 0) return 3;
     const uint32_t mb = ((X >> 4) & 3u) | (((Y >> 4) & 3u) << 2) | (((Z >> 4) & 3u) << 4);
@@ -266,14 +277,14 @@ VPX_HD int classify(Walk& w, const GridView& g) {
     const uint32_t k2 = pack3(X >> 4, Y >> 4, Z >> 4);
     if (k2 != w.k2) {
         w.k2 = k2;
-        w.m2 = g.l2[(uint64_t)(X >> 4) + (uint64_t)(Y >> 4) * g.nb2 + (uint64_t)(Z >> 4) * ((uint64_t)g.nb2 * g.nb2)];
+        w.m2 = mask_at(g.l2, g.nb2, X >> 4, Y >> 4, Z >> 4);
     }
     const uint32_t bb = ((X >> 2) & 3u) | (((Y >> 2) & 3u) << 2) | (((Z >> 2) & 3u) << 4);
     if (!((w.m2 >> bb) & 1ull)) return 1;
     const uint32_t k1 = pack3(X >> 2, Y >> 2, Z >> 2);
     if (k1 != w.k1) {
         w.k1 = k1;
-        w.m1 = g.l1[(uint64_t)(X >> 2) + (uint64_t)(Y >> 2) * g.nb1 + (uint64_t)(Z >> 2) * ((uint64_t)g.nb1 * g.nb1)];
+        w.m1 = mask_at(g.l1, g.nb1, X >> 2, Y >> 2, Z >> 2);
     }
     const uint32_t cb = (X & 3u) | ((Y & 3u) << 2) | ((Z & 3u) << 4);
     return ((w.m1 >> cb) & 1ull) ? 0 : 1;
@@ -366,6 +377,139 @@ VPX_HD int skip_box(Walk& w, const uint32_t lo[3], const uint32_t hi[3], float b
     return 1;
 }
 
+// ---------------------------------------------------------------- fast path
+// The common case of skip_box in straight-line integer code: every axis sequence is in
+// closed form over the box (at most one binade change, no tie, not stuck).  Same results.
+
+// Closed-form parameters of A -> fl(A + d) in A's binade: A = b*u, fl(A + d) = A + c*u.
+VPX_HD bool seg_params(float a, float d, uint32_t& b, uint32_t& c, uint32_t& e) {
+    const uint32_t ab = fbits(a), db = fbits(d);
+    const uint32_t ea = ab >> 23, ed = db >> 23;
+    if (ea - 1u >= 254u || ed - 1u >= 254u || ed >= ea) return false;  // sign/zero/denormal/inf/nan, d >= 2^E
+    const uint32_t sh = ea - ed;
+    if (sh > 24u) return false;  // stuck (d < u/2)
+    const uint32_t md = (db & 0x7fffffu) | 0x800000u;
+    const uint32_t rem = md & ((1u << sh) - 1u), half = 1u << (sh - 1u);
+    c = (md >> sh) + (rem > half ? 1u : 0u);
+    b = (ab & 0x7fffffu) | 0x800000u;
+    e = ea;
+    return rem != half && c != 0u;
+}
+
+// A(0..last) as up to two closed-form segments: i <= m1 in A(0)'s binade, i > m1 after the
+// plain IEEE step m1 -> m1+1 (only when last > m1).
+struct Seq2 {
+    uint32_t b1, c1, e1, m1;
+    uint32_t b2, c2, e2;
+};
+
+VPX_HD bool seq2_init(float a, float d, uint32_t last, Seq2& q) {  // last <= 63
+    if (!seg_params(a, d, q.b1, q.c1, q.e1)) return false;
+    const uint32_t room = 0xffffffu - q.b1;
+    q.b2 = q.c2 = q.e2 = 0u;
+    if (last * q.c1 <= room) {  // c1 <= 2^23: no overflow for last <= 63
+        q.m1 = last;
+        return true;
+    }
+    q.m1 = udiv(room, q.c1);
+    const float A = seg_value(q.b1 + q.m1 * q.c1, q.e1) + d;
+    if (!seg_params(A, d, q.b2, q.c2, q.e2)) return false;
+    return (last - q.m1 - 1u) * q.c2 <= 0xffffffu - q.b2;
+}
+
+VPX_HD float seq2_at(const Seq2& q, uint32_t i) {
+    const bool one = i <= q.m1;
+    const uint32_t b = one ? q.b1 + i * q.c1 : q.b2 + (i - q.m1 - 1u) * q.c2;
+    return seg_value(b, one ? q.e1 : q.e2);
+}
+
+// ceil(p / c) for p <= 2^24 + 1, c >= 1, from q ~ p / c (relative error < 2^-20); exact
+// when <= 1024, otherwise some value > 1024.
+VPX_HD uint32_t ceil_div_q(uint32_t p, uint32_t c, float q) {
+    if (!(q < 1024.0f)) return 1025u;
+    uint32_t j = (uint32_t)q + 1u;  // q's error is far below 1: j is ceil(p/c) or one off
+    if ((uint64_t)(j - 1u) * c >= p) --j;
+    if ((uint64_t)j * c < p) ++j;
+    return j;
+}
+
+VPX_HD uint32_t ceil_div_small(uint32_t p, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return ceil_div_q(p, c, (float)p * __builtin_amdgcn_rcpf((float)c));
+#else
+    return ceil_div_q(p, c, (float)p / (float)c);
+#endif
+}
+
+// First j >= 0 with (b + j c) u not below T (strict: >= T, else > T), T > 0 finite or inf.
+VPX_HD uint32_t seg_first(uint32_t b, uint32_t c, uint32_t e, uint32_t tb, bool strict) {
+    const uint32_t te = tb >> 23;
+    if (te < e) return 0u;
+    if (te > e) return 1025u;  // every term of the binade is below T
+    const uint32_t need = ((tb & 0x7fffffu) | 0x800000u) + (strict ? 0u : 1u);
+    return need <= b ? 0u : ceil_div_small(need - b, c);
+}
+
+// #{ i <= last : A(i) below T } clamped to `cap` (A is increasing).
+VPX_HD uint32_t seq2_count(const Seq2& q, float T, bool strict, uint32_t cap) {
+    const uint32_t tb = fbits(T);
+    uint32_t f = seg_first(q.b1, q.c1, q.e1, tb, strict);
+    if (f > q.m1 && q.e2 != 0u) {
+        const uint32_t f2 = seg_first(q.b2, q.c2, q.e2, tb, strict);
+        f = q.m1 + 1u + (f2 < 1025u ? f2 : 1025u);
+    }
+    return f < cap ? f : cap;
+}
+
+// skip_box for boxes whose three sequences pass seq2_init; 2 = use skip_box.
+VPX_HD int skip_box_fast(Walk& w, const uint32_t lo[3], const uint32_t hi[3], float bound, uint32_t& cells) {
+    const uint32_t ex = w.sx > 0 ? hi[0] - w.X + 1u : w.X - lo[0] + 1u;
+    const uint32_t ey = w.sy > 0 ? hi[1] - w.Y + 1u : w.Y - lo[1] + 1u;
+    const uint32_t ez = w.sz > 0 ? hi[2] - w.Z + 1u : w.Z - lo[2] + 1u;
+    Seq2 qx, qy, qz;
+    const bool okx = seq2_init(w.tx, w.dx, ex - 1u, qx);
+    const bool oky = seq2_init(w.ty, w.dy, ey - 1u, qy);
+    const bool okz = seq2_init(w.tz, w.dz, ez - 1u, qz);
+    if (!(okx && oky && okz)) return 2;
+    // the leaving event: smallest A_k(e_k - 1), ties -> z, then y, then x
+    const float Vx = seq2_at(qx, ex - 1u), Vy = seq2_at(qy, ey - 1u), Vz = seq2_at(qz, ez - 1u);
+    const int a = (Vz <= Vx && Vz <= Vy) ? 2 : (Vy <= Vx ? 1 : 0);
+    const float vs = a == 2 ? Vz : (a == 1 ? Vy : Vx);
+    // events of the other axes before it (axis k precedes a on ties iff k > a)
+    const uint32_t nx = a == 0 ? ex - 1u : seq2_count(qx, vs, true, ex - 1u);
+    const uint32_t ny = a == 1 ? ey - 1u : seq2_count(qy, vs, a == 2, ey - 1u);
+    const uint32_t nz = a == 2 ? ez - 1u : seq2_count(qz, vs, false, ez - 1u);
+    if (vs < bound) {
+        float tl = w.t;
+        bool moved = false;
+        if (nx) tl = seq2_at(qx, nx - 1u), moved = true;
+        if (ny) {
+            const float p = seq2_at(qy, ny - 1u);
+            tl = moved ? (tl < p ? p : tl) : p;
+            moved = true;
+        }
+        if (nz) {
+            const float p = seq2_at(qz, nz - 1u);
+            tl = moved ? (tl < p ? p : tl) : p;
+        }
+        w.t = tl;
+        w.tx = seq2_at(qx, nx), w.ty = seq2_at(qy, ny), w.tz = seq2_at(qz, nz);
+        w.X += nx * (uint32_t)w.sx;
+        w.Y += ny * (uint32_t)w.sy;
+        w.Z += nz * (uint32_t)w.sz;
+        cells += nx + ny + nz;
+        return 0;
+    }
+    cells += 1u + seq2_count(qx, bound, true, nx) + seq2_count(qy, bound, true, ny) + seq2_count(qz, bound, true, nz);
+    return 1;
+}
+
+// skip_box_fast, else the general skip_box.
+VPX_HD int skip_any(Walk& w, const uint32_t lo[3], const uint32_t hi[3], float bound, uint32_t& cells) {
+    const int r = skip_box_fast(w, lo, hi, bound, cells);
+    return r != 2 ? r : skip_box(w, lo, hi, bound, cells);
+}
+
 // Resumable form: at most `budget` loop iterations.  0 = not finished, 1 = solid cell
 // reached (w.t / w.X,Y,Z describe it), 2 = finished without a solid cell.
 VPX_HD int walk_skip_some(const GridView& g, Walk& w, float bound, uint32_t& cells, int budget) {
@@ -381,7 +525,7 @@ VPX_HD int walk_skip_some(const GridView& g, Walk& w, float bound, uint32_t& cel
             const uint32_t lo[3] = {w.X & ~m, w.Y & ~m, w.Z & ~m};
             uint32_t hi[3] = {lo[0] + m, lo[1] + m, lo[2] + m};
             for (int k = 0; k < 3; ++k) hi[k] = hi[k] < g.n - 1u ? hi[k] : g.n - 1u;
-            if (skip_box(w, lo, hi, bound, cells) == 1) return 2;
+            if (skip_any(w, lo, hi, bound, cells) == 1) return 2;
         }
         ++cells;
         if (!step1(w, g.n)) return 2;
@@ -404,7 +548,7 @@ VPX_HD bool walk_skip(const GridView& g, Walk& w, float bound, uint32_t& cells) 
             const uint32_t lo[3] = {w.X & ~m, w.Y & ~m, w.Z & ~m};
             uint32_t hi[3] = {lo[0] + m, lo[1] + m, lo[2] + m};
             for (int k = 0; k < 3; ++k) hi[k] = hi[k] < g.n - 1u ? hi[k] : g.n - 1u;
-            if (skip_box(w, lo, hi, bound, cells) == 1) return false;
+            if (skip_any(w, lo, hi, bound, cells) == 1) return false;
         }
         ++cells;  // visit the (empty) current cell
         if (!step1(w, g.n)) return false;

@@ -255,8 +255,17 @@ __device__ __forceinline__ f3 normal_voxel(const ORay& r, float t, uint32_t n, c
     return normalize(xform_vec(nn, matrix));
 }
 
+// Wave-uniform copy of a grid view (callers walk the same volume in every active lane),
+// kept in scalar registers.
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+template <class T>
+__device__ __forceinline__ T* uni_ptr(T* p) {
+    const uint64_t v = (uint64_t)p;
+    return (T*)(((uint64_t)uni((uint32_t)(v >> 32)) << 32) | uni((uint32_t)v));
+}
 __device__ __forceinline__ skip::GridView grid_view(const DevGrid& g) {
-    return skip::GridView{g.cells, g.l1, g.l2, g.l3, g.n, g.nb1, g.nb2, g.nb3};
+    return skip::GridView{uni_ptr(g.cells), uni_ptr(g.l1), uni_ptr(g.l2), uni_ptr(g.l3),
+                          uni(g.n), uni(g.nb1), uni(g.nb2), uni(g.nb3)};
 }
 __device__ __forceinline__ skip::Walk to_walk(const Dda& s) {
     skip::Walk w;
@@ -276,14 +285,26 @@ __device__ __forceinline__ skip::Walk to_walk(const Dda& s) {
 // plain cell steps — instead of inside every step iteration of the wave.
 constexpr uint32_t kStepThreshold = 16;
 
+#ifdef VPX_PHASE_PROF
+// Debug build only (-DVPX_PHASE_PROF): per-wave cycles / iterations / active lanes of the
+// step and skip phases of walk_wave, read back with vpx_debug_phase().
+__device__ unsigned long long g_phase[16];
+#define VPX_PH(...) __VA_ARGS__
+#else
+#define VPX_PH(...)
+#endif
+
 __device__ __forceinline__ bool walk_wave(const skip::GridView& g, skip::Walk& w, float bound, uint32_t& cells) {
     enum : int { kStep = 0, kSkip = 1, kMiss = 2, kHit = 3 };
     int mode = kStep, pending = 0;
+    VPX_PH(uint64_t cs = 0, ck = 0, ns = 0, nk = 0, ls = 0, lk = 0, fb = 0, cf = 0;)
     for (;;) {
+        VPX_PH(uint64_t t0 = __builtin_amdgcn_s_memtime();)
         for (;;) {
             const uint64_t stepping = __ballot(mode == kStep);
             if (!stepping) break;
             if ((uint32_t)__popcll(stepping) < kStepThreshold && __ballot(mode == kSkip)) break;
+            VPX_PH(++ns; ls += __popcll(stepping);)
             if (mode == kStep) {
                 if (!(w.t < bound)) {
                     mode = kMiss;
@@ -302,23 +323,44 @@ __device__ __forceinline__ bool walk_wave(const skip::GridView& g, skip::Walk& w
                 }
             }
         }
-        if (!__ballot(mode == kSkip)) {
+        VPX_PH(uint64_t t1 = __builtin_amdgcn_s_memtime(); cs += t1 - t0;)
+        const uint64_t skipping = __ballot(mode == kSkip);
+        if (!skipping) {
             if (!__ballot(mode == kStep)) break;
             continue;
         }
+        VPX_PH(++nk; lk += __popcll(skipping);)
         if (mode == kSkip) {
             const uint32_t m = pending == 3 ? 63u : 15u;
             const uint32_t lo[3] = {w.X & ~m, w.Y & ~m, w.Z & ~m};
             uint32_t hi[3] = {lo[0] + m, lo[1] + m, lo[2] + m};
             for (int k = 0; k < 3; ++k) hi[k] = hi[k] < g.n - 1u ? hi[k] : g.n - 1u;
-            if (skip::skip_box(w, lo, hi, bound, cells) == 1) {
+            int sr = skip::skip_box_fast(w, lo, hi, bound, cells);
+            VPX_PH(uint64_t t2 = __builtin_amdgcn_s_memtime(); if (__ballot(sr == 2)) ++fb;)
+            if (sr == 2) sr = skip::skip_box(w, lo, hi, bound, cells);
+            VPX_PH(cf += __builtin_amdgcn_s_memtime() - t2;)
+            if (sr == 1) {
                 mode = kMiss;
             } else {
                 ++cells;  // visit the landing cell, then take the leaving event
                 mode = skip::step1(w, g.n) ? kStep : kMiss;
             }
         }
+        VPX_PH(ck += __builtin_amdgcn_s_memtime() - t1;)
     }
+#ifdef VPX_PHASE_PROF
+    if ((threadIdx.x & 63) == __builtin_amdgcn_readfirstlane(threadIdx.x & 63)) {
+        atomicAdd(&g_phase[0], cs);
+        atomicAdd(&g_phase[1], ck);
+        atomicAdd(&g_phase[2], ns);
+        atomicAdd(&g_phase[3], nk);
+        atomicAdd(&g_phase[4], ls);
+        atomicAdd(&g_phase[5], lk);
+        atomicAdd(&g_phase[6], 1ull);
+        atomicAdd(&g_phase[7], fb);
+        atomicAdd(&g_phase[8], cf);
+    }
+#endif
     return mode == kHit;
 }
 

@@ -62,6 +62,7 @@ struct WaveBufs {
     float4* SD;    // [S][P] shadow direction, w = slot flags bits
     float4* SL;    // [S][P] unoccluded contribution of the slot
     float4* SM;    // [P] pending light: xyz = kd (area), w = bits(kind | discard<<3 | count<<4 | level<<8 | lc<<16)
+    uint32_t* smask;  // [P] shadow slots emitted this level (bit s = slot s)
     uint32_t P;    // paths (pixels) this call
     uint32_t S;    // shadow slots per path
 };
@@ -122,63 +123,6 @@ __device__ __forceinline__ void flush_counters(const Counters& k, uint32_t prima
         if (ce) atomicAdd(&ctr[2], (unsigned long long)ce);
         if (pr) atomicAdd(&ctr[3], (unsigned long long)pr);
     }
-}
-
-// ------------------------------------------------------------------- stage 1
-// FIRST: generate the primary ray (and the pixel's RNG state) and mark the path active.
-template <bool FIRST>
-__global__ __launch_bounds__(256) void k_nearest(SceneView sv, FrameArgs f, WaveBufs w, unsigned long long* ctr) {
-    const uint32_t p = blockIdx.x * 256u + threadIdx.x;
-    Counters k{0u, 0u, 0u};
-    uint32_t prim = 0;
-    if (p < w.P) {
-        Ray r;
-        uint32_t rng, flags;
-        bool go;
-        if (FIRST) {
-            uint32_t x, y;
-            go = path_pixel(f, p, x, y);
-            flags = go ? kActive : 0u;
-            w.depth[p] = f.max_bounces;
-            w.forms[p] = 0u;
-            if (go) {
-                Rng g{pixel_seed(f.seed_base, f.frame_index, f.width, f.height, x, y)};
-                r = primary_ray(f, x, y, g);
-                rng = g.s;
-                prim = 1;
-            } else {
-                rng = 0;
-                r.O = r.D = mk(0.f, 0.f, 0.f);
-                r.inside = false;
-            }
-            w.leaf[p] = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (f.max_bounces < 0) {  // Trace(ray, -1) returns 0 without a lookup
-                flags = 0u;
-                go = false;
-            }
-        } else {
-            const float4 o = w.O[p], d = w.D[p];
-            flags = __float_as_uint(d.w);
-            go = (flags & kActive) != 0u;
-            r.O = mk(o.x, o.y, o.z);
-            r.D = mk(d.x, d.y, d.z);
-            r.inside = (flags & kInside) != 0u;
-            rng = __float_as_uint(o.w);
-        }
-        if (go) {
-            r.t = kBig;
-            r.mat = kNone;
-            r.N = mk(0.f, 0.f, 0.f);
-            const int32_t vox = find_nearest(sv, r, k);
-            w.H[p] = make_float4(r.t, r.N.x, r.N.y, r.N.z);
-            w.HM[p] = r.mat | ((uint32_t)(vox + 2) << 8) | (r.inside ? 0x80000000u : 0u);
-        }
-        if (FIRST) {
-            w.O[p] = make_float4(r.O.x, r.O.y, r.O.z, __uint_as_float(rng));
-            w.D[p] = make_float4(r.D.x, r.D.y, r.D.z, __uint_as_float(flags));
-        }
-    }
-    flush_counters(k, prim, ctr);
 }
 
 // ------------------------------------------------------------------- stage 2
@@ -299,15 +243,11 @@ __device__ __forceinline__ uint32_t wave_append(uint32_t cnt, uint32_t* len) {
     return base + off;
 }
 
-// shadow_list / next_list (optional): compact work lists for the persistent DDA kernels
-// (entry = slot << 27 | path for shadows, path for the next level's FindNearest).
 __global__ __launch_bounds__(256) void k_shade(SceneView sv, FrameArgs f, WaveBufs w, int level,
-                                               unsigned long long* ctr, uint32_t* shadow_list, uint32_t* shadow_len,
-                                               uint32_t* next_list, uint32_t* next_len) {
+                                               unsigned long long* ctr) {
     const uint32_t p = blockIdx.x * 256u + threadIdx.x;
     Counters k{0u, 0u, 0u};
     uint32_t slots = 0;
-    bool next_active = false;
     if (p < w.P) {
         float4 od = w.D[p];
         uint32_t flags = __float_as_uint(od.w);
@@ -445,7 +385,6 @@ __global__ __launch_bounds__(256) void k_shade(SceneView sv, FrameArgs f, WaveBu
                 w.D[p] = make_float4(next.D.x, next.D.y, next.D.z, __uint_as_float(flags));
                 w.depth[p] = depth;
                 w.forms[p] = forms;
-                next_active = !done;
             }
             if (done) {
                 w.leaf[p] = make_float4(leaf.x, leaf.y, leaf.z, 0.f);
@@ -456,15 +395,7 @@ __global__ __launch_bounds__(256) void k_shade(SceneView sv, FrameArgs f, WaveBu
         }
         if (!pending) w.SM[p] = make_float4(0.f, 0.f, 0.f, __uint_as_float(0u));
     }
-    if (shadow_list) {  // wave-uniform
-        const uint32_t c = (uint32_t)__popc(slots);
-        uint32_t at = wave_append(c, shadow_len);
-        for (uint32_t m = slots; m; m &= m - 1u) shadow_list[at++] = ((uint32_t)__ffs(m) - 1u) << 27 | p;
-    }
-    if (next_list) {
-        const uint32_t at = wave_append(next_active ? 1u : 0u, next_len);
-        if (next_active) next_list[at] = p;
-    }
+    if (p < w.P) w.smask[p] = slots;
     flush_counters(k, 0u, ctr);
 }
 
@@ -496,45 +427,160 @@ __global__ __launch_bounds__(256) void k_resolve(SceneView sv, WaveBufs w) {
     w.LB[(uint64_t)lvl * w.P + p] = make_float4(inc.x, inc.y, inc.z, 0.f);
 }
 
-// ------------------------------------------------------------------- stage 3
-// Renderer::IsOccluded for the level's shadow rays, in the evaluator's order, then the
-// light sum exactly as the evaluators and Illumination form it.
-__global__ __launch_bounds__(256) void k_shadow(SceneView sv, WaveBufs w, unsigned long long* ctr) {
+// ------------------------------------------------------------ tile kernels
+// Minimum waves per SIMD requested for the DDA kernels (caps their VGPRs: the walks are
+// bound by dependent mask loads, so residency matters more than a few spilled values).
+#ifndef VPX_WPE_NEAREST
+#define VPX_WPE_NEAREST 5
+#endif
+#ifndef VPX_WPE_SHADOW
+#define VPX_WPE_SHADOW 5
+#endif
+#define VPX_WPE(n) __attribute__((amdgpu_waves_per_eu(n)))
+
+// One 256-thread workgroup per 16x16 tile.  Work is compacted inside the tile through LDS
+// (no global atomics), so a DDA wave only carries rays that will actually march, and the
+// waves of a sparse tile retire at once.
+
+// Rank of this thread's `cnt` items among the workgroup's (exclusive), and the total.
+__device__ __forceinline__ uint32_t block_scan(uint32_t cnt, uint32_t& total, uint32_t* sh) {
+    uint32_t wt;
+    const uint32_t off = wave_prefix(cnt, wt);
+    const uint32_t wid = threadIdx.x >> 6;
+    if ((threadIdx.x & 63u) == 0) sh[wid] = wt;
+    __syncthreads();
+    uint32_t base = 0;
+    total = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < 4; ++i) {
+        const uint32_t v = sh[i];
+        base += i < wid ? v : 0u;
+        total += v;
+    }
+    __syncthreads();
+    return base + off;
+}
+
+__device__ __forceinline__ void nearest_record(SceneView sv, const WaveBufs& w, uint32_t p, Ray& r, Counters& k) {
+    r.t = kBig;
+    r.mat = kNone;
+    r.N = mk(0.f, 0.f, 0.f);
+    const int32_t vox = find_nearest(sv, r, k);
+    w.H[p] = make_float4(r.t, r.N.x, r.N.y, r.N.z);
+    w.HM[p] = r.mat | ((uint32_t)(vox + 2) << 8) | (r.inside ? 0x80000000u : 0u);
+}
+
+// Primary rays + Renderer::FindNearest.  Every path's ray / RNG state is written; rays
+// that cannot hit a voxel or shape (one volume, no shapes, Setup3DDDA fails: the
+// reference returns before reading a cell) get their miss record directly.
+__global__ __launch_bounds__(256) VPX_WPE(VPX_WPE_NEAREST) void k_primary(SceneView sv, FrameArgs f, WaveBufs w,
+                                                 unsigned long long* __restrict__ ctr) {
+    __shared__ uint32_t sh[4];
+    __shared__ uint32_t lst[256];
     const uint32_t p = blockIdx.x * 256u + threadIdx.x;
     Counters k{0u, 0u, 0u};
+    uint32_t prim = 0;
+    bool walk = false;
     if (p < w.P) {
-        const float4 sm = w.SM[p];
-        const uint32_t pend = __float_as_uint(sm.w);
-        if (pend) {
-            const uint32_t kind = pend & 7u, count = (pend >> 4) & 15u, lvl = (pend >> 8) & 31u;
-            const uint32_t lc = pend >> 16;
-            const bool discard = (pend & 8u) != 0u;
-            f3 acc = mk(0.f, 0.f, 0.f);
-            for (uint32_t s = 0; s < count; ++s) {
-                const uint64_t i = (uint64_t)s * w.P + p;
-                const float4 sd = w.SD[i];
-                const uint32_t fl = __float_as_uint(sd.w);
-                if (!(fl & kSlotValid)) continue;
-                const float4 so = w.SO[i];
-                Ray r;
-                r.O = mk(so.x, so.y, so.z);
-                r.D = mk(sd.x, sd.y, sd.z);
-                r.t = so.w;
-                const bool occ = shadow(sv, r, k);
-                if (occ) continue;
-                const float4 v = w.SL[i];
-                if (kind == kLightArea)
-                    acc = acc + mk(v.x, v.y, v.z);
-                else
-                    acc = mk(v.x, v.y, v.z);
-            }
-            if (!discard) {
-                f3 inc = acc;
-                if (kind == kLightArea) inc = (acc / (float)sv.area_samples) * mk(sm.x, sm.y, sm.z);
-                inc = inc * (float)lc;
-                w.LB[(uint64_t)lvl * w.P + p] = make_float4(inc.x, inc.y, inc.z, 0.f);
+        uint32_t x, y;
+        bool go = path_pixel(f, p, x, y);
+        w.depth[p] = f.max_bounces;
+        w.forms[p] = 0u;
+        w.leaf[p] = make_float4(0.f, 0.f, 0.f, 0.f);
+        Ray r;
+        r.O = r.D = mk(0.f, 0.f, 0.f);
+        uint32_t rng = 0, flags = 0;
+        if (go) {
+            Rng g{pixel_seed(f.seed_base, f.frame_index, f.width, f.height, x, y)};
+            r = primary_ray(f, x, y, g);
+            rng = g.s;
+            prim = 1;
+            flags = kActive;
+        }
+        if (f.max_bounces < 0) {  // Trace(ray, -1) returns 0 without a lookup
+            go = false;
+            flags = 0u;
+        }
+        w.O[p] = make_float4(r.O.x, r.O.y, r.O.z, __uint_as_float(rng));
+        w.D[p] = make_float4(r.D.x, r.D.y, r.D.z, __uint_as_float(flags));
+        if (go) {
+            walk = true;
+            if (sv.num_volumes == 1 && !(sv.num_spheres | sv.num_triangles)) {
+                const vpx_volume& vol = sv.volumes[0];
+                ORay o;
+                o.O = xform_pos_ssem(r.O, vol.inv_matrix);
+                o.D = xform_vec_ssem(r.D, vol.inv_matrix);
+                o.rD = mk(1.0f / o.D.x, 1.0f / o.D.y, 1.0f / o.D.z);
+                Dda s;
+                if (!dda_setup(vol, sv.grids[vol.grid_id].n, o, s)) {
+                    walk = false;
+                    ++k.nearest;
+                    w.H[p] = make_float4(kBig, 0.f, 0.f, 0.f);
+                    w.HM[p] = kNone;  // vox -2, not inside glass
+                }
             }
         }
+    }
+    uint32_t total;
+    const uint32_t at = block_scan(walk ? 1u : 0u, total, sh);
+    if (walk) lst[at] = p;
+    __syncthreads();
+    if (threadIdx.x < total) {
+        const uint32_t q = lst[threadIdx.x];
+        const float4 o = w.O[q], d = w.D[q];
+        Ray r;
+        r.O = mk(o.x, o.y, o.z);
+        r.D = mk(d.x, d.y, d.z);
+        r.inside = false;
+        nearest_record(sv, w, q, r, k);
+    }
+    flush_counters(k, prim, ctr);
+}
+
+// Renderer::FindNearest for the tile's active paths (bounce levels).
+__global__ __launch_bounds__(256) VPX_WPE(VPX_WPE_NEAREST) void k_nearest_tile(SceneView sv, WaveBufs w, unsigned long long* __restrict__ ctr) {
+    __shared__ uint32_t sh[4];
+    __shared__ uint32_t lst[256];
+    const uint32_t p = blockIdx.x * 256u + threadIdx.x;
+    Counters k{0u, 0u, 0u};
+    const bool act = p < w.P && (__float_as_uint(w.D[p].w) & kActive);
+    uint32_t total;
+    const uint32_t at = block_scan(act ? 1u : 0u, total, sh);
+    if (act) lst[at] = p;
+    __syncthreads();
+    if (threadIdx.x < total) {
+        const uint32_t q = lst[threadIdx.x];
+        const float4 o = w.O[q], d = w.D[q];
+        Ray r;
+        r.O = mk(o.x, o.y, o.z);
+        r.D = mk(d.x, d.y, d.z);
+        r.inside = (__float_as_uint(d.w) & kInside) != 0u;
+        nearest_record(sv, w, q, r, k);
+    }
+    flush_counters(k, 0u, ctr);
+}
+
+// Renderer::IsOccluded for the tile's shadow slots (entry = slot << 27 | path); sets the
+// slot's occluded flag.  The light sums are formed in slot order by k_resolve.
+__global__ __launch_bounds__(256) VPX_WPE(VPX_WPE_SHADOW) void k_shadow_tile(SceneView sv, WaveBufs w, unsigned long long* __restrict__ ctr) {
+    __shared__ uint32_t sh[4];
+    extern __shared__ uint32_t lst_dyn[];  // [S * 256]
+    const uint32_t p = blockIdx.x * 256u + threadIdx.x;
+    Counters k{0u, 0u, 0u};
+    const uint32_t m = p < w.P ? w.smask[p] : 0u;
+    uint32_t total;
+    uint32_t at = block_scan((uint32_t)__popc(m), total, sh);
+    for (uint32_t b = m; b; b &= b - 1u) lst_dyn[at++] = ((uint32_t)__ffs(b) - 1u) << 27 | p;
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < total; i += 256u) {
+        const uint32_t e = lst_dyn[i];
+        const uint64_t slot = (uint64_t)(e >> 27) * w.P + (e & 0x07ffffffu);
+        const float4 so = w.SO[slot], sd = w.SD[slot];
+        Ray r;
+        r.O = mk(so.x, so.y, so.z);
+        r.D = mk(sd.x, sd.y, sd.z);
+        r.t = so.w;
+        if (shadow(sv, r, k)) w.SD[slot].w = __uint_as_float(__float_as_uint(sd.w) | 4u /* occluded */);
     }
     flush_counters(k, 0u, ctr);
 }

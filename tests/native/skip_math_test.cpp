@@ -76,3 +76,84 @@ int udiv_check() {
     return bad != 0;
 }
 static int _udiv = (udiv_check() ? (exit(1), 1) : 0);
+
+// (appended) ceil_div_q with perturbed quotients, as the device forms them (rcp * p)
+int ceil_check() {
+    std::mt19937_64 r(11);
+    long bad = 0;
+    for (long i = 0; i < 20000000; ++i) {
+        const uint32_t c = 1 + (uint32_t)(r() % ((i % 3) ? (1u << 23) : 64u));
+        const uint32_t p = 1 + (uint32_t)(r() % ((i % 2) ? (1u << 24) : (uint64_t)c * 70));
+        const double eps = ((double)(r() % 2001) - 1000.0) * 1e-9;
+        const float q = (float)(((double)p / c) * (1.0 + eps));
+        const uint64_t want = ((uint64_t)p + c - 1) / c;
+        const uint32_t got = vpx::skip::ceil_div_q(p, c, q);
+        if (want <= 1024 ? got != want : got <= 1024) { if (bad < 5) printf("ceil bad %u/%u got %u\n", p, c, got); ++bad; }
+    }
+    printf("ceil_div bad=%ld\n", bad);
+    return bad != 0;
+}
+static int _ceil = (ceil_check() ? (exit(1), 1) : 0);
+
+// (appended) skip_box_fast against the general skip_box on random and adversarial states
+static float rnd_head(std::mt19937_64& r, std::uniform_real_distribution<double>& U, int kind) {
+    switch (kind) {
+        case 0: return (float)std::exp(std::log(1e-3) + U(r) * (std::log(8.0) - std::log(1e-3)));
+        case 1: return std::nextafter((float)std::ldexp(1.0, (int)(r() % 6) - 3), 0.f) - (float)(U(r) * 1e-3);  // just below 2^k
+        default: return (float)std::ldexp(1.0, (int)(r() % 6) - 3) * (float)(1.0 + (r() % 64) * std::ldexp(1.0, -20));
+    }
+}
+int fast_check() {
+    using namespace vpx::skip;
+    std::mt19937_64 r(99);
+    std::uniform_real_distribution<double> U(0.0, 1.0);
+    long bad = 0, handled = 0, total = 0;
+    for (long i = 0; i < 4000000; ++i) {
+        Walk w{};
+        const uint32_t m = (i & 1) ? 63u : 15u;
+        uint32_t lo[3], hi[3];
+        uint32_t* C3[3] = {&w.X, &w.Y, &w.Z};
+        float* H3[3] = {&w.tx, &w.ty, &w.tz};
+        float* D3[3] = {&w.dx, &w.dy, &w.dz};
+        int32_t* S3[3] = {&w.sx, &w.sy, &w.sz};
+        float tmin = 1e30f;
+        for (int k = 0; k < 3; ++k) {
+            lo[k] = (uint32_t)(r() % 8) * (m + 1);
+            hi[k] = lo[k] + m;
+            *C3[k] = lo[k] + (uint32_t)(r() % (m + 1));
+            *S3[k] = (r() & 1) ? 1 : -1;
+            const float h = rnd_head(r, U, (int)(r() % 3));
+            float d;
+            switch (r() % 4) {
+                case 0: d = (float)std::exp(std::log(1e-5) + U(r) * (std::log(0.5) - std::log(1e-5))); break;
+                case 1: d = h * (float)std::ldexp(1.0, -(int)(1 + r() % 26)); break;  // ties / stuck
+                case 2: d = (float)std::ldexp(1.0, -(int)(4 + r() % 12)) * (float)(1 + r() % 8); break;
+                default: d = h * (float)(U(r) * 0.05); break;
+            }
+            *H3[k] = h;
+            *D3[k] = d;
+            tmin = h < tmin ? h : tmin;
+        }
+        w.t = tmin * (float)U(r);
+        const float hmax = w.tx > w.ty ? (w.tx > w.tz ? w.tx : w.tz) : (w.ty > w.tz ? w.ty : w.tz);
+        const int bk = (int)(r() % 4);
+        const float bound = bk == 0 ? 1e34f : bk == 1 ? INFINITY : (float)(tmin + U(r) * (hmax * 4 - tmin));
+        Walk a = w, b = w;
+        uint32_t ca = 7, cb = 7;
+        const int ra = skip_box_fast(a, lo, hi, bound, ca);
+        ++total;
+        if (ra == 2) continue;
+        ++handled;
+        const int rb = skip_box(b, lo, hi, bound, cb);
+        const bool same = ra == rb && ca == cb && (ra == 1 || (!memcmp(&a, &b, sizeof(Walk))));
+        if (!same) {
+            if (bad < 10)
+                printf("fast mismatch r %d/%d cells %u/%u t %a/%a h (%a %a %a)/(%a %a %a) XYZ (%u %u %u)/(%u %u %u)\n", ra, rb, ca, cb, a.t, b.t,
+                       a.tx, a.ty, a.tz, b.tx, b.ty, b.tz, a.X, a.Y, a.Z, b.X, b.Y, b.Z);
+            ++bad;
+        }
+    }
+    printf("skip_box_fast: %ld/%ld handled, bad=%ld\n", handled, total, bad);
+    return bad != 0;
+}
+static int _fast = (fast_check() ? (exit(1), 1) : 0);

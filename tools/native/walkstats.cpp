@@ -18,6 +18,38 @@ extern "C" void build_masks(const uint8_t* cells, uint32_t n, uint64_t* l1, uint
         if (l2[x + y * nb2 + z * nb2 * nb2]) l3[(x >> 2) + (y >> 2) * nb3 + (z >> 2) * nb3 * nb3] |= 1ull << ((x & 3) + 4 * (y & 3) + 16 * (z & 3));
 }
 
+static bool fast_ok(const Walk& w, const uint32_t lo[3], const uint32_t hi[3]) {
+    const float h[3] = {w.tx, w.ty, w.tz}, d[3] = {w.dx, w.dy, w.dz};
+    const int32_t s[3] = {w.sx, w.sy, w.sz};
+    const uint32_t c[3] = {w.X, w.Y, w.Z};
+    for (int k = 0; k < 3; ++k) {
+        if (!(h[k] > 0.0f) || !(d[k] > 0.0f)) return false;
+        const uint32_t e = s[k] > 0 ? hi[k] - c[k] + 1u : c[k] - lo[k] + 1u;
+        const Seg g = segment(h[k], d[k]);
+        if (!g.ok || g.stuck) return false;
+        if ((uint64_t)(e - 1u) * g.c > 0xffffffu - g.b) return false;
+    }
+    return true;
+}
+
+static uint64_t g_why[8];
+static void why(const Walk& w, const uint32_t lo[3], const uint32_t hi[3]) {
+    const float h[3] = {w.tx, w.ty, w.tz}, d[3] = {w.dx, w.dy, w.dz};
+    const int32_t s[3] = {w.sx, w.sy, w.sz};
+    const uint32_t c[3] = {w.X, w.Y, w.Z};
+    for (int k = 0; k < 3; ++k) {
+        const uint32_t e = s[k] > 0 ? hi[k] - c[k] + 1u : c[k] - lo[k] + 1u;
+        const uint32_t ab = fbits(h[k]), db = fbits(d[k]), ea = ab >> 23, ed = db >> 23;
+        if (ea - 1u >= 254u || ed - 1u >= 254u) { g_why[0]++; continue; }
+        if (ed >= ea) { g_why[1]++; continue; }
+        uint32_t b, cc, ee;
+        if (!seg_params(h[k], d[k], b, cc, ee)) { g_why[2]++; continue; }
+        Seq2 q;
+        if (!seq2_init(h[k], d[k], e - 1, q)) { g_why[3]++; continue; }
+    }
+}
+extern "C" void why_out(uint64_t* o) { for (int i = 0; i < 8; ++i) o[i] = g_why[i]; }
+
 // walks: setup state per ray given as (X,Y,Z,t,tx,ty,tz,dx,dy,dz,sx,sy,sz) float/int arrays
 extern "C" void walk_stats(const uint8_t* cells, const uint64_t* l1, const uint64_t* l2, const uint64_t* l3, uint32_t n,
                            const float* st, const int32_t* si, uint32_t nrays, float bound, uint64_t* out /*8*/) {
@@ -44,6 +76,7 @@ extern "C" void walk_stats(const uint8_t* cells, const uint64_t* l1, const uint6
                 uint32_t hi[3] = {lo[0] + m, lo[1] + m, lo[2] + m};
                 for (int k = 0; k < 3; ++k) hi[k] = hi[k] < n - 1u ? hi[k] : n - 1u;
                 const uint32_t before = c;
+                { Walk t = w; uint32_t cc = 0; const bool okf = skip_box_fast(t, lo, hi, bound, cc) != 2; out[7] += okf; if (!okf) why(w, lo, hi); }
                 const int rr = skip_box(w, lo, hi, bound, c);
                 if (rr == 1) break;
                 if (c == before) ++land0;

@@ -49,4 +49,8 @@ lib.walk_stats(cells.ctypes.data, l1.ctypes.data, l2.ctypes.data, l3.ctypes.data
                np.ascontiguousarray(si).ctypes.data, len(st), C.c_float(1e34), out.ctypes.data)
 R = len(st)
 print(f"{cfg}: rays entering grid {R}/{m}; per ray: cells {out[0]/R:.1f} iters {out[1]/R:.1f} steps {out[2]/R:.1f} "
-      f"skip16 {out[3]/R:.2f} skip64 {out[4]/R:.2f} zero-skips {out[5]/R:.2f} max iters {out[6]}")
+      f"skip16 {out[3]/R:.2f} skip64 {out[4]/R:.2f} zero-skips {out[5]/R:.2f} max iters {out[6]} fast-path skips {out[7]/max(out[3]+out[4],1):.3f}")
+wy = np.zeros(8, np.uint64)
+lib.why_out.argtypes = [V]
+lib.why_out(wy.ctypes.data)
+print("fast-path failures by axis reason (nonnormal, d>=2^E, tie/stuck, 2nd crossing):", wy[:4])
