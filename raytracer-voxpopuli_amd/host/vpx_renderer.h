@@ -1,0 +1,74 @@
+// vpx_renderer.h — C++ host mirror of the reference Renderer's hot-path surface.
+//
+// The reference keeps its game loop in `Renderer::Tick(float deltaTime)` (renderer.cpp:1972,
+// virtual in template/precomp.h:399) and renders with `Renderer::Update()`
+// (renderer.cpp:1646-1891): a parallel loop over pixels calling `Trace(ray, maxBounces)`,
+// a running-average accumulator and a Reinhard-Jodie tonemap into `Surface::pixels`.
+// This class keeps that surface — same member names, same meaning — and replaces the loop
+// by ONE call into libvpx_hip.so (include/vpx.h).  It talks to the library only through
+// the C-ABI; HIP is used here just for the two HBM frame buffers and the D2H copy.
+//
+// Errors: every method returns the VPX_* status of the first failing call (0 = ok) and
+// never throws; `LastError()` is the library's message.
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/vpx.h"
+
+namespace vpxhost {
+
+class Renderer {
+public:
+    explicit Renderer(int device = 0);
+    ~Renderer();
+    Renderer(const Renderer&) = delete;
+    Renderer& operator=(const Renderer&) = delete;
+
+    // Renderer::Init minus window/asset/game setup (renderer.cpp:688-736): frame buffers.
+    int Init(uint32_t width, uint32_t height);
+
+    // --- world (the host owns Scene::grid; the library keeps the device copy) -----------
+    int UploadGrid(uint32_t grid_id, const uint8_t* cells, uint32_t n);  // Scene::grid
+    int SetVolumes(const std::vector<vpx_volume>& volumes);               // voxelVolumes
+    int SetMaterials(const std::vector<vpx_material>& materials);         // materials
+    int SetLights(const std::vector<vpx_point_light>& points, const std::vector<vpx_spot_light>& spots,
+                  const std::vector<vpx_area_light>& areas, const vpx_dir_light& dir);
+    int SetShapes(const std::vector<vpx_sphere>& spheres, const std::vector<vpx_triangle>& triangles);
+    // Camera::camPos / camTarget + HandleInput(0) (template/camera.h:113-181).
+    int LookAt(const float pos[3], const float target[3]);
+
+    // --- per frame -----------------------------------------------------------------------
+    void ResetAccumulator() { numRenderedFrames = 0; }  // renderer.cpp:343-346
+    int Update(vpx_stats* stats = nullptr);             // renderer.cpp:1646-1891
+    int Tick(float deltaTime, vpx_stats* stats = nullptr);
+    // Surface::pixels (0x00RRGGBB, W*H) for display: device -> host copy of the frame.
+    int CopyScreen(uint32_t* host_pixels) const;
+    int CopyAccumulator(float* host_rgba) const;
+
+    const char* LastError() const;
+    vpx_ctx* Context() const { return ctx_; }
+
+    // Members of the reference Renderer this path reads (renderer.h:175-205).
+    int32_t maxBounces = 0;
+    uint32_t numRenderedFrames = 0;
+    float antiAliasingStrength = 1.0f;
+    int32_t numCheckShadowsAreaLight = 3;
+    bool staticCamera = false;  // reprojection branch: out of scope
+    uint32_t flags = 0;         // VPX_FLAG_AA / VPX_FLAG_DOF
+    float sky[3] = {0.392f, 0.584f, 0.829f};  // SampleSky, activateSky == false (renderer.cpp:2310-2313)
+    vpx_camera camera{};
+
+private:
+    int status_ = VPX_OK;
+    int device_ = 0;
+    vpx_ctx* ctx_ = nullptr;
+    uint32_t width_ = 0, height_ = 0;
+    float* accumulator_ = nullptr;  // float4[W*H] in HBM
+    uint32_t* screen_ = nullptr;    // uint32[W*H] in HBM
+    std::string err_;
+};
+
+}  // namespace vpxhost

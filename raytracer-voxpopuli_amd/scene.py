@@ -268,6 +268,24 @@ def city_scene(model="monu3", n=1024, width=1920, height=1080, max_bounces=0, ar
                   width, height, max_bounces=max_bounces)
 
 
+def pillars_grid(n):
+    """The procedural world of host/vpx_demo.cpp (same formula, for the C++-host test)."""
+    z, y, x = np.meshgrid(np.arange(n, dtype=np.int64), np.arange(n, dtype=np.int64), np.arange(n, dtype=np.int64),
+                          indexing="ij")
+    h = ((x >> 4) * 7 + (z >> 4) * 13) % 5 * n // 16
+    g = np.full((n, n, n), 255, np.uint8)
+    pil = ((x & 15) < 8) & ((z & 15) < 8) & (y < 2 + h)
+    g[pil] = (16 + h % 4)[pil].astype(np.uint8)
+    g[y < 2] = 0
+    return g.reshape(-1)
+
+
+def pillars_scene(n=256, width=640, height=360, max_bounces=0):
+    grid = GridSpec(n=n, dense=pillars_grid(n))
+    return _scene(f"pillars{n}", [grid], [volume()], default_materials(), list(CITY_LIGHTS["points"]), [], [],
+                  CITY_LIGHTS["dir_light"], CITY_CAM[0], CITY_CAM[1], width, height, max_bounces=max_bounces)
+
+
 C3_AREAS = [area_light((0.5, 2.0, 0.5)), area_light((-1.5, 1.5, 0.5)), area_light((2.5, 1.5, 0.5)),
             area_light((0.5, 1.5, -1.5))]
 

@@ -53,3 +53,18 @@ def test_host_helpers_reject_bad_arguments(pkg):
     assert lib.vpx_default_materials(None) == -1
     assert lib.vpx_tiles_packed_len(0, 10, 16, 16, 1) == 0
     assert lib.vpx_tiles_packed_len(33, 17, 16, 16, 2) == 3 * 256  # 6 tiles over 2 ranks
+
+
+def test_cpp_host_mirror_links_and_fails_cleanly_without_gpu(pkg):
+    """host/vpx_demo (the C++ Renderer mirror) is built, links libvpx_hip.so, and reports a
+    clean error (no abort) when no GPU is visible."""
+    import os
+    import subprocess
+
+    torch = pytest.importorskip("torch")
+    exe = os.path.join(os.path.dirname(pkg.__file__), "host", "vpx_demo")
+    assert os.path.exists(exe), "run __graft_entry__.build()"
+    if torch.cuda.device_count() > 0:
+        pytest.skip("a GPU is present (covered by test_gpu_parity)")
+    r = subprocess.run([exe, "16", "8", "8", "1"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 1 and "no usable HIP device" in r.stderr

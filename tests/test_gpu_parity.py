@@ -5,6 +5,7 @@ of the radiance / accumulator, and every RGB8 byte.  The oracle itself is "parit
 unpinned" against the reference; these tests pin the GPU to the oracle.
 """
 import ctypes as C
+import os
 
 import numpy as np
 import pytest
@@ -213,3 +214,25 @@ def test_degenerate_worlds(pkg, orc, fill):
     acc_g, rgb_g, _ = render_gpu(pkg, desc)
     acc_o, rgb_o, _ = orc.Oracle(pkg.abi, desc).render(desc.frame_params(0))
     assert np.array_equal(bits(acc_g), bits(acc_o)) and np.array_equal(rgb_g, rgb_o)
+
+
+def test_cpp_host_demo_matches_oracle(pkg, orc, tmp_path):
+    """The C++ host mirror (host/vpx_renderer.cpp via host/vpx_demo) drives the C-ABI like the
+    integrated game loop would: 3 accumulated frames, depth 1, equal to the oracle."""
+    import subprocess
+
+    exe = os.path.join(os.path.dirname(pkg.__file__), "host", "vpx_demo")
+    if not os.path.exists(exe):
+        pytest.fail("host/vpx_demo missing: run __graft_entry__.build()")
+    n, w, h, frames, depth = 64, 96, 64, 3, 1
+    out = tmp_path / "frame.rgb8"
+    r = subprocess.run([exe, str(n), str(w), str(h), str(frames), str(depth), str(out)], capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    rgb_cpp = np.fromfile(out, np.uint32)
+    desc = pkg.scene.pillars_scene(n, w, h, depth)
+    o = orc.Oracle(pkg.abi, desc)
+    acc = None
+    for f in range(frames):
+        acc, rgb, _ = o.render(desc.frame_params(f), accum=acc)
+    assert np.array_equal(rgb_cpp, rgb)
