@@ -142,41 +142,57 @@ __global__ void tiled_world_k(uint8_t* __restrict__ out, uint32_t n, const uint8
 }
 
 // ------------------------------------------------------------- occupancy masks
-// l1: one thread per 4x4x4 brick reads its 64 cells (16 rows of 4 bytes).
-__global__ void build_l1_k(const uint8_t* __restrict__ cells, uint32_t n, uint32_t nb1, uint64_t* __restrict__ l1) {
-    const uint64_t total = (uint64_t)nb1 * nb1 * nb1;
+// Layout: vpx_skip.hpp blk_index (l1, l2 blocked by parent) / lin_index (l3).
+// l1: one thread per output word (padded space nb2^3 * 64) reads its brick's 64 cells.
+__global__ void build_l1_k(const uint8_t* __restrict__ cells, uint32_t n, uint32_t nb1, uint32_t nb2,
+                           uint64_t* __restrict__ l1) {
+    const uint64_t total = (uint64_t)nb2 * nb2 * nb2 * 64;
     const uint64_t n64 = n;
-    for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b < total; b += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t bx = (uint32_t)(b % nb1), by = (uint32_t)((b / nb1) % nb1), bz = (uint32_t)(b / ((uint64_t)nb1 * nb1));
+    for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < total; s += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t parent = s >> 6;
+        const uint32_t j = (uint32_t)(s & 63u);
+        const uint32_t bx = (uint32_t)(parent % nb2) * 4 + (j & 3u);
+        const uint32_t by = (uint32_t)((parent / nb2) % nb2) * 4 + ((j >> 2) & 3u);
+        const uint32_t bz = (uint32_t)(parent / ((uint64_t)nb2 * nb2)) * 4 + (j >> 4);
         uint64_t m = 0;
-        for (uint32_t lz = 0; lz < 4; ++lz)
-            for (uint32_t ly = 0; ly < 4; ++ly) {
-                const uint32_t y = by * 4 + ly, z = bz * 4 + lz;
-                if (y >= n || z >= n) continue;
-                const uint8_t* row = cells + (uint64_t)y * n64 + (uint64_t)z * n64 * n64;
-                for (uint32_t lx = 0; lx < 4; ++lx) {
-                    const uint32_t x = bx * 4 + lx;
-                    if (x < n && row[x] != kNone) m |= 1ull << (lx + 4 * ly + 16 * lz);
+        if (bx < nb1 && by < nb1 && bz < nb1) {
+            for (uint32_t lz = 0; lz < 4; ++lz)
+                for (uint32_t ly = 0; ly < 4; ++ly) {
+                    const uint32_t y = by * 4 + ly, z = bz * 4 + lz;
+                    if (y >= n || z >= n) continue;
+                    const uint8_t* row = cells + (uint64_t)y * n64 + (uint64_t)z * n64 * n64;
+                    for (uint32_t lx = 0; lx < 4; ++lx) {
+                        const uint32_t x = bx * 4 + lx;
+                        if (x < n && row[x] != kNone) m |= 1ull << (lx + 4 * ly + 16 * lz);
+                    }
                 }
-            }
-        l1[b] = m;
+        }
+        l1[s] = m;
     }
 }
 
-// l2: one thread per 16^3 macro ORs its 64 child brick masks into one bit each.
-__global__ void build_l2_k(const uint64_t* __restrict__ l1, uint32_t nb1, uint32_t nb2, uint64_t* __restrict__ l2) {
-    const uint64_t total = (uint64_t)nb2 * nb2 * nb2;
-    for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < total; c += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t cx = (uint32_t)(c % nb2), cy = (uint32_t)((c / nb2) % nb2), cz = (uint32_t)(c / ((uint64_t)nb2 * nb2));
+// One level up: the word of parent block P (np parents per axis, linear P) ORs the 64
+// consecutive child words child[P*64 + j] into bit j.  Output blocked by grandparent
+// (ngp per axis, words ngp^3 * 64) or linear (ngp == 0, words np^3).
+__global__ void build_up_k(const uint64_t* __restrict__ child, uint32_t np, uint32_t ngp, uint64_t* __restrict__ out) {
+    const uint64_t total = ngp ? (uint64_t)ngp * ngp * ngp * 64 : (uint64_t)np * np * np;
+    for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < total; s += (uint64_t)gridDim.x * blockDim.x) {
+        uint32_t px, py, pz;
+        if (ngp) {
+            const uint64_t gp = s >> 6;
+            const uint32_t j = (uint32_t)(s & 63u);
+            px = (uint32_t)(gp % ngp) * 4 + (j & 3u);
+            py = (uint32_t)((gp / ngp) % ngp) * 4 + ((j >> 2) & 3u);
+            pz = (uint32_t)(gp / ((uint64_t)ngp * ngp)) * 4 + (j >> 4);
+        } else {
+            px = (uint32_t)(s % np), py = (uint32_t)((s / np) % np), pz = (uint32_t)(s / ((uint64_t)np * np));
+        }
         uint64_t m = 0;
-        for (uint32_t lz = 0; lz < 4; ++lz)
-            for (uint32_t ly = 0; ly < 4; ++ly)
-                for (uint32_t lx = 0; lx < 4; ++lx) {
-                    const uint32_t bx = cx * 4 + lx, by = cy * 4 + ly, bz = cz * 4 + lz;
-                    if (bx >= nb1 || by >= nb1 || bz >= nb1) continue;
-                    if (l1[(uint64_t)bx + (uint64_t)by * nb1 + (uint64_t)bz * nb1 * nb1]) m |= 1ull << (lx + 4 * ly + 16 * lz);
-                }
-        l2[c] = m;
+        if (px < np && py < np && pz < np) {
+            const uint64_t* c = child + (((uint64_t)pz * np + py) * np + px) * 64;
+            for (uint32_t j = 0; j < 64; ++j) m |= (c[j] != 0ull ? 1ull : 0ull) << j;
+        }
+        out[s] = m;
     }
 }
 
@@ -426,8 +442,13 @@ int launch_render(vpx_ctx* c, const SceneView& sv, const FrameArgs& f, uint32_t 
 }
 
 int snapshot_counters(vpx_ctx* c, unsigned long long out[4]) {
-    VPX_HIP(c, hipMemcpyAsync(out, c->d_ctr, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
+    unsigned long long all[4 * kCtrStripes];
+    VPX_HIP(c, hipMemcpyAsync(all, c->d_ctr, sizeof(all), hipMemcpyDeviceToHost, c->stream));
     VPX_HIP(c, hipStreamSynchronize(c->stream));
+    for (int i = 0; i < 4; ++i) {
+        out[i] = 0;
+        for (uint32_t s = 0; s < kCtrStripes; ++s) out[i] += all[4 * s + i];
+    }
     return VPX_OK;
 }
 
@@ -456,7 +477,7 @@ int vpx_create(int device, vpx_ctx** out) {
     if (!c) return VPX_E_NOMEM;
     c->device = device;
     if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess ||
-        hipMalloc(&c->d_ctr, 4 * sizeof(unsigned long long)) != hipSuccess ||
+        hipMalloc(&c->d_ctr, 4 * kCtrStripes * sizeof(unsigned long long)) != hipSuccess ||
         hipMalloc(&c->d_sum, sizeof(unsigned long long)) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
         hipEventCreate(&c->ev2) != hipSuccess) {
@@ -464,7 +485,7 @@ int vpx_create(int device, vpx_ctx** out) {
         return VPX_E_DEVICE;
     }
     c->stream = c->own_stream;
-    (void)hipMemset(c->d_ctr, 0, 4 * sizeof(unsigned long long));
+    (void)hipMemset(c->d_ctr, 0, 4 * kCtrStripes * sizeof(unsigned long long));
     *out = c;
     return VPX_OK;
 }
@@ -526,8 +547,8 @@ static int alloc_grid(vpx_ctx* c, uint32_t id, uint32_t n) {
     g.nb3 = (g.nb2 + 3) / 4;
     if (!g.ptr) {
         VPX_HIP(c, hipMalloc(&g.ptr, bytes));
-        VPX_HIP(c, hipMalloc(&g.l1, sizeof(uint64_t) * (size_t)g.nb1 * g.nb1 * g.nb1));
-        VPX_HIP(c, hipMalloc(&g.l2, sizeof(uint64_t) * (size_t)g.nb2 * g.nb2 * g.nb2));
+        VPX_HIP(c, hipMalloc(&g.l1, sizeof(uint64_t) * (size_t)g.nb2 * g.nb2 * g.nb2 * 64));
+        VPX_HIP(c, hipMalloc(&g.l2, sizeof(uint64_t) * (size_t)g.nb3 * g.nb3 * g.nb3 * 64));
         VPX_HIP(c, hipMalloc(&g.l3, sizeof(uint64_t) * (size_t)g.nb3 * g.nb3 * g.nb3));
     }
     return sync_grids(c);
@@ -536,11 +557,11 @@ static int alloc_grid(vpx_ctx* c, uint32_t id, uint32_t n) {
 // Rebuild the occupancy hierarchy after the grid bytes changed.
 static int build_masks(vpx_ctx* c, uint32_t id) {
     auto& g = c->grids[id];
-    hipLaunchKernelGGL(build_l1_k, dim3(2048), dim3(256), 0, c->stream, g.ptr, g.n, g.nb1, g.l1);
+    hipLaunchKernelGGL(build_l1_k, dim3(2048), dim3(256), 0, c->stream, g.ptr, g.n, g.nb1, g.nb2, g.l1);
     VPX_HIP(c, hipGetLastError());
-    hipLaunchKernelGGL(build_l2_k, dim3(512), dim3(256), 0, c->stream, g.l1, g.nb1, g.nb2, g.l2);
+    hipLaunchKernelGGL(build_up_k, dim3(512), dim3(256), 0, c->stream, g.l1, g.nb2, g.nb3, g.l2);
     VPX_HIP(c, hipGetLastError());
-    hipLaunchKernelGGL(build_l2_k, dim3(64), dim3(256), 0, c->stream, g.l2, g.nb2, g.nb3, g.l3);  // same OR-reduction one level up
+    hipLaunchKernelGGL(build_up_k, dim3(64), dim3(256), 0, c->stream, g.l2, g.nb3, 0u, g.l3);
     VPX_HIP(c, hipGetLastError());
     VPX_HIP(c, hipStreamSynchronize(c->stream));
     return VPX_OK;
@@ -731,7 +752,7 @@ int vpx_get_counters(vpx_ctx* c, vpx_stats* out, int reset) {
     std::memset(out, 0, sizeof(*out));
     fill_stats(out, zero, now);
     if (reset) {
-        VPX_HIP(c, hipMemsetAsync(c->d_ctr, 0, 4 * sizeof(unsigned long long), c->stream));
+        VPX_HIP(c, hipMemsetAsync(c->d_ctr, 0, 4 * kCtrStripes * sizeof(unsigned long long), c->stream));
         VPX_HIP(c, hipStreamSynchronize(c->stream));
     }
     return VPX_OK;

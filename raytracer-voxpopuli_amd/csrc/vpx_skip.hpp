@@ -252,24 +252,46 @@ struct Walk {
 
 VPX_HD uint32_t pack3(uint32_t a, uint32_t b, uint32_t c) { return a | (b << 11) | (c << 22); }
 
-// Mask word of block (bx, by, bz) in a level with nb blocks per axis.  nb <= 1024 (grids up
-// to 4096^3), so the index fits 32 bits and every product fits the 24-bit multiplier.
-VPX_HD uint64_t mask_at(const uint64_t* p, uint32_t nb, uint32_t bx, uint32_t by, uint32_t bz) {
+// Occupancy-level layout.  l1 (bricks) and l2 (macros) are stored BLOCKED: the 64 words
+// of one parent (a 4x4x4 group of blocks) are contiguous, parents in linear order.  A
+// wave's rays then share 128-byte lines across y/z neighbours too, and a parent's word
+// is the OR-reduction of 64 consecutive child words.  l3 is linear.  `np` = parents per
+// axis.  np <= 256 (grids up to 4096^3): every product fits the 24-bit multiplier.
+VPX_HD uint32_t blk_index(uint32_t bx, uint32_t by, uint32_t bz, uint32_t np) {
 #if defined(__HIP_DEVICE_COMPILE__)
-    const uint32_t i = __umul24(bz, __umul24(nb, nb)) + __umul24(by, nb) + bx;
+    const uint32_t parent = __umul24(bz >> 2, __umul24(np, np)) + __umul24(by >> 2, np) + (bx >> 2);
+#else
+    const uint32_t parent = (bz >> 2) * np * np + (by >> 2) * np + (bx >> 2);
+#endif
+    return (parent << 6) | (bx & 3u) | ((by & 3u) << 2) | ((bz & 3u) << 4);
+}
+
+VPX_HD uint64_t load_mask(const uint64_t* p, uint32_t i) {
+#if defined(__HIP_DEVICE_COMPILE__)
     return ((const __attribute__((address_space(1))) uint64_t*)p)[i];
 #else
-    return p[(uint64_t)bx + (uint64_t)by * nb + (uint64_t)bz * nb * nb];
+    return p[i];
+#endif
+}
+
+VPX_HD uint32_t lin_index(uint32_t x, uint32_t y, uint32_t z, uint32_t nb) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __umul24(z, __umul24(nb, nb)) + __umul24(y, nb) + x;
+#else
+    return z * nb * nb + y * nb + x;
 #endif
 }
 
 // 0: solid cell, 1: empty cell, 2: inside an empty 16^3 macro, 3: inside an empty 64^3 super.
+// Each level's word is cached by key; a step re-reads nothing unless it changed blocks.
+// (Checking only the brick key and walking the hierarchy on brick changes was measured
+// slower on the device: the per-wave divergence of that branch costs more than it saves.)
 VPX_HD int classify(Walk& w, const GridView& g) {
     const uint32_t X = w.X, Y = w.Y, Z = w.Z;
     const uint32_t k3 = pack3(X >> 6, Y >> 6, Z >> 6);
     if (k3 != w.k3) {
         w.k3 = k3;
-        w.m3 = mask_at(g.l3, g.nb3, X >> 6, Y >> 6, Z >> 6);
+        w.m3 = load_mask(g.l3, lin_index(X >> 6, Y >> 6, Z >> 6, g.nb3));
     }
     if (w.m3 == 0) return 3;
     const uint32_t mb = ((X >> 4) & 3u) | (((Y >> 4) & 3u) << 2) | (((Z >> 4) & 3u) << 4);
@@ -277,14 +299,14 @@ VPX_HD int classify(Walk& w, const GridView& g) {
     const uint32_t k2 = pack3(X >> 4, Y >> 4, Z >> 4);
     if (k2 != w.k2) {
         w.k2 = k2;
-        w.m2 = mask_at(g.l2, g.nb2, X >> 4, Y >> 4, Z >> 4);
+        w.m2 = load_mask(g.l2, blk_index(X >> 4, Y >> 4, Z >> 4, g.nb3));
     }
     const uint32_t bb = ((X >> 2) & 3u) | (((Y >> 2) & 3u) << 2) | (((Z >> 2) & 3u) << 4);
     if (!((w.m2 >> bb) & 1ull)) return 1;
     const uint32_t k1 = pack3(X >> 2, Y >> 2, Z >> 2);
     if (k1 != w.k1) {
         w.k1 = k1;
-        w.m1 = mask_at(g.l1, g.nb1, X >> 2, Y >> 2, Z >> 2);
+        w.m1 = load_mask(g.l1, blk_index(X >> 2, Y >> 2, Z >> 2, g.nb2));
     }
     const uint32_t cb = (X & 3u) | ((Y & 3u) << 2) | ((Z & 3u) << 4);
     return ((w.m1 >> cb) & 1ull) ? 0 : 1;
@@ -504,9 +526,165 @@ VPX_HD int skip_box_fast(Walk& w, const uint32_t lo[3], const uint32_t hi[3], fl
     return 1;
 }
 
+// ------------------------------------------------------- lean tier
+// skip_box in straight-line integer code for the common case: every axis sequence is in
+// closed form over the box with at most one binade change (no tie, not stuck).  Anything
+// else returns 2 and the lane takes skip_any later (the caller batches those lanes).
+// All products are < 2^24 x 2^6, so they use the full-rate 24-bit multiplier.
+
+VPX_HD uint32_t mul24(uint32_t a, uint32_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __umul24(a, b);
+#else
+    return a * b;
+#endif
+}
+
+VPX_HD float rcp_approx(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_rcpf(x);
+#else
+    return 1.0f / x;
+#endif
+}
+
+// Closed form of A -> fl(A + d) in A's binade, without branches, valid for i >= 1:
+// A(i) = (b + i c) u.  Without a tie, c = round(d / u) and b is A's significand.  With a
+// tie (d / u = c0 + 1/2 exactly) round-half-even makes every significand from A(1) on
+// even, so from there the increment is c0 rounded up to even; b is then the base that
+// reproduces A(1) = A + c0 + ((A + c0) & 1) (A(0) itself is read from the float).
+VPX_HD bool seg_params_nb(float a, float d, uint32_t& b, uint32_t& c, uint32_t& e) {
+    const uint32_t ab = fbits(a), db = fbits(d);
+    const uint32_t ea = ab >> 23, ed = db >> 23;
+    const uint32_t sh = ea - ed;  // meaningful when ok
+    const uint32_t shc = sh > 24u ? 24u : (sh < 1u ? 1u : sh);
+    const uint32_t md = (db & 0x7fffffu) | 0x800000u;
+    const uint32_t rem = md & ((1u << shc) - 1u), half = 1u << (shc - 1u);
+    const uint32_t c0 = md >> shc;
+    const uint32_t b0 = (ab & 0x7fffffu) | 0x800000u;
+    const bool tie = rem == half;
+    c = tie ? c0 + (c0 & 1u) : c0 + (rem > half ? 1u : 0u);
+    b = tie ? b0 + ((b0 + c0) & 1u) - (c0 & 1u) : b0;
+    e = ea;
+    return (ea - 1u < 254u) & (ed - 1u < 254u) & (ed < ea) & (sh <= 24u) & (c != 0u);
+}
+
+// ceil(p / c) clamped to 65 (p <= 2^24 + 1, c >= 1).
+VPX_HD uint32_t ceil_div_65(uint32_t p, uint32_t c) {
+    const float q = (float)p * rcp_approx((float)c);
+    uint32_t j = (uint32_t)(q < 64.5f ? q : 64.5f) + 1u;  // ceil(p/c) or one off, <= 65
+    j -= mul24(j - 1u, c) >= p ? 1u : 0u;
+    j += mul24(j, c) < p ? 1u : 0u;
+    return j < 65u ? j : 65u;
+}
+
+// floor(r / c) clamped to 64 (r < 2^24, c >= 1).
+VPX_HD uint32_t floor_div_64(uint32_t r, uint32_t c) {
+    const float q = (float)r * rcp_approx((float)c);
+    uint32_t m = (uint32_t)(q < 64.5f ? q : 64.5f);
+    m -= (m && mul24(m, c) > r) ? 1u : 0u;
+    m += mul24(m + 1u, c) <= r ? 1u : 0u;
+    return m < 64u ? m : 64u;
+}
+
+// First j >= 0 with (b + j c) u not below T (strict: >= T, else > T), clamped to 65.
+VPX_HD uint32_t seg_first65(uint32_t b, uint32_t c, uint32_t e, float T, bool strict) {
+    const uint32_t tb = fbits(T), te = tb >> 23;
+    const uint32_t need = ((tb & 0x7fffffu) | 0x800000u) + (strict ? 0u : 1u);
+    const uint32_t f = need <= b ? 0u : ceil_div_65(need - b, c);
+    return te == e ? f : (te < e ? 0u : 65u);
+}
+
+// One axis over the box: A(0..l) as one or two closed-form segments: A(i) = (b1 + i c1) u1
+// for i <= m1, then (b2 + (i - m1 - 1) c2) u2 after the plain IEEE step m1 -> m1 + 1.
+struct Axis {
+    uint32_t b1, c1, e1, m1, b2, c2, e2;
+};
+
+VPX_HD bool axis_init(float h, float d, uint32_t l, Axis& a) {
+    const bool ok1 = seg_params_nb(h, d, a.b1, a.c1, a.e1);
+    // A(i), 1 <= i <= m1, stay below 2^24 u (a tie base may be 2^24 itself: m1 = 0)
+    const uint32_t room = a.b1 <= 0xffffffu ? 0xffffffu - a.b1 : 0u;
+    const bool cross = mul24(l, a.c1) > room;  // l <= 63, c1 <= 2^23 when ok1
+    a.m1 = cross ? floor_div_64(room, a.c1 | 1u) : l;
+    const float Am = a.m1 ? bitsf((a.e1 << 23) | ((a.b1 + mul24(a.m1, a.c1)) & 0x7fffffu)) : h;
+    const float A = Am + d;  // the plain IEEE step into the next binade
+    uint32_t b2;
+    const bool ok2 = seg_params_nb(A, d, b2, a.c2, a.e2);
+    // the second segment starts at A itself: its closed form must hold from j = 0
+    const bool exact2 = b2 == ((fbits(A) & 0x7fffffu) | 0x800000u);
+    a.b2 = b2;
+    const bool fit2 = mul24(l - a.m1 - 1u, a.c2) <= 0xffffffu - a.b2;
+    // no event inside the box (l == 0): only A(0) = h is read
+    return (h > 0.0f) & (d > 0.0f) & (l == 0u || (ok1 & (!cross || (ok2 & exact2 & fit2))));
+}
+
+VPX_HD float axis_at(const Axis& a, float h, uint32_t i) {
+    const bool one = i <= a.m1;
+    const uint32_t b = one ? a.b1 + mul24(i, a.c1) : a.b2 + mul24(i - a.m1 - 1u, a.c2);
+    const float v = bitsf(((one ? a.e1 : a.e2) << 23) | (b & 0x7fffffu));
+    return i ? v : h;
+}
+
+// #{ i < cap : A(i) below T } (A increasing), cap <= 63.
+VPX_HD uint32_t axis_count(const Axis& a, float h, float T, bool strict, uint32_t cap) {
+    const bool h_below = strict ? h < T : h <= T;
+    uint32_t f1 = seg_first65(a.b1, a.c1, a.e1, T, strict);
+    f1 = h_below ? (f1 > 1u ? f1 : 1u) : 0u;  // index 0 is h itself
+    const uint32_t f2 = a.m1 + 1u + seg_first65(a.b2, a.c2, a.e2, T, strict);
+    const uint32_t f = f1 > a.m1 ? f2 : f1;
+    return f < cap ? f : cap;
+}
+
+VPX_HD int skip_box_fast1(Walk& w, const uint32_t lo[3], const uint32_t hi[3], float bound, uint32_t& cells) {
+    const uint32_t lx = (w.sx > 0 ? hi[0] - w.X : w.X - lo[0]);  // events inside the box, <= 63
+    const uint32_t ly = (w.sy > 0 ? hi[1] - w.Y : w.Y - lo[1]);
+    const uint32_t lz = (w.sz > 0 ? hi[2] - w.Z : w.Z - lo[2]);
+    Axis ax, ay, az;
+    const bool okx = axis_init(w.tx, w.dx, lx, ax);
+    const bool oky = axis_init(w.ty, w.dy, ly, ay);
+    const bool okz = axis_init(w.tz, w.dz, lz, az);
+    if (!(okx && oky && okz)) return 2;
+    const float Vx = axis_at(ax, w.tx, lx), Vy = axis_at(ay, w.ty, ly), Vz = axis_at(az, w.tz, lz);
+    const int a = (Vz <= Vx && Vz <= Vy) ? 2 : (Vy <= Vx ? 1 : 0);
+    const float vs = a == 2 ? Vz : (a == 1 ? Vy : Vx);
+    const bool inside = vs < bound;
+    const float T = inside ? vs : bound;
+    // events of the other axes before the leaving event (axis k precedes a on ties iff
+    // k > a), or, when the walk ends inside the box, before the bound (strict)
+    uint32_t nx = axis_count(ax, w.tx, T, true, lx);
+    uint32_t ny = axis_count(ay, w.ty, T, inside ? a == 2 : true, ly);
+    uint32_t nz = axis_count(az, w.tz, T, inside ? false : true, lz);
+    if (inside) {
+        nx = a == 0 ? lx : nx;
+        ny = a == 1 ? ly : ny;
+        nz = a == 2 ? lz : nz;
+        // t = the last event before the landing: the largest A_k(n_k - 1) over moved axes
+        const float px = axis_at(ax, w.tx, nx - 1u), py = axis_at(ay, w.ty, ny - 1u), pz = axis_at(az, w.tz, nz - 1u);
+        float tl = nx ? px : w.t;
+        tl = ny ? ((nx && !(tl < py)) ? tl : py) : tl;
+        tl = nz ? (((nx | ny) && !(tl < pz)) ? tl : pz) : tl;
+        w.t = tl;
+        w.tx = axis_at(ax, w.tx, nx), w.ty = axis_at(ay, w.ty, ny), w.tz = axis_at(az, w.tz, nz);
+        w.X += nx * (uint32_t)w.sx;
+        w.Y += ny * (uint32_t)w.sy;
+        w.Z += nz * (uint32_t)w.sz;
+        cells += nx + ny + nz;
+        return 0;
+    }
+    // case B: the counts relative to the leaving event bound the counts below `bound`
+    const uint32_t cx = a == 0 ? lx : axis_count(ax, w.tx, vs, true, lx);
+    const uint32_t cy = a == 1 ? ly : axis_count(ay, w.ty, vs, a == 2, ly);
+    const uint32_t cz = a == 2 ? lz : axis_count(az, w.tz, vs, false, lz);
+    cells += 1u + (nx < cx ? nx : cx) + (ny < cy ? ny : cy) + (nz < cz ? nz : cz);
+    return 1;
+}
+
 // skip_box_fast, else the general skip_box.
 VPX_HD int skip_any(Walk& w, const uint32_t lo[3], const uint32_t hi[3], float bound, uint32_t& cells) {
-    const int r = skip_box_fast(w, lo, hi, bound, cells);
+    int r = skip_box_fast1(w, lo, hi, bound, cells);
+    if (r != 2) return r;
+    r = skip_box_fast(w, lo, hi, bound, cells);
     return r != 2 ? r : skip_box(w, lo, hi, bound, cells);
 }
 
@@ -554,6 +732,33 @@ VPX_HD bool walk_skip(const GridView& g, Walk& w, float bound, uint32_t& cells) 
         if (!step1(w, g.n)) return false;
     }
 }
+
+#if !defined(__HIP_DEVICE_COMPILE__)
+// Host builder of the same hierarchy (tests and tools).  Sizes: l1 nb2^3*64, l2 nb3^3*64,
+// l3 nb3^3 words (nb1 = ceil(n/4), nb2 = ceil(nb1/4), nb3 = ceil(nb2/4)).
+inline void build_masks_host(const uint8_t* cells, uint32_t n, uint64_t* l1, uint64_t* l2, uint64_t* l3) {
+    const uint32_t nb1 = (n + 3) / 4, nb2 = (nb1 + 3) / 4, nb3 = (nb2 + 3) / 4;
+    std::memset(l1, 0, 8ull * nb2 * nb2 * nb2 * 64);
+    std::memset(l2, 0, 8ull * nb3 * nb3 * nb3 * 64);
+    std::memset(l3, 0, 8ull * nb3 * nb3 * nb3);
+    for (uint64_t z = 0; z < n; ++z)
+        for (uint64_t y = 0; y < n; ++y)
+            for (uint64_t x = 0; x < n; ++x)
+                if (cells[x + y * n + z * (uint64_t)n * n] != 255)
+                    l1[blk_index((uint32_t)x >> 2, (uint32_t)y >> 2, (uint32_t)z >> 2, nb2)] |=
+                        1ull << ((x & 3) + 4 * (y & 3) + 16 * (z & 3));
+    for (uint32_t z = 0; z < nb1; ++z)
+        for (uint32_t y = 0; y < nb1; ++y)
+            for (uint32_t x = 0; x < nb1; ++x)
+                if (l1[blk_index(x, y, z, nb2)])
+                    l2[blk_index(x >> 2, y >> 2, z >> 2, nb3)] |= 1ull << ((x & 3) + 4 * (y & 3) + 16 * (z & 3));
+    for (uint32_t z = 0; z < nb2; ++z)
+        for (uint32_t y = 0; y < nb2; ++y)
+            for (uint32_t x = 0; x < nb2; ++x)
+                if (l2[blk_index(x, y, z, nb3)])
+                    l3[lin_index(x >> 2, y >> 2, z >> 2, nb3)] |= 1ull << ((x & 3) + 4 * (y & 3) + 16 * (z & 3));
+}
+#endif
 
 }  // namespace skip
 }  // namespace vpx

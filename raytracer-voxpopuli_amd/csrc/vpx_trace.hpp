@@ -283,7 +283,10 @@ __device__ __forceinline__ skip::Walk to_walk(const Dda& s) {
 // classify / skip_box / step1 as skip::walk_skip (so results are identical), but the long
 // skip_box is executed in batches — only when few lanes of the wave still want to take
 // plain cell steps — instead of inside every step iteration of the wave.
-constexpr uint32_t kStepThreshold = 16;
+#ifndef VPX_STEP_THRESHOLD
+#define VPX_STEP_THRESHOLD 16
+#endif
+constexpr uint32_t kStepThreshold = VPX_STEP_THRESHOLD;
 
 #ifdef VPX_PHASE_PROF
 // Debug build only (-DVPX_PHASE_PROF): per-wave cycles / iterations / active lanes of the
@@ -294,6 +297,27 @@ __device__ unsigned long long g_phase[16];
 #define VPX_PH(...)
 #endif
 
+__device__ __forceinline__ void skip_box_of(const skip::Walk& w, int level, uint32_t n, uint32_t lo[3], uint32_t hi[3]) {
+    const uint32_t m = level == 3 ? 63u : 15u;
+    lo[0] = w.X & ~m, lo[1] = w.Y & ~m, lo[2] = w.Z & ~m;
+    hi[0] = (w.X | m) < n - 1u ? (w.X | m) : n - 1u;
+    hi[1] = (w.Y | m) < n - 1u ? (w.Y | m) : n - 1u;
+    hi[2] = (w.Z | m) < n - 1u ? (w.Z | m) : n - 1u;
+}
+
+// Lane modes: kStep wants a cell step, kSkip an empty-box skip, kMiss / kHit are done.
+// Phases are wave-uniform: cell steps while >= kStepThreshold lanes want one (or nobody
+// waits to skip), then the waiting lanes skip together.  Each lane runs exactly
+// skip::walk_skip's sequence (the reference's cells with the reference's floats).
+// Skip tiers: with LEAN the straight-line lean tier (skip_box_fast1) goes first, else
+// skip_box_fast (closed form, <= 1 binade change), then the general skip_box.
+#ifndef VPX_LEAN_NEAREST
+#define VPX_LEAN_NEAREST 1
+#endif
+#ifndef VPX_LEAN_SHADOW
+#define VPX_LEAN_SHADOW 1
+#endif
+template <bool LEAN>
 __device__ __forceinline__ bool walk_wave(const skip::GridView& g, skip::Walk& w, float bound, uint32_t& cells) {
     enum : int { kStep = 0, kSkip = 1, kMiss = 2, kHit = 3 };
     int mode = kStep, pending = 0;
@@ -331,14 +355,11 @@ __device__ __forceinline__ bool walk_wave(const skip::GridView& g, skip::Walk& w
         }
         VPX_PH(++nk; lk += __popcll(skipping);)
         if (mode == kSkip) {
-            const uint32_t m = pending == 3 ? 63u : 15u;
-            const uint32_t lo[3] = {w.X & ~m, w.Y & ~m, w.Z & ~m};
-            uint32_t hi[3] = {lo[0] + m, lo[1] + m, lo[2] + m};
-            for (int k = 0; k < 3; ++k) hi[k] = hi[k] < g.n - 1u ? hi[k] : g.n - 1u;
-            int sr = skip::skip_box_fast(w, lo, hi, bound, cells);
-            VPX_PH(uint64_t t2 = __builtin_amdgcn_s_memtime(); if (__ballot(sr == 2)) ++fb;)
+            uint32_t lo[3], hi[3];
+            skip_box_of(w, pending, g.n, lo, hi);
+            int sr = LEAN ? skip::skip_box_fast1(w, lo, hi, bound, cells) : 2;
+            if (sr == 2) sr = skip::skip_box_fast(w, lo, hi, bound, cells);
             if (sr == 2) sr = skip::skip_box(w, lo, hi, bound, cells);
-            VPX_PH(cf += __builtin_amdgcn_s_memtime() - t2;)
             if (sr == 1) {
                 mode = kMiss;
             } else {
@@ -527,7 +548,7 @@ __device__ __forceinline__ int32_t find_nearest(const SceneView& sv, Ray& r, Cou
         Dda s;
         if (!dda_setup(vol, g.n, o, s)) continue;
         skip::Walk w = to_walk(s);
-        if (walk_wave(grid_view(g), w, r.t, k.cells)) {
+        if (walk_wave<VPX_LEAN_NEAREST != 0>(grid_view(g), w, r.t, k.cells)) {
             r.t = w.t;
             r.N = normal_voxel(o, w.t, g.n, vol.matrix);
             r.mat = g.cells[(uint64_t)w.X + (uint64_t)w.Y * g.n + (uint64_t)w.Z * ((uint64_t)g.n * g.n)];
@@ -561,7 +582,7 @@ __device__ __forceinline__ bool is_occluded(const SceneView& sv, const Ray& r, C
         Dda s;
         if (!dda_setup(vol, g.n, o, s)) continue;
         skip::Walk w = to_walk(s);
-        if (walk_wave(grid_view(g), w, r.t, k.cells)) return true;  // first solid cell, t < bound
+        if (walk_wave<VPX_LEAN_SHADOW != 0>(grid_view(g), w, r.t, k.cells)) return true;  // first solid cell, t < bound
     }
     for (uint32_t i = 0; i < sv.num_spheres; ++i)
         if (sphere_is_hit(sv.spheres[i], r)) return true;

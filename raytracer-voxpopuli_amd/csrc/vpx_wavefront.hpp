@@ -112,16 +112,19 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
     return v;
 }
 
-// One 64-bit atomic per counter per wave: [0] shadow rays, [1] FindNearest calls,
-// [2] DDA cells, [3] primary rays.
+// Work counters: [0] shadow rays, [1] FindNearest calls, [2] DDA cells, [3] primary rays,
+// striped over kCtrStripes copies (one 64-bit atomic per counter per wave, spread over
+// addresses by workgroup so that waves do not serialise on one word); summed on readout.
+constexpr uint32_t kCtrStripes = 64;
 __device__ __forceinline__ void flush_counters(const Counters& k, uint32_t primary, unsigned long long* ctr) {
     const uint32_t sh = wave_sum(k.shadow), ne = wave_sum(k.nearest), ce = wave_sum(k.cells);
     const uint32_t pr = wave_sum(primary);
     if ((threadIdx.x & 63) == 0) {
-        if (sh) atomicAdd(&ctr[0], (unsigned long long)sh);
-        if (ne) atomicAdd(&ctr[1], (unsigned long long)ne);
-        if (ce) atomicAdd(&ctr[2], (unsigned long long)ce);
-        if (pr) atomicAdd(&ctr[3], (unsigned long long)pr);
+        unsigned long long* c = ctr + 4u * ((blockIdx.x * 4u + (threadIdx.x >> 6)) & (kCtrStripes - 1u));
+        if (sh) atomicAdd(&c[0], (unsigned long long)sh);
+        if (ne) atomicAdd(&c[1], (unsigned long long)ne);
+        if (ce) atomicAdd(&c[2], (unsigned long long)ce);
+        if (pr) atomicAdd(&c[3], (unsigned long long)pr);
     }
 }
 
@@ -231,16 +234,6 @@ __device__ __forceinline__ uint32_t wave_prefix(uint32_t v, uint32_t& total) {
     }
     total = __shfl(x, 63, 64);
     return x - v;
-}
-
-// Append `cnt` entries per lane to a device list with one atomic per wave.
-__device__ __forceinline__ uint32_t wave_append(uint32_t cnt, uint32_t* len) {
-    uint32_t total;
-    const uint32_t off = wave_prefix(cnt, total);
-    uint32_t base = 0;
-    if ((threadIdx.x & 63u) == 0 && total) base = atomicAdd(len, total);
-    base = __shfl(base, 0, 64);
-    return base + off;
 }
 
 __global__ __launch_bounds__(256) void k_shade(SceneView sv, FrameArgs f, WaveBufs w, int level,
@@ -436,6 +429,7 @@ __global__ __launch_bounds__(256) void k_resolve(SceneView sv, WaveBufs w) {
 #ifndef VPX_WPE_SHADOW
 #define VPX_WPE_SHADOW 5
 #endif
+
 #define VPX_WPE(n) __attribute__((amdgpu_waves_per_eu(n)))
 
 // One 256-thread workgroup per 16x16 tile.  Work is compacted inside the tile through LDS

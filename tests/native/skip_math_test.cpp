@@ -107,7 +107,7 @@ int fast_check() {
     using namespace vpx::skip;
     std::mt19937_64 r(99);
     std::uniform_real_distribution<double> U(0.0, 1.0);
-    long bad = 0, handled = 0, total = 0;
+    long bad = 0, handled = 0, handled1 = 0, total = 0;
     for (long i = 0; i < 4000000; ++i) {
         Walk w{};
         const uint32_t m = (i & 1) ? 63u : 15u;
@@ -138,10 +138,26 @@ int fast_check() {
         const float hmax = w.tx > w.ty ? (w.tx > w.tz ? w.tx : w.tz) : (w.ty > w.tz ? w.ty : w.tz);
         const int bk = (int)(r() % 4);
         const float bound = bk == 0 ? 1e34f : bk == 1 ? INFINITY : (float)(tmin + U(r) * (hmax * 4 - tmin));
-        Walk a = w, b = w;
-        uint32_t ca = 7, cb = 7;
+        Walk a = w, b = w, a1 = w;
+        uint32_t ca = 7, cb = 7, c1 = 7;
         const int ra = skip_box_fast(a, lo, hi, bound, ca);
+        const int r1 = skip_box_fast1(a1, lo, hi, bound, c1);
         ++total;
+        if (r1 != 2) {
+            ++handled1;
+            Walk b1 = w;
+            uint32_t cb1 = 7;
+            const int rb1 = skip_box(b1, lo, hi, bound, cb1);
+            if (!(r1 == rb1 && c1 == cb1 && (r1 == 1 || !memcmp(&a1, &b1, sizeof(Walk))))) {
+                if (bad < 10)
+                    printf("fast1 mismatch r %d/%d cells %u/%u t %a/%a\n  in: X %u %u %u s %d %d %d lo %u %u %u hi %u %u %u t %a h %a %a %a d %a %a %a bound %a\n"
+                           "  out fast1: h %a %a %a XYZ %u %u %u | ref: h %a %a %a XYZ %u %u %u\n",
+                           r1, rb1, c1, cb1, a1.t, b1.t, w.X, w.Y, w.Z, w.sx, w.sy, w.sz, lo[0], lo[1], lo[2], hi[0], hi[1], hi[2], w.t,
+                           w.tx, w.ty, w.tz, w.dx, w.dy, w.dz, bound, a1.tx, a1.ty, a1.tz, a1.X, a1.Y, a1.Z, b1.tx, b1.ty, b1.tz, b1.X,
+                           b1.Y, b1.Z);
+                ++bad;
+            }
+        }
         if (ra == 2) continue;
         ++handled;
         const int rb = skip_box(b, lo, hi, bound, cb);
@@ -153,7 +169,7 @@ int fast_check() {
             ++bad;
         }
     }
-    printf("skip_box_fast: %ld/%ld handled, bad=%ld\n", handled, total, bad);
+    printf("skip_box_fast: %ld/%ld handled (single-segment tier %ld), bad=%ld\n", handled, total, handled1, bad);
     return bad != 0;
 }
 static int _fast = (fast_check() ? (exit(1), 1) : 0);

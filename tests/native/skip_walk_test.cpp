@@ -34,24 +34,10 @@ static World make_world(uint32_t n, uint64_t seed, double density) {
                     if (r() % 5) w.cells[x + (size_t)y * n + (size_t)z * n * n] = (uint8_t)(r() % 200);
     }
     w.nb1 = (n + 3) / 4, w.nb2 = (w.nb1 + 3) / 4, w.nb3 = (w.nb2 + 3) / 4;
-    w.l1.assign((size_t)w.nb1 * w.nb1 * w.nb1, 0);
-    for (uint32_t z = 0; z < n; ++z)
-        for (uint32_t y = 0; y < n; ++y)
-            for (uint32_t x = 0; x < n; ++x)
-                if (w.cells[x + (size_t)y * n + (size_t)z * n * n] != 255)
-                    w.l1[(x >> 2) + (size_t)(y >> 2) * w.nb1 + (size_t)(z >> 2) * w.nb1 * w.nb1] |= 1ull << ((x & 3) + 4 * (y & 3) + 16 * (z & 3));
-    w.l2.assign((size_t)w.nb2 * w.nb2 * w.nb2, 0);
-    for (uint32_t z = 0; z < w.nb1; ++z)
-        for (uint32_t y = 0; y < w.nb1; ++y)
-            for (uint32_t x = 0; x < w.nb1; ++x)
-                if (w.l1[x + (size_t)y * w.nb1 + (size_t)z * w.nb1 * w.nb1])
-                    w.l2[(x >> 2) + (size_t)(y >> 2) * w.nb2 + (size_t)(z >> 2) * w.nb2 * w.nb2] |= 1ull << ((x & 3) + 4 * (y & 3) + 16 * (z & 3));
+    w.l1.assign((size_t)w.nb2 * w.nb2 * w.nb2 * 64, 0);
+    w.l2.assign((size_t)w.nb3 * w.nb3 * w.nb3 * 64, 0);
     w.l3.assign((size_t)w.nb3 * w.nb3 * w.nb3, 0);
-    for (uint32_t z = 0; z < w.nb2; ++z)
-        for (uint32_t y = 0; y < w.nb2; ++y)
-            for (uint32_t x = 0; x < w.nb2; ++x)
-                if (w.l2[x + (size_t)y * w.nb2 + (size_t)z * w.nb2 * w.nb2])
-                    w.l3[(x >> 2) + (size_t)(y >> 2) * w.nb3 + (size_t)(z >> 2) * w.nb3 * w.nb3] |= 1ull << ((x & 3) + 4 * (y & 3) + 16 * (z & 3));
+    build_masks_host(w.cells.data(), n, w.l1.data(), w.l2.data(), w.l3.data());
     return w;
 }
 
@@ -119,6 +105,34 @@ static bool walk_naive(const World& W, Walk s, float bound, uint32_t& cells, Wal
     return false;
 }
 
+// On a mismatch: replay the skipping walk and compare every skip tier against skip_box.
+static void debug_walk(const GridView& g, Walk w, float bound) {
+    for (int it = 0; it < 100000; ++it) {
+        if (!(w.t < bound)) return;
+        const int cls = classify(w, g);
+        if (cls == 0) return;
+        if (cls >= 2) {
+            const uint32_t m = cls == 3 ? 63u : 15u;
+            const uint32_t lo[3] = {w.X & ~m, w.Y & ~m, w.Z & ~m};
+            uint32_t hi[3] = {lo[0] + m, lo[1] + m, lo[2] + m};
+            for (int k = 0; k < 3; ++k) hi[k] = hi[k] < g.n - 1u ? hi[k] : g.n - 1u;
+            Walk a = w, b = w;
+            uint32_t ca = 0, cb = 0;
+            const int ra = skip_box_fast1(a, lo, hi, bound, ca), rb = skip_box(b, lo, hi, bound, cb);
+            if (ra != 2 && (ra != rb || ca != cb || (ra == 0 && memcmp(&a, &b, sizeof(Walk))))) {
+                printf("  first bad skip: r %d/%d cells %u/%u X %u %u %u s %d %d %d lo %u %u %u hi %u %u %u\n"
+                       "   t %a h %a %a %a d %a %a %a bound %a\n   fast1 t %a h %a %a %a XYZ %u %u %u\n   ref   t %a h %a %a %a XYZ %u %u %u\n",
+                       ra, rb, ca, cb, w.X, w.Y, w.Z, w.sx, w.sy, w.sz, lo[0], lo[1], lo[2], hi[0], hi[1], hi[2], w.t, w.tx, w.ty,
+                       w.tz, w.dx, w.dy, w.dz, bound, a.t, a.tx, a.ty, a.tz, a.X, a.Y, a.Z, b.t, b.tx, b.ty, b.tz, b.X, b.Y, b.Z);
+                return;
+            }
+            uint32_t c = 0;
+            if (skip_box(w, lo, hi, bound, c) == 1) return;
+        }
+        if (!step1(w, g.n)) return;
+    }
+}
+
 int main(int argc, char** argv) {
     _mm_setcsr(_mm_getcsr() | 0x8040u);
     const long rays = argc > 1 ? atol(argv[1]) : 20000;
@@ -161,6 +175,7 @@ int main(int argc, char** argv) {
                     if (bad < 10)
                         printf("n=%u dens=%.2f ray %ld: hit %d/%d cells %u/%u t %a/%a cell (%u,%u,%u)/(%u,%u,%u)\n", n, dens, i, r0, r1, c0, c1,
                                h0.t, h1.t, h0.X, h0.Y, h0.Z, h1.X, h1.Y, h1.Z);
+                    if (bad < 3) debug_walk(W.view(), s, bound);
                     ++bad;
                 }
             }

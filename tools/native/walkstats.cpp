@@ -8,14 +8,7 @@
 using namespace vpx::skip;
 
 extern "C" void build_masks(const uint8_t* cells, uint32_t n, uint64_t* l1, uint64_t* l2, uint64_t* l3) {
-    const uint32_t nb1 = (n + 3) / 4, nb2 = (nb1 + 3) / 4, nb3 = (nb2 + 3) / 4;
-    memset(l1, 0, 8ull * nb1 * nb1 * nb1); memset(l2, 0, 8ull * nb2 * nb2 * nb2); memset(l3, 0, 8ull * nb3 * nb3 * nb3);
-    for (uint64_t z = 0; z < n; ++z) for (uint64_t y = 0; y < n; ++y) for (uint64_t x = 0; x < n; ++x)
-        if (cells[x + y * n + z * n * n] != 255) l1[(x >> 2) + (y >> 2) * nb1 + (z >> 2) * nb1 * nb1] |= 1ull << ((x & 3) + 4 * (y & 3) + 16 * (z & 3));
-    for (uint64_t z = 0; z < nb1; ++z) for (uint64_t y = 0; y < nb1; ++y) for (uint64_t x = 0; x < nb1; ++x)
-        if (l1[x + y * nb1 + z * nb1 * nb1]) l2[(x >> 2) + (y >> 2) * nb2 + (z >> 2) * nb2 * nb2] |= 1ull << ((x & 3) + 4 * (y & 3) + 16 * (z & 3));
-    for (uint64_t z = 0; z < nb2; ++z) for (uint64_t y = 0; y < nb2; ++y) for (uint64_t x = 0; x < nb2; ++x)
-        if (l2[x + y * nb2 + z * nb2 * nb2]) l3[(x >> 2) + (y >> 2) * nb3 + (z >> 2) * nb3 * nb3] |= 1ull << ((x & 3) + 4 * (y & 3) + 16 * (z & 3));
+    build_masks_host(cells, n, l1, l2, l3);
 }
 
 static bool fast_ok(const Walk& w, const uint32_t lo[3], const uint32_t hi[3]) {
@@ -76,7 +69,7 @@ extern "C" void walk_stats(const uint8_t* cells, const uint64_t* l1, const uint6
                 uint32_t hi[3] = {lo[0] + m, lo[1] + m, lo[2] + m};
                 for (int k = 0; k < 3; ++k) hi[k] = hi[k] < n - 1u ? hi[k] : n - 1u;
                 const uint32_t before = c;
-                { Walk t = w; uint32_t cc = 0; const bool okf = skip_box_fast(t, lo, hi, bound, cc) != 2; out[7] += okf; if (!okf) why(w, lo, hi); }
+                { Walk t = w; uint32_t cc = 0; const bool okf = skip_box_fast1(t, lo, hi, bound, cc) != 2; out[7] += okf; if (!okf) why(w, lo, hi); }
                 const int rr = skip_box(w, lo, hi, bound, c);
                 if (rr == 1) break;
                 if (c == before) ++land0;
@@ -86,5 +79,80 @@ extern "C" void walk_stats(const uint8_t* cells, const uint64_t* l1, const uint6
         }
         out[0] += c; out[1] += iters; out[2] += steps; out[3] += sk16; out[4] += sk64; out[5] += land0;
         out[6] = out[6] > iters ? out[6] : iters;
+    }
+}
+
+// ---- box-choice simulation: how many steps / skips per ray for alternative empty boxes
+// opt bit 0: 32^3 groups of empty macros (from the l3 word); bit 1: 128^3 / 256^3 groups of
+// empty supers (l4 = bit per super); bit 2: 8^3 / 4^3 empty bricks inside non-empty macros.
+static uint64_t l3word(const GridView& g, uint32_t sx, uint32_t sy, uint32_t sz) {
+    if (sx >= g.nb3 || sy >= g.nb3 || sz >= g.nb3) return ~0ull;
+    return g.l3[lin_index(sx, sy, sz, g.nb3)];
+}
+extern "C" void walk_sim(const uint8_t* cells, const uint64_t* l1, const uint64_t* l2, const uint64_t* l3, uint32_t n,
+                         const float* st, const int32_t* si, const float* bounds, uint32_t nrays, int opt, uint64_t* out, float* tout) {
+    const uint32_t nb1 = (n + 3) / 4, nb2 = (nb1 + 3) / 4, nb3 = (nb2 + 3) / 4;
+    GridView g{cells, l1, l2, l3, n, nb1, nb2, nb3};
+    for (uint32_t r = 0; r < nrays; ++r) {
+        Walk w{};
+        w.X = si[6 * r], w.Y = si[6 * r + 1], w.Z = si[6 * r + 2];
+        w.sx = si[6 * r + 3], w.sy = si[6 * r + 4], w.sz = si[6 * r + 5];
+        w.t = st[7 * r], w.tx = st[7 * r + 1], w.ty = st[7 * r + 2], w.tz = st[7 * r + 3];
+        w.dx = st[7 * r + 4], w.dy = st[7 * r + 5], w.dz = st[7 * r + 6];
+        w.k1 = w.k2 = w.k3 = 0xffffffffu;
+        const float bound = bounds[r];
+        uint32_t c = 0;
+        uint64_t steps = 0, skips = 0;
+        bool hit = false;
+        for (;;) {
+            if (!(w.t < bound)) break;
+            const int cls = classify(w, g);
+            if (cls == 0) { ++c; hit = true; break; }
+            uint32_t m = 0, lo[3], hi[3];
+            bool box = false;
+            if (cls == 3) {
+                box = true, m = 63;
+                if (opt & 2) {  // 4x4x4 / 2x2x2 groups of empty supers
+                    const uint32_t sx = w.X >> 6, sy = w.Y >> 6, sz = w.Z >> 6;
+                    bool e4 = true, e2 = true;
+                    for (uint32_t z = 0; z < 4; ++z) for (uint32_t y = 0; y < 4; ++y) for (uint32_t x = 0; x < 4; ++x) {
+                        const uint64_t v = l3word(g, (sx & ~3u) + x, (sy & ~3u) + y, (sz & ~3u) + z);
+                        if (v) { e4 = false; if (((x >> 1) == ((sx >> 1) & 1)) && ((y >> 1) == ((sy >> 1) & 1)) && ((z >> 1) == ((sz >> 1) & 1))) e2 = false; }
+                    }
+                    m = e4 ? 255 : (e2 ? 127 : 63);
+                }
+            } else if (cls == 2) {
+                box = true, m = 15;
+                if (opt & 1) {
+                    const uint32_t gx = (w.X >> 5) & 1, gy = (w.Y >> 5) & 1, gz = (w.Z >> 5) & 1;
+                    if (!(w.m3 & (0x330033ull << (2 * gx + 8 * gy + 32 * gz)))) m = 31;
+                }
+            } else if (opt & 4) {  // empty cell: empty brick / 2x2x2 bricks?
+                const uint32_t bb = ((w.X >> 2) & 3u) | (((w.Y >> 2) & 3u) << 2) | (((w.Z >> 2) & 3u) << 4);
+                if (!((w.m2 >> bb) & 1ull)) {
+                    box = true, m = 3;
+                    const uint32_t gx = (w.X >> 3) & 1, gy = (w.Y >> 3) & 1, gz = (w.Z >> 3) & 1;
+                    if (!(w.m2 & (0x330033ull << (2 * gx + 8 * gy + 32 * gz)))) m = 7;
+                }
+            }
+            if (box) {
+                ++skips;
+                { Walk t = w; uint32_t cc = 0; uint32_t blo[3], bhi[3];
+                  for (int k = 0; k < 3; ++k) { const uint32_t q = k == 0 ? w.X : k == 1 ? w.Y : w.Z; blo[k] = q & ~m; bhi[k] = (q | m) < n - 1u ? (q | m) : n - 1u; }
+                  out[6] += skip_box_fast1(t, blo, bhi, bound, cc) == 2; }
+                for (int k = 0; k < 3; ++k) {
+                    const uint32_t cc = k == 0 ? w.X : k == 1 ? w.Y : w.Z;
+                    lo[k] = cc & ~m;
+                    hi[k] = (cc | m) < n - 1u ? (cc | m) : n - 1u;
+                }
+                if (skip_box(w, lo, hi, bound, c) == 1) break;
+            } else ++steps;
+            ++c;
+            if (!step1(w, n)) break;
+        }
+        out[0] += c; out[1] += steps; out[2] += skips; out[3] += hit;
+        out[4] += (uint64_t)w.X | ((uint64_t)w.Y << 20) | ((uint64_t)w.Z << 40);  // checksum of end state
+        out[5] += fbits(w.t);
+        if (tout) tout[r] = hit ? w.t : -1.0f;
     }
 }

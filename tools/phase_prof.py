@@ -27,4 +27,4 @@ cs, ck, ns, nk, ls, lk, walks, fb, cf = list(ph)[:9]
 print(f"walk calls(waves)={walks}  step: cycles={cs:.3e} iters={ns} lanes/iter={ls / max(ns, 1):.1f} "
       f"cyc/iter={cs / max(ns, 1):.0f} | skip: cycles={ck:.3e} iters={nk} lanes/iter={lk / max(nk, 1):.1f} "
       f"cyc/iter={ck / max(nk, 1):.0f} | per walk: step it={ns / walks:.1f} skip it={nk / walks:.1f}")
-print(f"fallback wave-iters {fb / max(nk, 1):.3f}; skip_box_fast+fallback cycles/iter {cf / max(nk, 1):.0f}")
+print(f"classify phases {fb} cycles {cf:.3e} ({cf / max(fb, 1):.0f}/iter)")

@@ -17,7 +17,7 @@ d = pkg.scene.CONFIGS[cfg]()
 o = orc.Oracle(pkg.abi, d)
 cells = o.cells[0]; n = d.grids[0].n
 nb = [(n + 3) // 4]; nb.append((nb[0] + 3) // 4); nb.append((nb[1] + 3) // 4)
-l1, l2, l3 = (np.zeros(b ** 3, np.uint64) for b in nb)
+l1, l2, l3 = np.zeros(nb[1] ** 3 * 64, np.uint64), np.zeros(nb[2] ** 3 * 64, np.uint64), np.zeros(nb[2] ** 3, np.uint64)
 lib.build_masks(cells.ctypes.data, n, l1.ctypes.data, l2.ctypes.data, l3.ctypes.data)
 # primary rays -> DDA setup (numpy float32, identity volume)
 rng = np.random.default_rng(0)
@@ -54,3 +54,52 @@ wy = np.zeros(8, np.uint64)
 lib.why_out.argtypes = [V]
 lib.why_out(wy.ctypes.data)
 print("fast-path failures by axis reason (nonnormal, d>=2^E, tie/stuck, 2nd crossing):", wy[:4])
+
+# ---- box-choice simulation on primary rays and shadow rays toward the lights
+lib.walk_sim.argtypes = [V, V, V, V, C.c_uint32, V, V, V, C.c_uint32, C.c_int, V, V]
+def sim(st_, si_, bnd, opt, tout=None):
+    o = np.zeros(8, np.uint64)
+    lib.walk_sim(cells.ctypes.data, l1.ctypes.data, l2.ctypes.data, l3.ctypes.data, n, np.ascontiguousarray(st_).ctypes.data,
+                 np.ascontiguousarray(si_).ctypes.data, np.ascontiguousarray(bnd, np.float32).ctypes.data, len(st_), opt,
+                 o.ctypes.data, None if tout is None else tout.ctypes.data)
+    return o
+def dda_state(org, dirs):
+    with np.errstate(divide="ignore", invalid="ignore"):
+        rD = (np.float32(1) / dirs).astype(np.float32)
+        inside = np.all((org >= 0) & (org <= 1), 1)
+        t0 = np.where(inside, 0, np.max(np.minimum((0 - org) * rD, (1 - org) * rD), 1)).astype(np.float32)
+        t1 = np.min(np.maximum((0 - org) * rD, (1 - org) * rD), 1)
+    ok = inside | ((t1 >= t0) & (t0 > 0))
+    ds = (dirs < 0).astype(np.float32)
+    pos = (org + dirs * (t0[:, None] + np.float32(5e-5))) * np.float32(n)
+    P0 = np.clip(pos.astype(np.int64), 0, n - 1)
+    stp = (1 - 2 * ds).astype(np.int32)
+    tdel = (cell * stp.astype(np.float32)) * rD
+    tmx = ((np.ceil(pos) - ds) * cell - org) * rD
+    s1 = np.concatenate([t0[:, None], tmx, tdel], 1).astype(np.float32)
+    s2 = np.concatenate([P0, stp], 1).astype(np.int32)
+    return s1[ok], s2[ok], ok
+th = np.zeros(len(st), np.float32)
+base = sim(st, si, np.full(len(st), 1e34, np.float32), 0, th)
+hitp = (cp + D * th[:, None])[th > 0].astype(np.float32)
+Dh = D[th > 0]
+org = (hitp - Dh * np.float32(2e-4)).astype(np.float32)
+L = np.float32([0.5, 1.5, 0.5])
+dl = L - org
+dist = np.sqrt((dl * dl).sum(1)).astype(np.float32)
+sets = {"primary": (st, si, np.full(len(st), 1e34, np.float32))}
+s1, s2, ok = dda_state(org, (dl / dist[:, None]).astype(np.float32))
+sets["shadow-point"] = (s1, s2, dist[ok])
+dd = np.float32([0.3, 1.0, 0.2]); dd = dd / np.sqrt((dd * dd).sum())
+s1, s2, ok = dda_state(org, np.broadcast_to(dd, org.shape).astype(np.float32).copy())
+sets["shadow-dir"] = (s1, s2, np.full(ok.sum(), 1e34, np.float32))
+for name, (a, b, bnd) in sets.items():
+    R = len(a)
+    line = []
+    ref = None
+    for opt in (0, 1, 2, 3, 4, 7):
+        o = sim(a, b, bnd, opt)
+        if ref is None: ref = o
+        assert o[0] == ref[0] and o[3] == ref[3] and o[4] == ref[4] and o[5] == ref[5], (name, opt)  # same cells / hits / end state
+        line.append(f"opt{opt}: steps {o[1]/R:.1f} skips {o[2]/R:.1f} lean-miss {o[6]/max(o[2],1):.4f} cost {(o[1] + 5.8 * o[2]) / R:.0f}")
+    print(f"{name} ({R} rays, cells {ref[0]/R:.0f}): " + " | ".join(line))
