@@ -81,6 +81,26 @@ def cpu_baseline(pkg, desc, budget_s=12.0):
                       f"rays, {dt:.1f} s); world generated on host in {gen_s:.1f} s"}
 
 
+STAGE_KERNELS = {"primary": "k_primary", "shade": "k_shade", "shadow": "k_shadow_tile", "resolve": "k_resolve",
+                 "bounce": "k_nearest_tile", "finish": "k_finish"}
+
+
+def pmc_traffic(kernel, config, W, H):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of this
+    workload (profiles/*_pmc_traffic.json, FETCH_SIZE x2 + WRITE_SIZE per the gfx950
+    correction); None when no summary for this exact workload exists."""
+    import glob
+    best = None
+    for f in sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "*_pmc_traffic.json"))):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if d.get("config") == config and d.get("width") == W and d.get("height") == H and kernel in d.get("kernels", {}):
+            best = d["kernels"][kernel]["hbm_bytes_per_launch"]
+    return best
+
+
 def run(args):
     pkg = entry.load_package()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -141,6 +161,9 @@ def run(args):
         step()
     torch.cuda.synchronize()
     ctx.counters(reset=True)
+    # per-stage HIP events on the library's stream (the same stream the kernels run on)
+    ctx.profile_enable(args.steps * (4 * (desc.max_bounces + 1) + 4))
+    ctx.profile_read(reset=True)
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -171,11 +194,20 @@ def run(args):
         K = args.steps
         ms_step = elapsed * 1000.0 / K
         value = rays / elapsed / 1e6
-        # roofline of the dominant kernel (render), per launch on one GPU
-        cells_per_launch = float(st.dda_cells) / K
-        pix_per_launch = float(st.primary_rays) / K
-        alg_bytes = cells_per_launch * 1.0 + pix_per_launch * 36.0
+        # roofline of the dominant kernel: the stage with the largest device time in the
+        # timed region, its algorithmic bytes per launch (1 B per DDA cell
+        # read; 36 B per pixel for the accumulate/tonemap stage) over its average launch time
+        prof = ctx.profile_read()
+        dom = max(prof, key=lambda k: prof[k][0])
+        dom_ms, dom_launches, dom_cells = prof[dom]
+        kernel_ms = dom_ms / max(dom_launches, 1)
+        if dom == "finish":
+            alg_bytes = float(st.primary_rays) / K * 36.0
+        else:
+            alg_bytes = float(dom_cells) / max(dom_launches, 1)
         achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
+        frame_bytes = float(st.dda_cells) / K + float(st.primary_rays) / K * 36.0
+        traffic = pmc_traffic(STAGE_KERNELS[dom], args.config, W, H)
         out = {
             "metric": METRIC, "value": round(value, 3), "unit": "Mray/s", "n_gpus": n, "steps": K,
             "warmup": args.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True,
@@ -189,9 +221,12 @@ def run(args):
             "rays_per_step": {"primary": prim / K, "shadow": shad / K, "dda_cells": cells / K},
             "mpix_per_s": round(prim / elapsed / 1e6, 3),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
-                         "kernel": "render_tiles", "kernel_ms": round(kernel_ms, 4),
-                         "alg_bytes_per_launch": round(alg_bytes)},
+                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                         "kernel": STAGE_KERNELS[dom], "kernel_ms": round(kernel_ms, 4),
+                         "alg_bytes_per_launch": round(alg_bytes),
+                         "stages_ms": {k: round(v[0] / max(v[1], 1), 4) for k, v in prof.items() if v[1]},
+                         "frame_alg_bytes": round(frame_bytes),
+                         "frame_achieved": round(frame_bytes / (ms_step * 1e-3) / 1e9, 2)},
             "cpu_baseline": None,
         }
         if n == 1 and not args.no_cpu:

@@ -241,6 +241,27 @@ int vpx_composite_tiles(vpx_ctx* ctx, const vpx_frame_params* params, uint32_t t
    (no per-frame synchronisation); kernel_ms/total_ms are not filled here.            */
 int vpx_get_counters(vpx_ctx* ctx, vpx_stats* out, int reset);
 
+/* ---- per-stage profile (measurement; off by default) ------------------------------ */
+/* Stages of one vpx_render / vpx_render_tiles call. */
+#define VPX_STAGE_PRIMARY 0  /* primary rays + Renderer::FindNearest                   */
+#define VPX_STAGE_SHADE 1    /* Trace material switch (+ glass/smoke exit marches)      */
+#define VPX_STAGE_SHADOW 2   /* Renderer::IsOccluded of the emitted shadow rays         */
+#define VPX_STAGE_RESOLVE 3  /* light sums                                              */
+#define VPX_STAGE_BOUNCE 4   /* Renderer::FindNearest of bounce rays                    */
+#define VPX_STAGE_FINISH 5   /* fold + accumulate + tonemap (or tile pack)              */
+#define VPX_NUM_STAGES 6
+typedef struct vpx_profile {
+    float stage_ms[8];            /* summed device time per stage (HIP events on the stream) */
+    uint32_t stage_launches[8];   /* kernel launches timed per stage                         */
+    uint64_t stage_cells[8];      /* DDA cells read per stage (all launches, incl. untimed)  */
+} vpx_profile;
+/* Time every stage launch of the next renders with HIP events on the library's stream
+   (up to `max_launches` launches; 0 turns profiling off).  Adds no synchronisation. */
+int vpx_profile_enable(vpx_ctx* ctx, uint32_t max_launches);
+/* Synchronise, sum the recorded stage times and return them (reset: clear events and
+   the per-stage cell counters). */
+int vpx_profile_read(vpx_ctx* ctx, vpx_profile* out, int reset);
+
 /* ---- unit entries (host pointers; mirror the reference per-ray functions) ---------- */
 int vpx_find_nearest(vpx_ctx* ctx, const vpx_ray* rays, uint32_t n, vpx_hit* hits);
 int vpx_is_occluded(vpx_ctx* ctx, const vpx_ray* rays, uint32_t n, uint8_t* occluded);

@@ -85,7 +85,13 @@ class Stats(C.Structure):
         return {k: getattr(self, k) for k, _ in self._fields_}
 
 
-STRUCT_SIZES = {Volume: 160, Material: 32, PointLight: 24, SpotLight: 40, AreaLight: 32, DirLight: 24,
+class Profile(C.Structure):
+    _fields_ = [("stage_ms", C.c_float * 8), ("stage_launches", C.c_uint32 * 8), ("stage_cells", C.c_uint64 * 8)]
+
+
+STAGES = ("primary", "shade", "shadow", "resolve", "bounce", "finish")
+
+STRUCT_SIZES = {Profile: 128, Volume: 160, Material: 32, PointLight: 24, SpotLight: 40, AreaLight: 32, DirLight: 24,
                 Sphere: 32, Triangle: 64, Camera: 80, FrameParams: 48, Ray: 32, Hit: 32, Stats: 40}
 
 
@@ -126,6 +132,8 @@ SIGNATURES = {
     "vpx_composite_tiles": (C.c_int, [C.c_void_p, C.POINTER(FrameParams), C.c_uint32, C.c_uint32, C.c_uint32,
                                       C.c_void_p, C.c_void_p, C.c_void_p]),
     "vpx_get_counters": (C.c_int, [C.c_void_p, C.POINTER(Stats), C.c_int]),
+    "vpx_profile_enable": (C.c_int, [C.c_void_p, C.c_uint32]),
+    "vpx_profile_read": (C.c_int, [C.c_void_p, C.POINTER(Profile), C.c_int]),
     "vpx_find_nearest": (C.c_int, [C.c_void_p, C.POINTER(Ray), C.c_uint32, C.POINTER(Hit)]),
     "vpx_is_occluded": (C.c_int, [C.c_void_p, C.POINTER(Ray), C.c_uint32, C.c_void_p]),
     "vpx_trace": (C.c_int, [C.c_void_p, C.POINTER(Ray), C.c_void_p, C.c_uint32, C.c_int32, C.POINTER(C.c_float),

@@ -93,6 +93,15 @@ class Context:
                                                C.c_void_p(accum_ptr), C.c_void_p(rgb_ptr or 0)),
                   "vpx_composite_tiles")
 
+    def profile_enable(self, max_launches):
+        self._chk(self.lib.vpx_profile_enable(self.h, int(max_launches)), "vpx_profile_enable")
+
+    def profile_read(self, reset=True):
+        """Per-stage device times / launches / DDA cells: {stage: (ms_total, launches, cells)}."""
+        pr = abi.Profile()
+        self._chk(self.lib.vpx_profile_read(self.h, C.byref(pr), 1 if reset else 0), "vpx_profile_read")
+        return {name: (pr.stage_ms[i], pr.stage_launches[i], pr.stage_cells[i]) for i, name in enumerate(abi.STAGES)}
+
     def counters(self, reset=False):
         st = abi.Stats()
         self._chk(self.lib.vpx_get_counters(self.h, C.byref(st), 1 if reset else 0), "vpx_get_counters")

@@ -244,7 +244,11 @@ struct vpx_ctx {
     vpx_dir_light dir{{1, 0, 0}, {0, 0, 0}};  // DirectionalLight default (DirectionalLight.h:12)
     vpx_camera cam{};
     bool have_materials = false, have_camera = false;
-    unsigned long long* d_ctr = nullptr;  // [0] shadow, [1] nearest calls, [2] cells, [3] primary
+    unsigned long long* d_ctr = nullptr;  // striped work counters (vpx_wavefront.hpp flush_counters)
+    // per-stage profile: event pairs around stage launches while enabled
+    std::vector<hipEvent_t> prof_ev;
+    std::vector<int> prof_stage;
+    uint32_t prof_cap = 0, prof_used = 0;
     unsigned long long* d_sum = nullptr;
     void* d_scratch = nullptr;
     size_t scratch_bytes = 0;
@@ -416,6 +420,17 @@ int ensure_wave(vpx_ctx* c, uint32_t P, uint32_t L, uint32_t S) {
     return VPX_OK;
 }
 
+// Profile marks: a stage's start (stage >= 0) or end (-1) event on the stream, while the
+// event pool lasts; a start without room for its end is not recorded.
+static void prof_mark(vpx_ctx* c, int stage) {
+    if (!c->prof_cap) return;
+    if (stage >= 0 && c->prof_used + 2 > c->prof_cap) return;
+    if (stage < 0 && (c->prof_used & 1u) == 0) return;  // its start was dropped
+    if (hipEventRecord(c->prof_ev[c->prof_used], c->stream) != hipSuccess) return;
+    c->prof_stage[c->prof_used] = stage;
+    ++c->prof_used;
+}
+
 // The frame: primary -> [shade -> shadow -> resolve -> nearest]* -> finish, all on
 // c->stream, one 256-thread workgroup per 16x16 tile in every kernel.
 template <bool PACKED>
@@ -428,31 +443,46 @@ int launch_render(vpx_ctx* c, const SceneView& sv, const FrameArgs& f, uint32_t 
     if (rc) return rc;
     const WaveBufs w = c->wave;
     const dim3 grid(tiles), block(kThreads);
-    const size_t slds = sizeof(uint32_t) * S * kThreads;
+    const size_t slds = sizeof(uint32_t) * S * kThreads * kGroupTiles;
+    const dim3 ggrid((tiles + kGroupTiles - 1) / kGroupTiles);
+    prof_mark(c, VPX_STAGE_PRIMARY);
     hipLaunchKernelGGL(k_primary, grid, block, 0, c->stream, sv, f, w, c->d_ctr);
+    prof_mark(c, -1);
     for (int level = 0; level <= f.max_bounces; ++level) {
+        prof_mark(c, VPX_STAGE_SHADE);
         hipLaunchKernelGGL(k_shade, grid, block, 0, c->stream, sv, f, w, level, c->d_ctr);
-        hipLaunchKernelGGL(k_shadow_tile, grid, block, slds, c->stream, sv, w, c->d_ctr);
+        prof_mark(c, -1);
+        prof_mark(c, VPX_STAGE_SHADOW);
+        hipLaunchKernelGGL(k_shadow_tile, ggrid, block, slds, c->stream, sv, w, c->d_ctr);
+        prof_mark(c, -1);
+        prof_mark(c, VPX_STAGE_RESOLVE);
         hipLaunchKernelGGL(k_resolve, grid, block, 0, c->stream, sv, w);
-        if (level < f.max_bounces) hipLaunchKernelGGL(k_nearest_tile, grid, block, 0, c->stream, sv, w, c->d_ctr);
+        prof_mark(c, -1);
+        if (level < f.max_bounces) {
+            prof_mark(c, VPX_STAGE_BOUNCE);
+            hipLaunchKernelGGL(k_nearest_tile, ggrid, block, 0, c->stream, sv, w, c->d_ctr);
+            prof_mark(c, -1);
+        }
     }
+    prof_mark(c, VPX_STAGE_FINISH);
     hipLaunchKernelGGL((k_finish<PACKED>), grid, block, 0, c->stream, f, w, accum, rgb8, packed);
+    prof_mark(c, -1);
     VPX_HIP(c, hipGetLastError());
     return VPX_OK;
 }
 
-int snapshot_counters(vpx_ctx* c, unsigned long long out[4]) {
-    unsigned long long all[4 * kCtrStripes];
+int snapshot_counters(vpx_ctx* c, unsigned long long out[kCtrWords]) {
+    unsigned long long all[kCtrWords * kCtrStripes];
     VPX_HIP(c, hipMemcpyAsync(all, c->d_ctr, sizeof(all), hipMemcpyDeviceToHost, c->stream));
     VPX_HIP(c, hipStreamSynchronize(c->stream));
-    for (int i = 0; i < 4; ++i) {
+    for (uint32_t i = 0; i < kCtrWords; ++i) {
         out[i] = 0;
-        for (uint32_t s = 0; s < kCtrStripes; ++s) out[i] += all[4 * s + i];
+        for (uint32_t s = 0; s < kCtrStripes; ++s) out[i] += all[kCtrWords * s + i];
     }
     return VPX_OK;
 }
 
-void fill_stats(vpx_stats* s, const unsigned long long a[4], const unsigned long long b[4]) {
+void fill_stats(vpx_stats* s, const unsigned long long a[kCtrWords], const unsigned long long b[kCtrWords]) {
     s->shadow_rays = b[0] - a[0];
     s->primary_rays = b[3] - a[3];
     s->bounce_rays = (b[1] - a[1]) - s->primary_rays;
@@ -477,7 +507,7 @@ int vpx_create(int device, vpx_ctx** out) {
     if (!c) return VPX_E_NOMEM;
     c->device = device;
     if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess ||
-        hipMalloc(&c->d_ctr, 4 * kCtrStripes * sizeof(unsigned long long)) != hipSuccess ||
+        hipMalloc(&c->d_ctr, kCtrWords * kCtrStripes * sizeof(unsigned long long)) != hipSuccess ||
         hipMalloc(&c->d_sum, sizeof(unsigned long long)) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
         hipEventCreate(&c->ev2) != hipSuccess) {
@@ -485,7 +515,7 @@ int vpx_create(int device, vpx_ctx** out) {
         return VPX_E_DEVICE;
     }
     c->stream = c->own_stream;
-    (void)hipMemset(c->d_ctr, 0, 4 * kCtrStripes * sizeof(unsigned long long));
+    (void)hipMemset(c->d_ctr, 0, kCtrWords * kCtrStripes * sizeof(unsigned long long));
     *out = c;
     return VPX_OK;
 }
@@ -504,6 +534,7 @@ int vpx_destroy(vpx_ctx* c) {
                     c->d_spheres, c->d_triangles, c->d_ctr, c->d_sum, c->d_scratch, c->d_wave};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
+    for (hipEvent_t e : c->prof_ev) (void)hipEventDestroy(e);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->ev2) (void)hipEventDestroy(c->ev2);
@@ -675,7 +706,7 @@ int vpx_render(vpx_ctx* c, const vpx_frame_params* p, float* accum, uint32_t* rg
     if (rc) return rc;
     if (!accum) return fail(c, VPX_E_INVALID, "accum (device float4[W*H]) is required");
     VPX_HIP(c, hipSetDevice(c->device));
-    unsigned long long before[4] = {0, 0, 0, 0};
+    unsigned long long before[kCtrWords] = {};
     if (stats && (rc = snapshot_counters(c, before))) return rc;
     const SceneView sv = view_of(c, p->sky, p->area_samples);
     const FrameArgs f = frame_of(c, p, 0, 1);
@@ -683,7 +714,7 @@ int vpx_render(vpx_ctx* c, const vpx_frame_params* p, float* accum, uint32_t* rg
     if ((rc = launch_render<false>(c, sv, f, f.num_tiles, reinterpret_cast<float4*>(accum), rgb8, nullptr))) return rc;
     if (stats) {
         VPX_HIP(c, hipEventRecord(c->ev1, c->stream));
-        unsigned long long after[4];
+        unsigned long long after[kCtrWords];
         if ((rc = snapshot_counters(c, after))) return rc;
         std::memset(stats, 0, sizeof(*stats));
         fill_stats(stats, before, after);
@@ -709,7 +740,7 @@ int vpx_render_tiles(vpx_ctx* c, const vpx_frame_params* p, uint32_t tile_w, uin
     if (tile_w != kTile || tile_h != kTile) return fail(c, VPX_E_INVALID, "tiles must be 16x16");
     if (n_ranks == 0 || rank >= n_ranks || !packed) return fail(c, VPX_E_INVALID, "bad rank / packed buffer");
     VPX_HIP(c, hipSetDevice(c->device));
-    unsigned long long before[4] = {0, 0, 0, 0};
+    unsigned long long before[kCtrWords] = {};
     if (stats && (rc = snapshot_counters(c, before))) return rc;
     const SceneView sv = view_of(c, p->sky, p->area_samples);
     const FrameArgs f = frame_of(c, p, rank, n_ranks);
@@ -718,7 +749,7 @@ int vpx_render_tiles(vpx_ctx* c, const vpx_frame_params* p, uint32_t tile_w, uin
         return rc;
     if (stats) {
         VPX_HIP(c, hipEventRecord(c->ev1, c->stream));
-        unsigned long long after[4];
+        unsigned long long after[kCtrWords];
         if ((rc = snapshot_counters(c, after))) return rc;
         std::memset(stats, 0, sizeof(*stats));
         fill_stats(stats, before, after);
@@ -745,14 +776,14 @@ int vpx_composite_tiles(vpx_ctx* c, const vpx_frame_params* p, uint32_t tile_w, 
 
 int vpx_get_counters(vpx_ctx* c, vpx_stats* out, int reset) {
     if (!c || !out) return fail(c, VPX_E_INVALID, "null argument");
-    unsigned long long now[4];
+    unsigned long long now[kCtrWords];
     int rc = snapshot_counters(c, now);
     if (rc) return rc;
-    const unsigned long long zero[4] = {0, 0, 0, 0};
+    const unsigned long long zero[kCtrWords] = {};
     std::memset(out, 0, sizeof(*out));
     fill_stats(out, zero, now);
     if (reset) {
-        VPX_HIP(c, hipMemsetAsync(c->d_ctr, 0, 4 * kCtrStripes * sizeof(unsigned long long), c->stream));
+        VPX_HIP(c, hipMemsetAsync(c->d_ctr, 0, kCtrWords * kCtrStripes * sizeof(unsigned long long), c->stream));
         VPX_HIP(c, hipStreamSynchronize(c->stream));
     }
     return VPX_OK;
@@ -845,6 +876,50 @@ uint32_t vpx_pixel_seed(uint32_t base, uint32_t frame, uint32_t w, uint32_t h, u
 
 }  // extern "C"
 
+extern "C" int vpx_profile_enable(vpx_ctx* c, uint32_t max_launches) {
+    if (!c) return VPX_E_INVALID;
+    VPX_HIP(c, hipStreamSynchronize(c->stream));
+    for (hipEvent_t e : c->prof_ev) (void)hipEventDestroy(e);
+    c->prof_ev.clear();
+    c->prof_stage.clear();
+    c->prof_cap = c->prof_used = 0;
+    if (!max_launches) return VPX_OK;
+    if (max_launches > 1u << 16) return fail(c, VPX_E_INVALID, "max_launches too large");
+    c->prof_ev.resize(2 * (size_t)max_launches, nullptr);
+    c->prof_stage.resize(2 * (size_t)max_launches, -1);
+    for (auto& e : c->prof_ev) VPX_HIP(c, hipEventCreate(&e));
+    c->prof_cap = 2 * max_launches;
+    return VPX_OK;
+}
+
+extern "C" int vpx_profile_read(vpx_ctx* c, vpx_profile* out, int reset) {
+    if (!c || !out) return fail(c, VPX_E_INVALID, "null argument");
+    std::memset(out, 0, sizeof(*out));
+    unsigned long long now[kCtrWords];
+    int rc = snapshot_counters(c, now);  // synchronises the stream
+    if (rc) return rc;
+    for (uint32_t st = 0; st < 8; ++st) out->stage_cells[st] = now[8 + st];
+    for (uint32_t i = 0; i + 1 < c->prof_used; i += 2) {
+        float ms = 0.f;
+        VPX_HIP(c, hipEventElapsedTime(&ms, c->prof_ev[i], c->prof_ev[i + 1]));
+        const int st = c->prof_stage[i];
+        if (st >= 0 && st < 8) {
+            out->stage_ms[st] += ms;
+            ++out->stage_launches[st];
+        }
+    }
+    if (reset) {
+        c->prof_used = 0;
+        unsigned long long* d = c->d_ctr;
+        std::vector<unsigned long long> h(kCtrWords * kCtrStripes);
+        VPX_HIP(c, hipMemcpy(h.data(), d, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost));
+        for (uint32_t s = 0; s < kCtrStripes; ++s)
+            for (uint32_t st = 8; st < 16; ++st) h[kCtrWords * s + st] = 0;
+        VPX_HIP(c, hipMemcpy(d, h.data(), sizeof(unsigned long long) * h.size(), hipMemcpyHostToDevice));
+    }
+    return VPX_OK;
+}
+
 #ifdef VPX_PHASE_PROF
 extern "C" int vpx_debug_phase(unsigned long long* out, int reset) {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(vpx::g_phase), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
@@ -855,4 +930,3 @@ extern "C" int vpx_debug_phase(unsigned long long* out, int reset) {
     return 0;
 }
 #endif
-

@@ -113,17 +113,23 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
 }
 
 // Work counters: [0] shadow rays, [1] FindNearest calls, [2] DDA cells, [3] primary rays,
-// striped over kCtrStripes copies (one 64-bit atomic per counter per wave, spread over
-// addresses by workgroup so that waves do not serialise on one word); summed on readout.
+// [8 + s] DDA cells of stage s (VPX_STAGE_*), striped over kCtrStripes copies of
+// kCtrWords words (one 64-bit atomic per counter per wave, spread over addresses by
+// workgroup so that waves do not serialise on one word); summed on readout.
 constexpr uint32_t kCtrStripes = 64;
-__device__ __forceinline__ void flush_counters(const Counters& k, uint32_t primary, unsigned long long* ctr) {
+constexpr uint32_t kCtrWords = 16;
+__device__ __forceinline__ void flush_counters(const Counters& k, uint32_t primary, unsigned long long* ctr,
+                                               uint32_t stage = 7u) {
     const uint32_t sh = wave_sum(k.shadow), ne = wave_sum(k.nearest), ce = wave_sum(k.cells);
     const uint32_t pr = wave_sum(primary);
     if ((threadIdx.x & 63) == 0) {
-        unsigned long long* c = ctr + 4u * ((blockIdx.x * 4u + (threadIdx.x >> 6)) & (kCtrStripes - 1u));
+        unsigned long long* c = ctr + kCtrWords * ((blockIdx.x * 4u + (threadIdx.x >> 6)) & (kCtrStripes - 1u));
         if (sh) atomicAdd(&c[0], (unsigned long long)sh);
         if (ne) atomicAdd(&c[1], (unsigned long long)ne);
-        if (ce) atomicAdd(&c[2], (unsigned long long)ce);
+        if (ce) {
+            atomicAdd(&c[2], (unsigned long long)ce);
+            atomicAdd(&c[8 + stage], (unsigned long long)ce);
+        }
         if (pr) atomicAdd(&c[3], (unsigned long long)pr);
     }
 }
@@ -389,7 +395,7 @@ __global__ __launch_bounds__(256) void k_shade(SceneView sv, FrameArgs f, WaveBu
         if (!pending) w.SM[p] = make_float4(0.f, 0.f, 0.f, __uint_as_float(0u));
     }
     if (p < w.P) w.smask[p] = slots;
-    flush_counters(k, 0u, ctr);
+    flush_counters(k, 0u, ctr, VPX_STAGE_SHADE);
 }
 
 // Light sum of a level once its shadow rays are resolved (kSlotOcc set by k_shadow1):
@@ -528,22 +534,48 @@ __global__ __launch_bounds__(256) VPX_WPE(VPX_WPE_NEAREST) void k_primary(SceneV
         r.inside = false;
         nearest_record(sv, w, q, r, k);
     }
-    flush_counters(k, prim, ctr);
+    flush_counters(k, prim, ctr, VPX_STAGE_PRIMARY);
 }
 
-// Renderer::FindNearest for the tile's active paths (bounce levels).
+// Sparse stages (bounce FindNearest, IsOccluded) can gather the work of G tiles per
+// workgroup (entries stay in tile order).  Measured on C1: G = 1, 2, 4, 8 -> 2.70, 2.87,
+// 3.22, 4.36 ms/frame.  Walk lengths are heavy-tailed (mean ~60 iterations, max ~400),
+// so a wave costs about its longest ray: packing more rays per wave raises every wave's
+// maximum more than it saves in partially filled waves.  G = 1.
+#ifndef VPX_GROUP_TILES
+#define VPX_GROUP_TILES 1
+#endif
+constexpr uint32_t kGroupTiles = VPX_GROUP_TILES;
+
+// Prefix scan over the G*256 paths of a workgroup (each thread scans G paths).
+template <uint32_t G>
+__device__ __forceinline__ uint32_t group_scan(const uint32_t (&cnt)[G], uint32_t& total, uint32_t* sh) {
+    uint32_t mine = 0;
+#pragma unroll
+    for (uint32_t g = 0; g < G; ++g) mine += cnt[g];
+    return block_scan(mine, total, sh);
+}
+
+// Renderer::FindNearest for the active paths of G tiles (bounce levels).
 __global__ __launch_bounds__(256) VPX_WPE(VPX_WPE_NEAREST) void k_nearest_tile(SceneView sv, WaveBufs w, unsigned long long* __restrict__ ctr) {
     __shared__ uint32_t sh[4];
-    __shared__ uint32_t lst[256];
-    const uint32_t p = blockIdx.x * 256u + threadIdx.x;
+    __shared__ uint32_t lst[256 * kGroupTiles];
+    const uint32_t base = blockIdx.x * 256u * kGroupTiles;
     Counters k{0u, 0u, 0u};
-    const bool act = p < w.P && (__float_as_uint(w.D[p].w) & kActive);
+    uint32_t cnt[kGroupTiles];
+#pragma unroll
+    for (uint32_t g = 0; g < kGroupTiles; ++g) {  // thread t scans paths base + t*G + g
+        const uint32_t p = base + threadIdx.x * kGroupTiles + g;
+        cnt[g] = (p < w.P && (__float_as_uint(w.D[p].w) & kActive)) ? 1u : 0u;
+    }
     uint32_t total;
-    const uint32_t at = block_scan(act ? 1u : 0u, total, sh);
-    if (act) lst[at] = p;
+    uint32_t at = group_scan<kGroupTiles>(cnt, total, sh);
+#pragma unroll
+    for (uint32_t g = 0; g < kGroupTiles; ++g)
+        if (cnt[g]) lst[at++] = base + threadIdx.x * kGroupTiles + g;
     __syncthreads();
-    if (threadIdx.x < total) {
-        const uint32_t q = lst[threadIdx.x];
+    for (uint32_t i = threadIdx.x; i < total; i += 256u) {
+        const uint32_t q = lst[i];
         const float4 o = w.O[q], d = w.D[q];
         Ray r;
         r.O = mk(o.x, o.y, o.z);
@@ -551,20 +583,30 @@ __global__ __launch_bounds__(256) VPX_WPE(VPX_WPE_NEAREST) void k_nearest_tile(S
         r.inside = (__float_as_uint(d.w) & kInside) != 0u;
         nearest_record(sv, w, q, r, k);
     }
-    flush_counters(k, 0u, ctr);
+    flush_counters(k, 0u, ctr, VPX_STAGE_BOUNCE);
 }
 
-// Renderer::IsOccluded for the tile's shadow slots (entry = slot << 27 | path); sets the
-// slot's occluded flag.  The light sums are formed in slot order by k_resolve.
+// Renderer::IsOccluded for the shadow slots of G tiles (entry = slot << 27 | path); sets
+// the slot's occluded flag.  The light sums are formed in slot order by k_resolve.
 __global__ __launch_bounds__(256) VPX_WPE(VPX_WPE_SHADOW) void k_shadow_tile(SceneView sv, WaveBufs w, unsigned long long* __restrict__ ctr) {
     __shared__ uint32_t sh[4];
-    extern __shared__ uint32_t lst_dyn[];  // [S * 256]
-    const uint32_t p = blockIdx.x * 256u + threadIdx.x;
+    extern __shared__ uint32_t lst_dyn[];  // [S * 256 * G]
+    const uint32_t base = blockIdx.x * 256u * kGroupTiles;
     Counters k{0u, 0u, 0u};
-    const uint32_t m = p < w.P ? w.smask[p] : 0u;
+    uint32_t m[kGroupTiles], cnt[kGroupTiles];
+#pragma unroll
+    for (uint32_t g = 0; g < kGroupTiles; ++g) {
+        const uint32_t p = base + threadIdx.x * kGroupTiles + g;
+        m[g] = p < w.P ? w.smask[p] : 0u;
+        cnt[g] = (uint32_t)__popc(m[g]);
+    }
     uint32_t total;
-    uint32_t at = block_scan((uint32_t)__popc(m), total, sh);
-    for (uint32_t b = m; b; b &= b - 1u) lst_dyn[at++] = ((uint32_t)__ffs(b) - 1u) << 27 | p;
+    uint32_t at = group_scan<kGroupTiles>(cnt, total, sh);
+#pragma unroll
+    for (uint32_t g = 0; g < kGroupTiles; ++g) {
+        const uint32_t p = base + threadIdx.x * kGroupTiles + g;
+        for (uint32_t b = m[g]; b; b &= b - 1u) lst_dyn[at++] = ((uint32_t)__ffs(b) - 1u) << 27 | p;
+    }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < total; i += 256u) {
         const uint32_t e = lst_dyn[i];
@@ -576,7 +618,7 @@ __global__ __launch_bounds__(256) VPX_WPE(VPX_WPE_SHADOW) void k_shadow_tile(Sce
         r.t = so.w;
         if (shadow(sv, r, k)) w.SD[slot].w = __uint_as_float(__float_as_uint(sd.w) | 4u /* occluded */);
     }
-    flush_counters(k, 0u, ctr);
+    flush_counters(k, 0u, ctr, VPX_STAGE_SHADOW);
 }
 
 // ------------------------------------------------------------------- stage 4
