@@ -1,0 +1,63 @@
+"""GPU parity at BASELINE.json's full sizes (C1-C4 on one GPU).
+
+The oracle cannot render these frames in seconds, so each test checks size-independent
+properties instead: the 1 GiB / 8 GiB device world equals the host generator (checksum of
+every byte), and a seeded sample of pixels of the full-size GPU frame equals the oracle's
+samples for the same pixels bit for bit (accumulator floats after frame 0 = the sample,
+and the RGB8 bytes).  Worlds are generated on the host too (up to 8 GiB), so these run
+one config at a time and free everything afterwards.
+"""
+import gc
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():
+    pytest.skip("no GPU", allow_module_level=True)
+
+from cases import bits  # noqa: E402
+
+SAMPLES = 3000
+
+
+def sample_ids(W, H, seed):
+    rng = np.random.default_rng(seed)
+    ids = rng.choice(W * H, SAMPLES, replace=False)
+    edge = np.array([0, W - 1, (H - 1) * W, H * W - 1, (H // 2) * W + W // 2])  # corners + centre
+    return np.unique(np.concatenate([ids, edge])).astype(np.uint32)
+
+
+@pytest.mark.parametrize("cfg", ["C1", "C2", "C3", "C4"])
+def test_full_size_config_sampled(pkg, orc, cfg):
+    desc = pkg.scene.CONFIGS[cfg]()
+    W, H = desc.width, desc.height
+    r = pkg.renderer.Renderer(desc, 0)
+    r.Init()
+    st = r.Tick(0.0, stats=True)
+    torch.cuda.synchronize()
+    acc = r.accumulator.view(-1, 4)
+    ids = sample_ids(W, H, sum(map(ord, cfg)))
+    idx = torch.from_numpy(ids.astype(np.int64)).to(acc.device)
+    acc_g = acc[idx].cpu().numpy()
+    rgb_g = r.screen.view(-1)[idx].cpu().numpy().view(np.uint32)
+    sums = [r.ctx.grid_checksum(i) for i in range(len(desc.grids))]
+    r.ctx.close()
+    del r, acc
+    torch.cuda.empty_cache()
+
+    o = orc.Oracle(pkg.abi, desc)
+    for i, c in enumerate(o.cells):  # the whole device world, byte for byte (checksum)
+        assert sums[i] == o.lib.oracle_grid_checksum(c.ctypes.data, c.size), f"grid {i}"
+    sample, ost = o.render_pixels(desc.frame_params(0), ids)
+    assert np.array_equal(bits(acc_g), bits(sample)), f"{cfg}: accumulator mismatch"
+    rgb_o = np.zeros(len(ids), np.uint32)
+    acc_o = np.zeros((len(ids), 4), np.float32)
+    for k in range(len(ids)):
+        o.lib.oracle_accumulate_tonemap(sample[k].ctypes.data, 0, acc_o[k].ctypes.data, rgb_o[k:k + 1].ctypes.data)
+    assert np.array_equal(rgb_g, rgb_o), f"{cfg}: RGB8 mismatch"
+    assert st.primary_rays == W * H
+    del o
+    gc.collect()
