@@ -37,13 +37,14 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level
 METRIC = "Mray/s (primary+shadow) at 1920×1080, 1024³ world; 1/2/4/8-GPU"
 
 
-def weak_size(n):
-    """Frame of N x 1920x1080 pixels: 1 -> 1920x1080, 2 -> 3840x1080, 4 -> 3840x2160, 8 -> 7680x2160."""
+def weak_size(n, base=(1920, 1080)):
+    """Frame of N x the config's own frame: for C1, 1 -> 1920x1080, 2 -> 3840x1080,
+    4 -> 3840x2160, 8 -> 7680x2160."""
     a = 1 << math.ceil(math.log2(n) / 2) if n > 1 else 1
     b = n // a
     if a * b != n:
         a, b = n, 1
-    return 1920 * a, 1080 * b
+    return base[0] * a, base[1] * b
 
 
 def build_scene(pkg, cfg, width=None, height=None):
@@ -114,10 +115,9 @@ def run(args):
     if n > 1:
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    W, H = weak_size(n)
+    desc = pkg.scene.CONFIGS[args.config]()
+    W, H = weak_size(n, (desc.width, desc.height))
     desc = build_scene(pkg, args.config, W, H)
-    if n == 1 and args.config != "C1":
-        W, H = desc.width, desc.height
     stream = torch.cuda.Stream()  # a real stream: the kernel and its HIP events share it
     torch.cuda.set_stream(stream)
     ctx = pkg.context.Context(local)
@@ -212,7 +212,7 @@ def run(args):
             "metric": METRIC, "value": round(value, 3), "unit": "Mray/s", "n_gpus": n, "steps": K,
             "warmup": args.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-            "data": "synthetic world: monu3.vox (decoded by the reference's ogt_vox) tiled into a "
+            "data": f"synthetic world '{desc.name}': the reference's .vox asset decoded like ogt_vox, placed in a "
                     f"{desc.grids[0].n}^3 u8 grid on device; fixed lights/camera (SURVEY.md §8(d))",
             "config": {"workload": f"{args.config}: {W}x{H}, {desc.grids[0].n}^3 {desc.name}, 1 spp, "
                                    f"Trace depth {desc.max_bounces} (primary+shadow)",

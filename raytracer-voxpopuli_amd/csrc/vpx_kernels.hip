@@ -922,9 +922,9 @@ extern "C" int vpx_profile_read(vpx_ctx* c, vpx_profile* out, int reset) {
 
 #ifdef VPX_PHASE_PROF
 extern "C" int vpx_debug_phase(unsigned long long* out, int reset) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(vpx::g_phase), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(vpx::g_phase), sizeof(unsigned long long) * 32) != hipSuccess) return -1;
     if (reset) {
-        const unsigned long long z[16] = {};
+        const unsigned long long z[32] = {};
         if (hipMemcpyToSymbol(HIP_SYMBOL(vpx::g_phase), z, sizeof(z)) != hipSuccess) return -1;
     }
     return 0;

@@ -283,6 +283,13 @@ __device__ __forceinline__ skip::Walk to_walk(const Dda& s) {
 // classify / skip_box / step1 as skip::walk_skip (so results are identical), but the long
 // skip_box is executed in batches — only when few lanes of the wave still want to take
 // plain cell steps — instead of inside every step iteration of the wave.
+// Skip-phase weights (measured on C1 / C3: FindNearest 2, IsOccluded 4).
+#ifndef VPX_SKIPW_NEAREST
+#define VPX_SKIPW_NEAREST 2
+#endif
+#ifndef VPX_SKIPW_SHADOW
+#define VPX_SKIPW_SHADOW 4
+#endif
 #ifndef VPX_STEP_THRESHOLD
 #define VPX_STEP_THRESHOLD 16
 #endif
@@ -291,7 +298,7 @@ constexpr uint32_t kStepThreshold = VPX_STEP_THRESHOLD;
 #ifdef VPX_PHASE_PROF
 // Debug build only (-DVPX_PHASE_PROF): per-wave cycles / iterations / active lanes of the
 // step and skip phases of walk_wave, read back with vpx_debug_phase().
-__device__ unsigned long long g_phase[16];
+__device__ unsigned long long g_phase[32];
 #define VPX_PH(...) __VA_ARGS__
 #else
 #define VPX_PH(...)
@@ -317,7 +324,24 @@ __device__ __forceinline__ void skip_box_of(const skip::Walk& w, int level, uint
 #ifndef VPX_LEAN_SHADOW
 #define VPX_LEAN_SHADOW 1
 #endif
-template <bool LEAN>
+#ifndef VPX_ADAPT_SHADOW
+#define VPX_ADAPT_SHADOW 0
+#endif
+// ADAPT (rays that start on a surface): skip only boxes the lean tier can take — per axis
+// h >= l * d, i.e. at most one binade change — shrinking an empty 64^3 super to the 16^3
+// macro around the cell when needed; otherwise march the cell like the reference.
+__device__ __forceinline__ bool lean_fits(const skip::Walk& w, uint32_t m, uint32_t n) {
+    const uint32_t lx = w.sx > 0 ? ((w.X | m) < n - 1u ? (w.X | m) : n - 1u) - w.X : w.X - (w.X & ~m);
+    const uint32_t ly = w.sy > 0 ? ((w.Y | m) < n - 1u ? (w.Y | m) : n - 1u) - w.Y : w.Y - (w.Y & ~m);
+    const uint32_t lz = w.sz > 0 ? ((w.Z | m) < n - 1u ? (w.Z | m) : n - 1u) - w.Z : w.Z - (w.Z & ~m);
+    return (!lx || w.tx >= (float)lx * w.dx) && (!ly || w.ty >= (float)ly * w.dy) && (!lz || w.tz >= (float)lz * w.dz);
+}
+__device__ __forceinline__ int lean_box(const skip::Walk& w, int cls, uint32_t n) {
+    if (lean_fits(w, cls == 3 ? 63u : 15u, n)) return cls;
+    return (cls == 3 && lean_fits(w, 15u, n)) ? 2 : 1;
+}
+
+template <bool LEAN, bool ADAPT = false, int PHK = 0, uint32_t SKIPW = 0>
 __device__ __forceinline__ bool walk_wave(const skip::GridView& g, skip::Walk& w, float bound, uint32_t& cells) {
     enum : int { kStep = 0, kSkip = 1, kMiss = 2, kHit = 3 };
     int mode = kStep, pending = 0;
@@ -327,17 +351,21 @@ __device__ __forceinline__ bool walk_wave(const skip::GridView& g, skip::Walk& w
         for (;;) {
             const uint64_t stepping = __ballot(mode == kStep);
             if (!stepping) break;
-            if ((uint32_t)__popcll(stepping) < kStepThreshold && __ballot(mode == kSkip)) break;
+            // cost-weighted: a skip phase costs several step phases, so keep stepping while
+            // steppers x SKIPW >= waiting skippers (SKIPW = 0: while >= kStepThreshold step)
+            if (SKIPW ? (uint32_t)__popcll(stepping) * SKIPW < (uint32_t)__popcll(__ballot(mode == kSkip))
+                      : ((uint32_t)__popcll(stepping) < kStepThreshold && __ballot(mode == kSkip)))
+                break;
             VPX_PH(++ns; ls += __popcll(stepping);)
             if (mode == kStep) {
                 if (!(w.t < bound)) {
                     mode = kMiss;
                 } else {
-                    const int cls = skip::classify(w, g);
+                    int cls = skip::classify(w, g);
                     if (cls == 0) {
                         ++cells;
                         mode = kHit;
-                    } else if (cls >= 2) {
+                    } else if (cls >= 2 && (!ADAPT || (cls = lean_box(w, cls, g.n)) >= 2)) {
                         mode = kSkip;
                         pending = cls;
                     } else {
@@ -371,15 +399,15 @@ __device__ __forceinline__ bool walk_wave(const skip::GridView& g, skip::Walk& w
     }
 #ifdef VPX_PHASE_PROF
     if ((threadIdx.x & 63) == __builtin_amdgcn_readfirstlane(threadIdx.x & 63)) {
-        atomicAdd(&g_phase[0], cs);
-        atomicAdd(&g_phase[1], ck);
-        atomicAdd(&g_phase[2], ns);
-        atomicAdd(&g_phase[3], nk);
-        atomicAdd(&g_phase[4], ls);
-        atomicAdd(&g_phase[5], lk);
-        atomicAdd(&g_phase[6], 1ull);
-        atomicAdd(&g_phase[7], fb);
-        atomicAdd(&g_phase[8], cf);
+        atomicAdd(&g_phase[PHK + 0], cs);
+        atomicAdd(&g_phase[PHK + 1], ck);
+        atomicAdd(&g_phase[PHK + 2], ns);
+        atomicAdd(&g_phase[PHK + 3], nk);
+        atomicAdd(&g_phase[PHK + 4], ls);
+        atomicAdd(&g_phase[PHK + 5], lk);
+        atomicAdd(&g_phase[PHK + 6], 1ull);
+        atomicAdd(&g_phase[PHK + 7], fb);
+        atomicAdd(&g_phase[PHK + 8], cf);
     }
 #endif
     return mode == kHit;
@@ -548,7 +576,7 @@ __device__ __forceinline__ int32_t find_nearest(const SceneView& sv, Ray& r, Cou
         Dda s;
         if (!dda_setup(vol, g.n, o, s)) continue;
         skip::Walk w = to_walk(s);
-        if (walk_wave<VPX_LEAN_NEAREST != 0>(grid_view(g), w, r.t, k.cells)) {
+        if (walk_wave<VPX_LEAN_NEAREST != 0, false, 0, VPX_SKIPW_NEAREST>(grid_view(g), w, r.t, k.cells)) {
             r.t = w.t;
             r.N = normal_voxel(o, w.t, g.n, vol.matrix);
             r.mat = g.cells[(uint64_t)w.X + (uint64_t)w.Y * g.n + (uint64_t)w.Z * ((uint64_t)g.n * g.n)];
@@ -582,7 +610,7 @@ __device__ __forceinline__ bool is_occluded(const SceneView& sv, const Ray& r, C
         Dda s;
         if (!dda_setup(vol, g.n, o, s)) continue;
         skip::Walk w = to_walk(s);
-        if (walk_wave<VPX_LEAN_SHADOW != 0>(grid_view(g), w, r.t, k.cells)) return true;  // first solid cell, t < bound
+        if (walk_wave<VPX_LEAN_SHADOW != 0, VPX_ADAPT_SHADOW != 0, 16, VPX_SKIPW_SHADOW>(grid_view(g), w, r.t, k.cells)) return true;  // first solid cell, t < bound
     }
     for (uint32_t i = 0; i < sv.num_spheres; ++i)
         if (sphere_is_hit(sv.spheres[i], r)) return true;

@@ -135,11 +135,34 @@ extern "C" void walk_sim(const uint8_t* cells, const uint64_t* l1, const uint64_
                     if (!(w.m2 & (0x330033ull << (2 * gx + 8 * gy + 32 * gz)))) m = 7;
                 }
             }
+            if (box && (opt & 8)) {  // adaptive: shrink the box until the lean tier applies (h >= l d per axis)
+                auto fits = [&](uint32_t mm) {
+                    const float h[3] = {w.tx, w.ty, w.tz}, d[3] = {w.dx, w.dy, w.dz};
+                    const int32_t sg[3] = {w.sx, w.sy, w.sz};
+                    const uint32_t c3[3] = {w.X, w.Y, w.Z};
+                    for (int k = 0; k < 3; ++k) {
+                        const uint32_t lo_ = c3[k] & ~mm, hi_ = (c3[k] | mm) < n - 1u ? (c3[k] | mm) : n - 1u;
+                        const uint32_t l = sg[k] > 0 ? hi_ - c3[k] : c3[k] - lo_;
+                        if (l && !(h[k] >= (float)l * d[k])) return false;
+                    }
+                    return true;
+                };
+                if (!fits(m)) {
+                    if (m > 15 && fits(15)) m = 15;
+                    else box = false;
+                }
+            }
             if (box) {
                 ++skips;
                 { Walk t = w; uint32_t cc = 0; uint32_t blo[3], bhi[3];
                   for (int k = 0; k < 3; ++k) { const uint32_t q = k == 0 ? w.X : k == 1 ? w.Y : w.Z; blo[k] = q & ~m; bhi[k] = (q | m) < n - 1u ? (q | m) : n - 1u; }
-                  out[6] += skip_box_fast1(t, blo, bhi, bound, cc) == 2; }
+                  const bool miss = skip_box_fast1(t, blo, bhi, bound, cc) == 2;
+                  out[6] += miss;
+                  if (miss && m > 15) {  // retry with the 16^3 macro box around the cell
+                      for (int k = 0; k < 3; ++k) { const uint32_t q = k == 0 ? w.X : k == 1 ? w.Y : w.Z; blo[k] = q & ~15u; bhi[k] = (q | 15u) < n - 1u ? (q | 15u) : n - 1u; }
+                      Walk t2 = w; uint32_t c2 = 0;
+                      out[7] += skip_box_fast1(t2, blo, bhi, bound, c2) == 2;
+                  } else out[7] += miss; }
                 for (int k = 0; k < 3; ++k) {
                     const uint32_t cc = k == 0 ? w.X : k == 1 ? w.Y : w.Z;
                     lo[k] = cc & ~m;

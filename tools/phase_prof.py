@@ -12,19 +12,20 @@ import bench  # noqa: E402
 pkg = entry.load_package()
 lib = pkg.abi.load_library()
 lib.vpx_debug_phase.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
-desc = bench.build_scene(pkg, os.environ.get("CFG", "C1"), 1920, 1080)
+desc = pkg.scene.CONFIGS[os.environ.get("CFG", "C1")]()
 ctx = pkg.context.Context(0)
 ctx.load_scene(desc)
 W, H = desc.width, desc.height
 acc = torch.zeros(W * H * 4, dtype=torch.float32, device="cuda")
 rgb = torch.zeros(W * H, dtype=torch.int32, device="cuda")
-ph = (C.c_ulonglong * 16)()
+ph = (C.c_ulonglong * 32)()
 for f in range(4):
     ctx.render(desc.frame_params(frame_index=f), acc.data_ptr(), rgb.data_ptr())
     torch.cuda.synchronize()
     lib.vpx_debug_phase(ph, 1)
-cs, ck, ns, nk, ls, lk, walks, fb, cf = list(ph)[:9]
-print(f"walk calls(waves)={walks}  step: cycles={cs:.3e} iters={ns} lanes/iter={ls / max(ns, 1):.1f} "
-      f"cyc/iter={cs / max(ns, 1):.0f} | skip: cycles={ck:.3e} iters={nk} lanes/iter={lk / max(nk, 1):.1f} "
-      f"cyc/iter={ck / max(nk, 1):.0f} | per walk: step it={ns / walks:.1f} skip it={nk / walks:.1f}")
-print(f"classify phases {fb} cycles {cf:.3e} ({cf / max(fb, 1):.0f}/iter)")
+for name, off in (("nearest", 0), ("shadow", 16)):
+    cs, ck, ns, nk, ls, lk, walks, fb, cf = list(ph)[off:off + 9]
+    walks = max(walks, 1)
+    print(f"[{name}] walk calls(waves)={walks}  step: cycles={cs:.3e} iters={ns} lanes/iter={ls / max(ns, 1):.1f} "
+          f"cyc/iter={cs / max(ns, 1):.0f} | skip: cycles={ck:.3e} iters={nk} lanes/iter={lk / max(nk, 1):.1f} "
+          f"cyc/iter={ck / max(nk, 1):.0f} | per walk: step it={ns / walks:.1f} skip it={nk / walks:.1f}")
