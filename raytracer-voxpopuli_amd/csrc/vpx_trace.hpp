@@ -386,7 +386,7 @@ __device__ __forceinline__ bool walk_wave(const skip::GridView& g, skip::Walk& w
             uint32_t lo[3], hi[3];
             skip_box_of(w, pending, g.n, lo, hi);
             int sr = LEAN ? skip::skip_box_fast1(w, lo, hi, bound, cells) : 2;
-            if (sr == 2) sr = skip::skip_box_fast(w, lo, hi, bound, cells);
+            if (!LEAN && sr == 2) sr = skip::skip_box_fast(w, lo, hi, bound, cells);  // (a subset of the lean tier)
             if (sr == 2) sr = skip::skip_box(w, lo, hi, bound, cells);
             if (sr == 1) {
                 mode = kMiss;
