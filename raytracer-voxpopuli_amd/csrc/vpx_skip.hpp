@@ -288,6 +288,7 @@ VPX_HD uint32_t lin_index(uint32_t x, uint32_t y, uint32_t z, uint32_t nb) {
 // slower on the device: the per-wave divergence of that branch costs more than it saves.)
 VPX_HD int classify(Walk& w, const GridView& g) {
     const uint32_t X = w.X, Y = w.Y, Z = w.Z;
+
     const uint32_t k3 = pack3(X >> 6, Y >> 6, Z >> 6);
     if (k3 != w.k3) {
         w.k3 = k3;

@@ -324,24 +324,8 @@ __device__ __forceinline__ void skip_box_of(const skip::Walk& w, int level, uint
 #ifndef VPX_LEAN_SHADOW
 #define VPX_LEAN_SHADOW 1
 #endif
-#ifndef VPX_ADAPT_SHADOW
-#define VPX_ADAPT_SHADOW 0
-#endif
-// ADAPT (rays that start on a surface): skip only boxes the lean tier can take — per axis
-// h >= l * d, i.e. at most one binade change — shrinking an empty 64^3 super to the 16^3
-// macro around the cell when needed; otherwise march the cell like the reference.
-__device__ __forceinline__ bool lean_fits(const skip::Walk& w, uint32_t m, uint32_t n) {
-    const uint32_t lx = w.sx > 0 ? ((w.X | m) < n - 1u ? (w.X | m) : n - 1u) - w.X : w.X - (w.X & ~m);
-    const uint32_t ly = w.sy > 0 ? ((w.Y | m) < n - 1u ? (w.Y | m) : n - 1u) - w.Y : w.Y - (w.Y & ~m);
-    const uint32_t lz = w.sz > 0 ? ((w.Z | m) < n - 1u ? (w.Z | m) : n - 1u) - w.Z : w.Z - (w.Z & ~m);
-    return (!lx || w.tx >= (float)lx * w.dx) && (!ly || w.ty >= (float)ly * w.dy) && (!lz || w.tz >= (float)lz * w.dz);
-}
-__device__ __forceinline__ int lean_box(const skip::Walk& w, int cls, uint32_t n) {
-    if (lean_fits(w, cls == 3 ? 63u : 15u, n)) return cls;
-    return (cls == 3 && lean_fits(w, 15u, n)) ? 2 : 1;
-}
 
-template <bool LEAN, bool ADAPT = false, int PHK = 0, uint32_t SKIPW = 0>
+template <bool LEAN, int PHK = 0, uint32_t SKIPW = 0>
 __device__ __forceinline__ bool walk_wave(const skip::GridView& g, skip::Walk& w, float bound, uint32_t& cells) {
     enum : int { kStep = 0, kSkip = 1, kMiss = 2, kHit = 3 };
     int mode = kStep, pending = 0;
@@ -361,11 +345,11 @@ __device__ __forceinline__ bool walk_wave(const skip::GridView& g, skip::Walk& w
                 if (!(w.t < bound)) {
                     mode = kMiss;
                 } else {
-                    int cls = skip::classify(w, g);
+                    const int cls = skip::classify(w, g);
                     if (cls == 0) {
                         ++cells;
                         mode = kHit;
-                    } else if (cls >= 2 && (!ADAPT || (cls = lean_box(w, cls, g.n)) >= 2)) {
+                    } else if (cls >= 2) {
                         mode = kSkip;
                         pending = cls;
                     } else {
@@ -576,7 +560,7 @@ __device__ __forceinline__ int32_t find_nearest(const SceneView& sv, Ray& r, Cou
         Dda s;
         if (!dda_setup(vol, g.n, o, s)) continue;
         skip::Walk w = to_walk(s);
-        if (walk_wave<VPX_LEAN_NEAREST != 0, false, 0, VPX_SKIPW_NEAREST>(grid_view(g), w, r.t, k.cells)) {
+        if (walk_wave<VPX_LEAN_NEAREST != 0, 0, VPX_SKIPW_NEAREST>(grid_view(g), w, r.t, k.cells)) {
             r.t = w.t;
             r.N = normal_voxel(o, w.t, g.n, vol.matrix);
             r.mat = g.cells[(uint64_t)w.X + (uint64_t)w.Y * g.n + (uint64_t)w.Z * ((uint64_t)g.n * g.n)];
@@ -610,7 +594,7 @@ __device__ __forceinline__ bool is_occluded(const SceneView& sv, const Ray& r, C
         Dda s;
         if (!dda_setup(vol, g.n, o, s)) continue;
         skip::Walk w = to_walk(s);
-        if (walk_wave<VPX_LEAN_SHADOW != 0, VPX_ADAPT_SHADOW != 0, 16, VPX_SKIPW_SHADOW>(grid_view(g), w, r.t, k.cells)) return true;  // first solid cell, t < bound
+        if (walk_wave<VPX_LEAN_SHADOW != 0, 16, VPX_SKIPW_SHADOW>(grid_view(g), w, r.t, k.cells)) return true;  // first solid cell, t < bound
     }
     for (uint32_t i = 0; i < sv.num_spheres; ++i)
         if (sphere_is_hit(sv.spheres[i], r)) return true;

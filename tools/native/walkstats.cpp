@@ -26,6 +26,8 @@ static bool fast_ok(const Walk& w, const uint32_t lo[3], const uint32_t hi[3]) {
 }
 
 static uint64_t g_why[8];
+static uint64_t g_cross[16];
+extern "C" void cross_out(uint64_t* o) { for (int i = 0; i < 16; ++i) { o[i] = g_cross[i]; g_cross[i] = 0; } }
 static void why(const Walk& w, const uint32_t lo[3], const uint32_t hi[3]) {
     const float h[3] = {w.tx, w.ty, w.tz}, d[3] = {w.dx, w.dy, w.dz};
     const int32_t s[3] = {w.sx, w.sy, w.sz};
@@ -158,6 +160,20 @@ extern "C" void walk_sim(const uint8_t* cells, const uint64_t* l1, const uint64_
                   for (int k = 0; k < 3; ++k) { const uint32_t q = k == 0 ? w.X : k == 1 ? w.Y : w.Z; blo[k] = q & ~m; bhi[k] = (q | m) < n - 1u ? (q | m) : n - 1u; }
                   const bool miss = skip_box_fast1(t, blo, bhi, bound, cc) == 2;
                   out[6] += miss;
+                  if (miss) {  // crossings needed: max over axes of binades spanned by A(0..l)
+                      const float hh[3] = {w.tx, w.ty, w.tz}, dd[3] = {w.dx, w.dy, w.dz};
+                      const int32_t sg[3] = {w.sx, w.sy, w.sz};
+                      const uint32_t c3[3] = {w.X, w.Y, w.Z};
+                      uint32_t worst = 0;
+                      for (int k = 0; k < 3; ++k) {
+                          const uint32_t l = sg[k] > 0 ? bhi[k] - c3[k] : c3[k] - blo[k];
+                          if (!l || !(hh[k] > 0) || !(dd[k] > 0)) continue;
+                          const float A = jump(hh[k], dd[k], l);
+                          const uint32_t cr = (fbits(A) >> 23) - (fbits(hh[k]) >> 23);
+                          worst = cr > worst ? cr : worst;
+                      }
+                      g_cross[worst < 15 ? worst : 15]++;
+                  }
                   if (miss && m > 15) {  // retry with the 16^3 macro box around the cell
                       for (int k = 0; k < 3; ++k) { const uint32_t q = k == 0 ? w.X : k == 1 ? w.Y : w.Z; blo[k] = q & ~15u; bhi[k] = (q | 15u) < n - 1u ? (q | 15u) : n - 1u; }
                       Walk t2 = w; uint32_t c2 = 0;

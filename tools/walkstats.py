@@ -97,9 +97,11 @@ for name, (a, b, bnd) in sets.items():
     R = len(a)
     line = []
     ref = None
-    for opt in (0, 8, 9):
+    for opt in (0,):
         o = sim(a, b, bnd, opt)
         if ref is None: ref = o
         assert o[0] == ref[0] and o[3] == ref[3] and o[4] == ref[4] and o[5] == ref[5], (name, opt)  # same cells / hits / end state
         line.append(f"opt{opt}: steps {o[1]/R:.1f} skips {o[2]/R:.1f} lean-miss {o[6]/max(o[2],1):.4f} (+16 retry {o[7]/max(o[2],1):.4f}) cost {(o[1] + 5.8 * o[2]) / R:.0f}")
     print(f"{name} ({R} rays, cells {ref[0]/R:.0f}): " + " | ".join(line))
+    cr = np.zeros(16, np.uint64); lib.cross_out.argtypes = [V]; lib.cross_out(cr.ctypes.data)
+    print("   lean failures by binade crossings (max over axes):", cr[:10])
