@@ -202,6 +202,18 @@ int vpx_upload_grid(vpx_ctx* ctx, uint32_t grid_id, const uint8_t* cells, uint32
 int vpx_generate_tiled_grid(vpx_ctx* ctx, uint32_t grid_id, uint32_t n, const uint8_t* model,
                             uint32_t mx, uint32_t my, uint32_t mz,
                             uint32_t px, uint32_t py, uint32_t pz, uint32_t ground);
+/* In-place world edits.  Each refreshes the occupancy levels
+   of the touched bricks only.
+   Scene::ResetGrid(type) (template/scene.cpp:356-359): every cell = value. */
+int vpx_grid_fill(vpx_ctx* ctx, uint32_t grid_id, uint8_t value);
+/* Dirty-region upload: a box of cells, host bytes x fastest (src[x + y*dx + z*dx*dy]),
+   written at (x0, y0, z0) — what Scene::Set-based edits change (LoadModelPartial from
+   ModifyingProp::Update, src/Game/ModifyingProp.cpp:11-21; zone changes). */
+int vpx_grid_write_box(vpx_ctx* ctx, uint32_t grid_id, const uint8_t* src, uint32_t x0, uint32_t y0,
+                       uint32_t z0, uint32_t dx, uint32_t dy, uint32_t dz);
+/* Scene::CreateEmmisiveSphere(mat, radius) (template/scene.cpp:685-711) on the device:
+   cells with length(worldsize/2 - (x,y,z)) < radius get `mat` (others unchanged). */
+int vpx_grid_emissive_sphere(vpx_ctx* ctx, uint32_t grid_id, uint8_t mat, float radius);
 /* FNV-1a-style 64-bit checksum of a device grid (for size-independent parity checks). */
 int vpx_grid_checksum(vpx_ctx* ctx, uint32_t grid_id, uint64_t* out);
 int vpx_set_volumes(vpx_ctx* ctx, const vpx_volume* volumes, uint32_t count);

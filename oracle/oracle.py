@@ -37,6 +37,11 @@ def _lib(abi):
     lib.oracle_load_model.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, P(C.c_float),
                                       C.c_void_p]
     lib.oracle_load_model.restype = None
+    lib.oracle_load_model_partial.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
+                                              P(C.c_float), C.c_uint32, C.c_uint32, C.c_void_p]
+    lib.oracle_load_model_partial.restype = None
+    lib.oracle_emissive_sphere.argtypes = [C.c_void_p, C.c_uint32, C.c_uint8, C.c_float]
+    lib.oracle_emissive_sphere.restype = None
     lib.oracle_orient_model.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p]
     lib.oracle_orient_model.restype = None
     lib.oracle_tiled_world.argtypes = [C.c_void_p] + [C.c_uint32] * 8 + [C.c_void_p]

@@ -1143,6 +1143,50 @@ void oracle_load_model(const uint8_t* vox, uint32_t sx, uint32_t sy, uint32_t sz
             }
 }
 
+/* Scene::LoadModelPartial (template/scene.cpp:531-604): ResetGrid() to NONE, the
+   LoadModel scale rule, then only voxels with x in [columns - thickness, columns +
+   thickness] (uint32 arithmetic, as written: the lower bound wraps when thickness >
+   columns).  Writes outside the grid are skipped (the reference's Set does not check). */
+void oracle_load_model_partial(const uint8_t* vox, uint32_t sx, uint32_t sy, uint32_t sz, uint32_t n,
+                               const float scale_model[3], uint32_t columns, uint32_t thickness, uint8_t* out)
+{
+    const uint64_t n64 = n;
+    memset(out, NONE_MAT, n64 * n64 * n64);
+    float scl[3] = {scale_model[0], scale_model[1], scale_model[2]};
+    if (sx > n) {
+        scl[0] *= (float)n / (float)sx;
+        scl[1] *= (float)n / (float)sy;
+        scl[2] *= (float)n / (float)sz;
+    }
+    const uint32_t lo = columns - thickness, hi = columns + thickness;
+    for (uint32_t z = 0; z < sz; ++z)
+        for (uint32_t y = 0; y < sy; ++y)
+            for (uint32_t x = 0; x < sx; ++x) {
+                const int gx = f2i_trunc((float)x * scl[0]);
+                const int gy = f2i_trunc((float)z * scl[1]);
+                const int gz = f2i_trunc((float)y * scl[2]);
+                const uint8_t c = vox[x + (uint64_t)y * sx + (uint64_t)z * sx * sy];
+                if (c == 0 || !(x >= lo && x <= hi)) continue;
+                if (gx < 0 || gy < 0 || gz < 0 || (uint32_t)gx >= n || (uint32_t)gy >= n || (uint32_t)gz >= n)
+                    continue;
+                out[(uint64_t)gx + (uint64_t)gy * n64 + (uint64_t)gz * n64 * n64] = c;
+            }
+}
+
+/* Scene::CreateEmmisiveSphere (template/scene.cpp:685-711), worldsize = n. */
+void oracle_emissive_sphere(uint8_t* grid, uint32_t n, uint8_t mat, float radius)
+{
+    const uint64_t n64 = n;
+    const float c = (float)n / 2.0f;
+    for (uint32_t z = 0; z < n; ++z)
+        for (uint32_t y = 0; y < n; ++y)
+            for (uint32_t x = 0; x < n; ++x) {
+                const float vx = c - (float)x, vy = c - (float)y, vz = c - (float)z;
+                const float d = sqrtf(vx * vx + vy * vy + vz * vz);
+                if (d < radius) grid[x + (uint64_t)y * n64 + (uint64_t)z * n64 * n64] = mat;
+            }
+}
+
 void oracle_orient_model(const uint8_t* vox, uint32_t sx, uint32_t sy, uint32_t sz, uint8_t* out)
 {
     /* grid-oriented dims: gx = sx, gy = sz, gz = sy */

@@ -98,6 +98,11 @@ void oracle_offset_ray(const float p[3], const float n[3], float out[3]);
 float oracle_cube_intersect(const float b0[3], const float b1[3], const float o[3],
                             const float d[3], const float rd[3]);
 
+/* World edits: Scene::LoadModelPartial / CreateEmmisiveSphere. */
+void oracle_load_model_partial(const uint8_t* vox, uint32_t sx, uint32_t sy, uint32_t sz, uint32_t n,
+                               const float scale_model[3], uint32_t columns, uint32_t thickness, uint8_t* out);
+void oracle_emissive_sphere(uint8_t* grid, uint32_t n, uint8_t mat, float radius);
+
 #ifdef __cplusplus
 }
 #endif

@@ -132,6 +132,9 @@ SIGNATURES = {
     "vpx_composite_tiles": (C.c_int, [C.c_void_p, C.POINTER(FrameParams), C.c_uint32, C.c_uint32, C.c_uint32,
                                       C.c_void_p, C.c_void_p, C.c_void_p]),
     "vpx_get_counters": (C.c_int, [C.c_void_p, C.POINTER(Stats), C.c_int]),
+    "vpx_grid_fill": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint8]),
+    "vpx_grid_write_box": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p] + [C.c_uint32] * 6),
+    "vpx_grid_emissive_sphere": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint8, C.c_float]),
     "vpx_profile_enable": (C.c_int, [C.c_void_p, C.c_uint32]),
     "vpx_profile_read": (C.c_int, [C.c_void_p, C.POINTER(Profile), C.c_int]),
     "vpx_find_nearest": (C.c_int, [C.c_void_p, C.POINTER(Ray), C.c_uint32, C.POINTER(Hit)]),

@@ -66,6 +66,24 @@ class Context:
     def set_camera(self, cam):
         self._chk(self.lib.vpx_set_camera(self.h, C.byref(cam)), "vpx_set_camera")
 
+    # ------------------------------------------------------------ world edits
+    def grid_fill(self, grid_id, value):
+        """Scene::ResetGrid(type) (template/scene.cpp:356-359) on the device copy."""
+        self._chk(self.lib.vpx_grid_fill(self.h, grid_id, int(value)), "vpx_grid_fill")
+
+    def grid_write_box(self, grid_id, box, origin):
+        """Dirty-region upload: box = uint8 array (dz, dy, dx) written at origin (x0, y0, z0)."""
+        b = np.ascontiguousarray(box, np.uint8)
+        dz, dy, dx = b.shape
+        x0, y0, z0 = origin
+        self._chk(self.lib.vpx_grid_write_box(self.h, grid_id, b.ctypes.data_as(C.c_void_p), x0, y0, z0, dx, dy, dz),
+                  "vpx_grid_write_box")
+
+    def grid_emissive_sphere(self, grid_id, mat, radius):
+        """Scene::CreateEmmisiveSphere(mat, radius) (template/scene.cpp:685-711)."""
+        self._chk(self.lib.vpx_grid_emissive_sphere(self.h, grid_id, int(mat), float(radius)),
+                  "vpx_grid_emissive_sphere")
+
     def grid_checksum(self, grid_id=0):
         out = C.c_uint64()
         self._chk(self.lib.vpx_grid_checksum(self.h, grid_id, C.byref(out)), "vpx_grid_checksum")

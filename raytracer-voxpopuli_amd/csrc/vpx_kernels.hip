@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -193,6 +194,70 @@ __global__ void build_up_k(const uint64_t* __restrict__ child, uint32_t np, uint
             for (uint32_t j = 0; j < 64; ++j) m |= (c[j] != 0ull ? 1ull : 0ull) << j;
         }
         out[s] = m;
+    }
+}
+
+// Region rebuild after an edit: the l1 words of bricks [b0, b0 + cnt) (per axis), then
+// the l2 / l3 words of their parents.  Same words as build_l1_k / build_up_k compute.
+__global__ void build_l1_box_k(const uint8_t* __restrict__ cells, uint32_t n, uint32_t nb2, uint64_t* __restrict__ l1,
+                               uint32_t bx0, uint32_t by0, uint32_t bz0, uint32_t cx, uint32_t cy, uint32_t cz) {
+    const uint64_t total = (uint64_t)cx * cy * cz;
+    const uint64_t n64 = n;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t bx = bx0 + (uint32_t)(i % cx), by = by0 + (uint32_t)((i / cx) % cy),
+                       bz = bz0 + (uint32_t)(i / ((uint64_t)cx * cy));
+        uint64_t m = 0;
+        for (uint32_t lz = 0; lz < 4; ++lz)
+            for (uint32_t ly = 0; ly < 4; ++ly) {
+                const uint32_t y = by * 4 + ly, z = bz * 4 + lz;
+                if (y >= n || z >= n) continue;
+                const uint8_t* row = cells + (uint64_t)y * n64 + (uint64_t)z * n64 * n64;
+                for (uint32_t lx = 0; lx < 4; ++lx) {
+                    const uint32_t x = bx * 4 + lx;
+                    if (x < n && row[x] != kNone) m |= 1ull << (lx + 4 * ly + 16 * lz);
+                }
+            }
+        l1[skip::blk_index(bx, by, bz, nb2)] = m;
+    }
+}
+
+__global__ void build_up_box_k(const uint64_t* __restrict__ child, uint32_t np, uint32_t ngp, uint64_t* __restrict__ out,
+                               uint32_t px0, uint32_t py0, uint32_t pz0, uint32_t cx, uint32_t cy, uint32_t cz) {
+    const uint64_t total = (uint64_t)cx * cy * cz;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t px = px0 + (uint32_t)(i % cx), py = py0 + (uint32_t)((i / cx) % cy),
+                       pz = pz0 + (uint32_t)(i / ((uint64_t)cx * cy));
+        const uint64_t* c = child + (((uint64_t)pz * np + py) * np + px) * 64;
+        uint64_t m = 0;
+        for (uint32_t j = 0; j < 64; ++j) m |= (c[j] != 0ull ? 1ull : 0ull) << j;
+        out[ngp ? skip::blk_index(px, py, pz, ngp) : (uint32_t)(((uint64_t)pz * np + py) * np + px)] = m;
+    }
+}
+
+// Scatter a staged box (x fastest) into the grid.
+__global__ void write_box_k(uint8_t* __restrict__ grid, uint32_t n, const uint8_t* __restrict__ src, uint32_t x0,
+                            uint32_t y0, uint32_t z0, uint32_t dx, uint32_t dy, uint32_t dz) {
+    const uint64_t total = (uint64_t)dx * dy * dz;
+    const uint64_t n64 = n;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t x = i % dx, y = (i / dx) % dy, z = i / ((uint64_t)dx * dy);
+        grid[(x0 + x) + (y0 + y) * n64 + (z0 + z) * n64 * n64] = src[i];
+    }
+}
+
+// Scene::CreateEmmisiveSphere (template/scene.cpp:685-711) over the sphere's bounding box:
+// point = float3(x, y, z), d = length(float3(worldsize / 2) - point) (sqrtf of the
+// left-to-right dot), set when d < radius.
+__global__ void emissive_sphere_k(uint8_t* __restrict__ grid, uint32_t n, uint8_t mat, float radius, uint32_t x0,
+                                  uint32_t cnt) {
+    const uint64_t total = (uint64_t)cnt * cnt * cnt;
+    const uint64_t n64 = n;
+    const float c = (float)n / 2.0f;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t x = x0 + (uint32_t)(i % cnt), y = x0 + (uint32_t)((i / cnt) % cnt), z = x0 + (uint32_t)(i / ((uint64_t)cnt * cnt));
+        const float vx = c - (float)x, vy = c - (float)y, vz = c - (float)z;
+        const float d = sqrtf(vx * vx + vy * vy + vz * vz);
+        if (d < radius) grid[x + y * n64 + z * n64 * n64] = mat;
     }
 }
 
@@ -596,6 +661,79 @@ static int build_masks(vpx_ctx* c, uint32_t id) {
     VPX_HIP(c, hipGetLastError());
     VPX_HIP(c, hipStreamSynchronize(c->stream));
     return VPX_OK;
+}
+
+// Refresh the occupancy levels for the cells [x0, x1) x [y0, y1) x [z0, z1) only.
+static int build_masks_box(vpx_ctx* c, uint32_t id, uint32_t x0, uint32_t y0, uint32_t z0, uint32_t x1, uint32_t y1,
+                           uint32_t z1) {
+    auto& g = c->grids[id];
+    if (x0 >= x1 || y0 >= y1 || z0 >= z1) return VPX_OK;
+    uint32_t lo[3] = {x0 >> 2, y0 >> 2, z0 >> 2}, hi[3] = {(x1 - 1) >> 2, (y1 - 1) >> 2, (z1 - 1) >> 2};
+    auto blocks = [](uint64_t a, uint64_t b, uint64_t cc) { return (unsigned)std::min<uint64_t>(4096, (a * b * cc + 255) / 256); };
+    hipLaunchKernelGGL(build_l1_box_k, dim3(blocks(hi[0] - lo[0] + 1, hi[1] - lo[1] + 1, hi[2] - lo[2] + 1)), dim3(256), 0,
+                       c->stream, g.ptr, g.n, g.nb2, g.l1, lo[0], lo[1], lo[2], hi[0] - lo[0] + 1, hi[1] - lo[1] + 1,
+                       hi[2] - lo[2] + 1);
+    VPX_HIP(c, hipGetLastError());
+    for (int k = 0; k < 3; ++k) lo[k] >>= 2, hi[k] >>= 2;  // macros
+    hipLaunchKernelGGL(build_up_box_k, dim3(blocks(hi[0] - lo[0] + 1, hi[1] - lo[1] + 1, hi[2] - lo[2] + 1)), dim3(256), 0,
+                       c->stream, g.l1, g.nb2, g.nb3, g.l2, lo[0], lo[1], lo[2], hi[0] - lo[0] + 1, hi[1] - lo[1] + 1,
+                       hi[2] - lo[2] + 1);
+    VPX_HIP(c, hipGetLastError());
+    for (int k = 0; k < 3; ++k) lo[k] >>= 2, hi[k] >>= 2;  // supers
+    hipLaunchKernelGGL(build_up_box_k, dim3(blocks(hi[0] - lo[0] + 1, hi[1] - lo[1] + 1, hi[2] - lo[2] + 1)), dim3(256), 0,
+                       c->stream, g.l2, g.nb3, 0u, g.l3, lo[0], lo[1], lo[2], hi[0] - lo[0] + 1, hi[1] - lo[1] + 1,
+                       hi[2] - lo[2] + 1);
+    VPX_HIP(c, hipGetLastError());
+    VPX_HIP(c, hipStreamSynchronize(c->stream));
+    return VPX_OK;
+}
+
+int vpx_grid_fill(vpx_ctx* c, uint32_t id, uint8_t value) {
+    if (!c) return VPX_E_INVALID;
+    if (id >= c->grids.size() || !c->grids[id].ptr) return fail(c, VPX_E_INVALID, "unknown grid");
+    auto& g = c->grids[id];
+    VPX_HIP(c, hipMemsetAsync(g.ptr, value, (size_t)g.n * g.n * g.n, c->stream));
+    return build_masks(c, id);
+}
+
+int vpx_grid_write_box(vpx_ctx* c, uint32_t id, const uint8_t* src, uint32_t x0, uint32_t y0, uint32_t z0,
+                       uint32_t dx, uint32_t dy, uint32_t dz) {
+    if (!c || !src) return fail(c, VPX_E_INVALID, "null argument");
+    if (id >= c->grids.size() || !c->grids[id].ptr) return fail(c, VPX_E_INVALID, "unknown grid");
+    auto& g = c->grids[id];
+    if ((uint64_t)x0 + dx > g.n || (uint64_t)y0 + dy > g.n || (uint64_t)z0 + dz > g.n)
+        return fail(c, VPX_E_INVALID, "box outside the grid");
+    const size_t bytes = (size_t)dx * dy * dz;
+    if (!bytes) return VPX_OK;
+    uint8_t* d = nullptr;
+    VPX_HIP(c, hipMalloc(&d, bytes));
+    if (hipMemcpyAsync(d, src, bytes, hipMemcpyHostToDevice, c->stream) != hipSuccess) {
+        (void)hipFree(d);
+        return fail(c, VPX_E_DEVICE, "box upload failed");
+    }
+    hipLaunchKernelGGL(write_box_k, dim3((unsigned)std::min<size_t>(4096, (bytes + 255) / 256)), dim3(256), 0, c->stream,
+                       g.ptr, g.n, d, x0, y0, z0, dx, dy, dz);
+    const hipError_t e = hipStreamSynchronize(c->stream);
+    (void)hipFree(d);
+    if (e != hipSuccess) return fail(c, VPX_E_DEVICE, hipGetErrorString(e));
+    return build_masks_box(c, id, x0, y0, z0, x0 + dx, y0 + dy, z0 + dz);
+}
+
+int vpx_grid_emissive_sphere(vpx_ctx* c, uint32_t id, uint8_t mat, float radius) {
+    if (!c) return VPX_E_INVALID;
+    if (id >= c->grids.size() || !c->grids[id].ptr) return fail(c, VPX_E_INVALID, "unknown grid");
+    auto& g = c->grids[id];
+    if (!(radius > 0.0f)) return VPX_OK;  // no cell has length < radius <= 0 (NaN: none either)
+    // cells with |c - x| < radius per axis, c = n/2: a conservative integer box
+    const double cc = g.n / 2.0, r = std::min<double>(radius, 4.0 * g.n);
+    const int64_t a = std::max<int64_t>(0, (int64_t)std::floor(cc - r) - 1);
+    const int64_t b = std::min<int64_t>((int64_t)g.n - 1, (int64_t)std::ceil(cc + r) + 1);
+    if (b < a) return VPX_OK;
+    const uint32_t x0 = (uint32_t)a, cnt = (uint32_t)(b - a + 1);
+    hipLaunchKernelGGL(emissive_sphere_k, dim3((unsigned)std::min<uint64_t>(4096, ((uint64_t)cnt * cnt * cnt + 255) / 256)),
+                       dim3(256), 0, c->stream, g.ptr, g.n, mat, radius, x0, cnt);
+    VPX_HIP(c, hipGetLastError());
+    return build_masks_box(c, id, x0, x0, x0, x0 + cnt, x0 + cnt, x0 + cnt);
 }
 
 int vpx_upload_grid(vpx_ctx* c, uint32_t id, const uint8_t* cells, uint32_t n) {

@@ -58,10 +58,34 @@ def load_model_grid(size, voxels, n, scale_model=(1.0, 1.0, 1.0)):
     gz = (yy.astype(np.float32) * scl[2]).astype(np.int64)
     ok = (gx >= 0) & (gy >= 0) & (gz >= 0) & (gx < n) & (gy < n) & (gz < n)
     idx = gx[ok] + gy[ok] * n + gz[ok] * n * n
-    # later voxels (z-major, then y, then x) overwrite earlier ones, as the loop does
+    # later voxels (z-major, then y, then x) overwrite earlier ones, as the loop does:
+    # keep the last occurrence of every target cell explicitly
     order = np.lexsort((xx[ok], yy[ok], zz[ok]))
-    grid[idx[order]] = vals[ok][order]
+    tgt, val = idx[order], vals[ok][order]
+    _, last = np.unique(tgt[::-1], return_index=True)
+    keep = len(tgt) - 1 - last
+    grid[tgt[keep]] = val[keep]
     return grid
+
+
+def load_model_partial(size, voxels, n, columns, thickness, scale_model=(1.0, 1.0, 1.0)):
+    """Scene::LoadModelPartial (template/scene.cpp:531-604), as ModifyingProp::Update calls
+    it every 0.9 s (src/Game/ModifyingProp.cpp:11-21): ResetGrid() to NONE, LoadModel's
+    mapping, only voxels with x in [columns - thickness, columns + thickness] (uint32
+    arithmetic: the lower bound wraps when thickness > columns).  Returns (grid, box)
+    where box = (x0, y0, z0, x1, y1, z1) bounds the non-NONE cells (None if empty) —
+    the dirty region to upload after a device-side ResetGrid."""
+    sx = int(size[0])
+    v = np.asarray(voxels, np.uint8).reshape(int(size[2]), int(size[1]), sx).copy()
+    lo, hi = (int(columns) - int(thickness)) % (1 << 32), int(columns) + int(thickness)
+    keep = (np.arange(sx) >= lo) & (np.arange(sx) <= hi)
+    v[:, :, ~keep] = 0
+    grid = load_model_grid(size, v.reshape(-1), n, scale_model)
+    nz = np.nonzero(grid.reshape(n, n, n) != NONE)
+    if len(nz[0]) == 0:
+        return grid, None
+    z, y, x = nz
+    return grid, (int(x.min()), int(y.min()), int(z.min()), int(x.max()) + 1, int(y.max()) + 1, int(z.max()) + 1)
 
 
 def default_materials():

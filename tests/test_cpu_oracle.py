@@ -258,3 +258,45 @@ def test_default_materials_table(pkg):
     assert tuple(m[8].albedo) == (1.0, 0.5, 1.0) and m[8].ior == np.float32(1.45)
     assert [m[i].emissive for i in range(9, 15)] == [3, 8, 12, 15, 16, 22]
     assert m[15].emissive == 5 and m[2].roughness == np.float32(0.25) and m[100].roughness == 1.0
+
+
+# ------------------------------------------------------ world edits
+@pytest.mark.parametrize("name,n,columns,thickness", [("monu3", 64, 20, 3), ("monu3", 64, 2, 5), ("monu3", 32, 40, 8),
+                                                      ("roomGlass", 128, 60, 10), ("teapot", 128, 0, 0)])
+def test_load_model_partial_two_restatements(pkg, orc, name, n, columns, thickness):
+    """scene.load_model_partial (numpy) == oracle_load_model_partial (C), incl. the uint32
+    wrap of columns - thickness and LoadModel's downscale; the returned box bounds every
+    placed voxel."""
+    size, vox, _ = pkg.scene.load_model(name)
+    a, box = pkg.scene.load_model_partial(size, vox, n, columns, thickness)
+    lib = orc._lib(pkg.abi)
+    b = np.empty(n ** 3, np.uint8)
+    one = (C.c_float * 3)(1, 1, 1)
+    lib.oracle_load_model_partial(np.ascontiguousarray(vox).ctypes.data, int(size[0]), int(size[1]), int(size[2]), n,
+                                  one, columns, thickness, b.ctypes.data)
+    assert np.array_equal(a, b)
+    g = a.reshape(n, n, n)
+    if box is None:
+        assert np.all(g == 255)
+    else:
+        x0, y0, z0, x1, y1, z1 = box
+        inside = np.zeros_like(g, bool)
+        inside[z0:z1, y0:y1, x0:x1] = True
+        assert np.all(g[~inside] == 255) and np.any(g[inside] != 255)
+    if columns < thickness:  # lower bound wraps: nothing is kept
+        assert box is None
+
+
+@pytest.mark.parametrize("n,radius", [(40, 7.5), (41, 12.0), (32, 0.5), (24, 100.0)])
+def test_emissive_sphere_restatement(orc, pkg, n, radius):
+    """oracle_emissive_sphere == an independent float32 numpy evaluation of
+    Scene::CreateEmmisiveSphere (length(float3(worldsize/2) - point) < radius)."""
+    lib = orc._lib(pkg.abi)
+    g = np.full(n ** 3, 255, np.uint8)
+    lib.oracle_emissive_sphere(g.ctypes.data, n, 15, radius)
+    z, y, x = np.meshgrid(np.arange(n), np.arange(n), np.arange(n), indexing="ij")
+    c = np.float32(n) / np.float32(2)
+    vx, vy, vz = (c - a.astype(np.float32) for a in (x, y, z))
+    d = np.sqrt(((vx * vx) + (vy * vy)) + (vz * vz)).astype(np.float32)
+    want = np.where(d < np.float32(radius), 15, 255).astype(np.uint8).reshape(-1)
+    assert np.array_equal(g, want)
