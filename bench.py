@@ -110,17 +110,25 @@ def run(args):
     n = args.gpus
     if world != n:
         raise SystemExit(f"--gpus {n} but WORLD_SIZE={world}")
-    torch.cuda.set_device(local)
+    # VPX_BENCH_SHARED_DEVICE=1 rehearses the N-rank flow on ONE GPU (every rank on device 0,
+    # gloo collectives through host copies) — for checking the sharded path on a 1-GPU box;
+    # real multi-GPU runs use one GPU per rank and RCCL ("nccl").
+    shared = os.environ.get("VPX_BENCH_SHARED_DEVICE") == "1"
+    dev = 0 if shared else local
+    torch.cuda.set_device(dev)
     dist = None
     if n > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if shared:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
     desc = pkg.scene.CONFIGS[args.config]()
     W, H = weak_size(n, (desc.width, desc.height))
     desc = build_scene(pkg, args.config, W, H)
     stream = torch.cuda.Stream()  # a real stream: the kernel and its HIP events share it
     torch.cuda.set_stream(stream)
-    ctx = pkg.context.Context(local)
+    ctx = pkg.context.Context(dev)
     ctx.set_stream(stream.cuda_stream)
     ctx.load_scene(desc)
     torch.cuda.synchronize()
@@ -129,8 +137,8 @@ def run(args):
     if n > 1:
         L = ctx.packed_len(W, H, n)
         packed = torch.zeros(L * 4, dtype=torch.float32, device="cuda")
-        gathered = [torch.empty_like(packed) for _ in range(n)] if rank == 0 else None
         gbuf = torch.empty(n * L * 4, dtype=torch.float32, device="cuda") if rank == 0 else None
+        gathered = list(gbuf.view(n, L * 4)) if rank == 0 else None  # gather straight into gbuf
 
     frame = [0]
     ev = []
@@ -149,9 +157,15 @@ def run(args):
             ctx.render_tiles(p, rank, n, packed.data_ptr())
             if record:
                 e1.record(stream)
-            dist.gather(packed, gathered, dst=0)
+            if shared:
+                stream.synchronize()
+                parts = [torch.empty(L * 4) for _ in range(n)] if rank == 0 else None
+                dist.gather(packed.cpu(), parts, dst=0)
+                if rank == 0:
+                    gbuf.copy_(torch.cat(parts))
+            else:
+                dist.gather(packed, gathered, dst=0)
             if rank == 0:
-                torch.cat(gathered, out=gbuf)
                 ctx.composite_tiles(p, n, gbuf.data_ptr(), acc.data_ptr(), rgb.data_ptr())
         if record:
             ev.append((e0, e1))
@@ -178,7 +192,7 @@ def run(args):
     st = ctx.counters()
     local_rays = float(st.primary_rays + st.shadow_rays)
     vals = torch.tensor([elapsed, local_rays, float(st.primary_rays), float(st.shadow_rays), float(st.dda_cells),
-                         float(np.mean(ks))], dtype=torch.float64, device="cuda")
+                         float(np.mean(ks))], dtype=torch.float64, device="cpu" if shared else "cuda")
     if dist:
         mx = vals.clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
@@ -217,7 +231,9 @@ def run(args):
             "config": {"workload": f"{args.config}: {W}x{H}, {desc.grids[0].n}^3 {desc.name}, 1 spp, "
                                    f"Trace depth {desc.max_bounces} (primary+shadow)",
                        "width": W, "height": H, "world_n": desc.grids[0].n, "max_bounces": desc.max_bounces,
-                       "spp": 1, "parallelism": "single GPU" if n == 1 else f"tile-shard x{n} + RCCL gather to rank 0"},
+                       "spp": 1, "parallelism": "single GPU" if n == 1 else (
+                           f"tile-shard x{n} + RCCL gather to rank 0" if not shared
+                           else f"REHEARSAL: {n} ranks sharing one GPU, gloo gather via host")},
             "rays_per_step": {"primary": prim / K, "shadow": shad / K, "dda_cells": cells / K},
             "mpix_per_s": round(prim / elapsed / 1e6, 3),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
