@@ -287,6 +287,9 @@ __device__ __forceinline__ skip::Walk to_walk(const Dda& s) {
 #ifndef VPX_SKIPW_NEAREST
 #define VPX_SKIPW_NEAREST 2
 #endif
+#ifndef VPX_SKIPW_BOUNCE
+#define VPX_SKIPW_BOUNCE 2
+#endif
 #ifndef VPX_SKIPW_SHADOW
 #define VPX_SKIPW_SHADOW 4
 #endif
@@ -547,6 +550,7 @@ struct Counters {
 
 // Renderer::FindNearest, renderer.cpp:946-1018.  Linear loop over the volumes with the
 // SSE transforms; a later volume wins only with a strictly smaller t (ties -> lowest index).
+template <uint32_t SKIPW = VPX_SKIPW_NEAREST>
 __device__ __forceinline__ int32_t find_nearest(const SceneView& sv, Ray& r, Counters& k) {
     int32_t vox = -2;
     ++k.nearest;
@@ -560,7 +564,7 @@ __device__ __forceinline__ int32_t find_nearest(const SceneView& sv, Ray& r, Cou
         Dda s;
         if (!dda_setup(vol, g.n, o, s)) continue;
         skip::Walk w = to_walk(s);
-        if (walk_wave<VPX_LEAN_NEAREST != 0, 0, VPX_SKIPW_NEAREST>(grid_view(g), w, r.t, k.cells)) {
+        if (walk_wave<VPX_LEAN_NEAREST != 0, 0, SKIPW>(grid_view(g), w, r.t, k.cells)) {
             r.t = w.t;
             r.N = normal_voxel(o, w.t, g.n, vol.matrix);
             r.mat = g.cells[(uint64_t)w.X + (uint64_t)w.Y * g.n + (uint64_t)w.Z * ((uint64_t)g.n * g.n)];
