@@ -249,6 +249,26 @@ int vpx_composite_tiles(vpx_ctx* ctx, const vpx_frame_params* params, uint32_t t
                         uint32_t tile_h, uint32_t n_ranks, const float* gathered,
                         float* accum, uint32_t* rgb8);
 
+/* ---- static-camera path ------------------------------------ */
+/* Renderer::prevCamera as CopyToPrevCamera leaves it (renderer.cpp:1893-1902): position
+   and the four frustum-plane normals of Camera::SetFrustumNormals (camera.h:53-66). */
+typedef struct vpx_prev_camera {
+    float cam_pos[3];
+    float left_normal[3];
+    float right_normal[3];
+    float top_normal[3];
+    float bottom_normal[3];
+    float pad;
+} vpx_prev_camera;  /* 64 bytes */
+/* One frame of Renderer::Tick's static branch (renderer.cpp:1996-2101): TraceReproject
+   (renderer.cpp:1330-1585) of Camera::GetPrimaryRayNoDOF per pixel (AA / DOF flags are
+   ignored), then per pixel PointToUV into `prev`, IsOccludedPrevFrame, SampleHistory,
+   ClampHistory, the material weight, lerp, ApplyReinhardJodie, RGB8.  `history`
+   (float4[W*H], DEVICE) is illuminationHistoryBuffer: read, then replaced by this frame's
+   illumination (tempIlluminationBuffer).  `rgb8` DEVICE uint32[W*H] (may be NULL). */
+int vpx_render_reproject(vpx_ctx* ctx, const vpx_frame_params* params, const vpx_prev_camera* prev,
+                         float* history, uint32_t* rgb8, vpx_stats* stats);
+
 /* Work counters accumulated on device over every render call since the last reset
    (no per-frame synchronisation); kernel_ms/total_ms are not filled here.            */
 int vpx_get_counters(vpx_ctx* ctx, vpx_stats* out, int reset);
@@ -290,6 +310,10 @@ int vpx_camera_look_at(const float pos[3], const float target[3], uint32_t width
 /* Scene::SetCubeBoundaries + Scene::SetTransform (scene.cpp:213-217, 373-405). */
 int vpx_volume_set_transform(const float position[3], const float scale[3],
                              const float rotation[3], vpx_volume* out);
+/* Camera::HandleInput(0) basis + SetFrustumNormals + CopyToPrevCamera
+   (camera.h:53-66, 113-181; renderer.cpp:710-711, 1893-1902). */
+int vpx_prev_camera_look_at(const float pos[3], const float target[3], uint32_t width, uint32_t height,
+                            vpx_prev_camera* out);
 /* Renderer::MaterialSetUp table, padded to 256 entries (renderer.cpp:357-443). */
 int vpx_default_materials(vpx_material* out256);
 /* Per-pixel xorshift32 state used by vpx_render: 0x12345678 + WangHash((k+1)*17),

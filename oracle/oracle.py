@@ -29,6 +29,8 @@ def _lib(abi):
                                  C.c_void_p, P(abi.Stats)]
     lib.oracle_render_pixels.argtypes = [C.c_void_p, P(abi.FrameParams), C.c_void_p, C.c_uint32, C.c_void_p,
                                          P(abi.Stats), C.c_int]
+    lib.oracle_render_reproject.argtypes = [C.c_void_p, P(abi.FrameParams), P(abi.PrevCamera), C.c_void_p,
+                                            C.c_void_p, P(abi.Stats), C.c_int]
     lib.oracle_render.argtypes = [C.c_void_p, P(abi.FrameParams), C.c_void_p, C.c_void_p, P(abi.Stats), C.c_int]
     lib.oracle_accumulate_tonemap.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p]
     lib.oracle_accumulate_tonemap.restype = None
@@ -168,6 +170,14 @@ class Oracle:
         assert self.lib.oracle_render(self.ptr, C.byref(params), acc.ctypes.data, rgb.ctypes.data, C.byref(st),
                                       threads) == 0
         return acc, rgb, st
+
+    def render_reproject(self, params, prev, history, threads=0):
+        """One static-camera frame; history float32[H*W, 4] updated in place."""
+        rgb = np.zeros(params.width * params.height, np.uint32)
+        st = self.abi.Stats()
+        assert self.lib.oracle_render_reproject(self.ptr, C.byref(params), C.byref(prev), history.ctypes.data,
+                                                rgb.ctypes.data, C.byref(st), threads) == 0
+        return rgb, st
 
     def focus_distance(self, width, height):
         return self.lib.oracle_focus_distance(self.ptr, width, height)

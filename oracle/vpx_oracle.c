@@ -1093,6 +1093,303 @@ int oracle_render(const oracle_scene* sc, const vpx_frame_params* p, float* accu
     return run_jobs(sc, p, NULL, p->width * p->height, NULL, accum, rgb8, stats, threads);
 }
 
+/* ------------------------------------------------- static-camera path -- */
+typedef struct { v3 albedo, illum; } aidata; /* AlbedoIlluminationData, renderer.h:10-19 */
+static inline v3 ai_color(aidata a) { return vmul(a.albedo, a.illum); } /* GetColor */
+
+/* Renderer::TraceReproject and its helpers, renderer.cpp:1330-1585 (SampleSkyReproject
+   :2328-2333 with activateSky == false returns {sky, 1}). */
+static aidata trace_reproject(tctx* c, ray_t* r, int depth)
+{
+    aidata out;
+    if (depth < 0) {
+        out.albedo = V3(0, 0, 0), out.illum = V3(0, 0, 0);
+        return out;
+    }
+    const int32_t vox = renderer_find_nearest(c, r);
+    if (r->mat == NONE_MAT) {
+        out.albedo = V3(c->sky[0], c->sky[1], c->sky[2]), out.illum = V3(1, 1, 1);
+        return out;
+    }
+    const vpx_material* mat = &c->sc->materials[r->mat];
+    switch (r->mat) {
+    case 5: case 6: case 7: { /* TraceMetal :1330-1340 */
+        const v3 refl = reflect(r->D, r->N);
+        const v3 o = offset_ray(ray_point(r), r->N);
+        const v3 d = vadd(refl, vmuls(random_sphere_sample(c), mat->roughness));
+        ray_t nr = make_ray(o, d);
+        out.illum = ai_color(trace_reproject(c, &nr, depth - 1));
+        out.albedo = albedo_of(c, r->mat);
+        return out;
+    }
+    case 0: case 1: case 2: case 3: case 4: { /* TraceNonMetal :1342-1357 */
+        const v3 rdir = vadd(r->N, random_sphere_sample(c)); /* RandomLambertianReflectionVector */
+        const v3 inc = illumination(c, r);
+        ray_t nr = make_ray(offset_ray(ray_point(r), r->N), rdir);
+        v3 il = V3(0, 0, 0);
+        il = vadd(il, inc);
+        il = vadd(il, ai_color(trace_reproject(c, &nr, depth - 1)));
+        out.albedo = albedo_of(c, r->mat), out.illum = il;
+        return out;
+    }
+    case VPX_MAT_GLASS: { /* TraceDialectric :1359-1421 */
+        v3 color = V3(1, 1, 1);
+        int in_glass = r->inside;
+        const float ior = mat->ior;
+        const float ratio = in_glass ? ior : 1.0f / ior;
+        int inside_volume = 1;
+        if (in_glass) {
+            color = albedo_of(c, r->mat);
+            if (vox >= 0) inside_volume = exit_march(c, r, vox, 0);
+        }
+        if (!inside_volume) {
+            r->O = vadd(r->O, vmuls(r->D, r->t));
+            r->t = 0;
+        }
+        const float cos_t = smin(vdot(vneg(r->D), r->N), 1.0f);
+        const float sin_t = sqrtf(1.0f - cos_t * cos_t);
+        const int cannot = ratio * sin_t > 1.0f;
+        v3 rdir, rn;
+        if (cannot || schlick(cos_t, ratio) > rf(c)) {
+            rdir = reflect(r->D, r->N);
+            rn = r->N;
+        } else {
+            rdir = refract(r->D, r->N, ratio);
+            in_glass = !in_glass;
+            rn = vneg(r->N);
+        }
+        ray_t nr = make_ray(offset_ray(ray_point(r), rn), rdir);
+        nr.inside = in_glass;
+        out.albedo = color, out.illum = ai_color(trace_reproject(c, &nr, depth - 1));
+        return out;
+    }
+    case 9: case 10: case 11: case 12: case 13: case 14: { /* TraceSmoke :1423-1494 */
+        v3 color = V3(1, 1, 1);
+        int in_glass = r->inside;
+        int inside_volume = 1;
+        float intensity = 0, dist = 0;
+        if (vox == 0) (void)illumination(c, r); /* player probe: only the inLight flag uses it */
+        if (in_glass) {
+            intensity = mat->emissive;
+            color = albedo_of(c, r->mat);
+            if (vox >= 0) inside_volume = exit_march(c, r, vox, 1);
+            dist = r->t;
+        }
+        const float threshold = rf(c) * 100 - intensity;
+        if (rf(c) * dist > threshold) {
+            const float lo = r->t * .45f, hi = r->t;
+            const float tt = lo + rf(c) * (hi - lo);
+            r->O = vadd(r->O, vmuls(r->D, tt));
+            r->D = random_direction(c);
+            r->t = 0;
+        }
+        color = absorption(color, intensity, dist);
+        if (!inside_volume) {
+            r->O = vadd(r->O, vmuls(r->D, r->t));
+            r->t = 0;
+        }
+        const v3 rdir = refract(r->D, r->N, 1.0f);
+        in_glass = !in_glass;
+        ray_t nr = make_ray(offset_ray(ray_point(r), vneg(r->N)), rdir);
+        nr.inside = in_glass;
+        out.albedo = color, out.illum = ai_color(trace_reproject(c, &nr, depth - 1));
+        return out;
+    }
+    case VPX_MAT_EMISSIVE: /* TraceEmmision :1496-1499 */
+        out.albedo = vmuls(albedo_of(c, r->mat), mat->emissive), out.illum = V3(1, 1, 1);
+        return out;
+    default: { /* TraceModelMaterials :1501-1511 */
+        const v3 rdir = diffuse_reflection(c, r->N);
+        const v3 inc = illumination(c, r);
+        ray_t nr = make_ray(offset_ray(ray_point(r), r->N), rdir);
+        v3 il = inc;
+        il = vadd(il, ai_color(trace_reproject(c, &nr, depth - 1)));
+        out.albedo = albedo_of(c, r->mat), out.illum = il;
+        return out;
+    }
+    }
+}
+
+static inline v3 ycocg(v3 c) /* RGBToYCoCg, renderer.cpp:833-839 */
+{
+    const float k = 0.5f * 256.0f / 255.0f;
+    return V3(vdot(c, V3(1, 2, 1)) * 0.25f, vdot(c, V3(2, 0, -2)) * 0.25f + k, vdot(c, V3(-1, 2, -1)) * 0.25f + k);
+}
+static inline v3 ycocg_rgb(v3 c) /* YCoCgToRGB, renderer.cpp:842-851 */
+{
+    const float k = 0.5f * 256.0f / 255.0f;
+    const float co = c.y - k, cg = c.z - k;
+    return V3(c.x + co - cg, c.x + cg, c.x - co - cg);
+}
+static inline int on_screen(int x, int y, uint32_t W, uint32_t H) /* IsValidScreen(float2) */
+{
+    return (float)x >= 0.0f && (float)x < (float)W && (float)y >= 0.0f && (float)y < (float)H;
+}
+
+typedef struct {
+    const oracle_scene* sc;
+    const vpx_frame_params* p;
+    const vpx_prev_camera* prev;
+    float *alb, *ill, *rd, *hist, *temp;
+    uint32_t* rgb8;
+    int pass;
+    uint32_t tid, nthreads;
+    uint64_t shadow, nearest, cells;
+} rjob_t;
+
+static void* reproject_worker(void* arg)
+{
+    rjob_t* j = (rjob_t*)arg;
+    const fpstate fs = fp_enter();
+    tctx c;
+    tctx_init(&c, j->sc);
+    c.sky[0] = j->p->sky[0], c.sky[1] = j->p->sky[1], c.sky[2] = j->p->sky[2];
+    c.area_samples = j->p->area_samples;
+    const uint32_t W = j->p->width, H = j->p->height;
+    const vpx_camera* cam = &j->sc->camera;
+    for (uint32_t i = j->tid; i < W * H; i += j->nthreads) {
+        const uint32_t x = i % W, y = i / W;
+        if (j->pass == 0) { /* Tick static branch, first loop (renderer.cpp:2001-2022) */
+            c.rng = oracle_pixel_seed(j->p->seed_base, j->p->frame_index, W, H, x, y);
+            const float u = (float)x * (1.0f / (float)W), v = (float)y * (1.0f / (float)H);
+            const v3 tl = v3f(cam->top_left), tr = v3f(cam->top_right), bl = v3f(cam->bottom_left);
+            const v3 P = vadd(vadd(tl, vmuls(vsub(tr, tl), u)), vmuls(vsub(bl, tl), v));
+            const v3 cp = v3f(cam->cam_pos);
+            ray_t r = make_ray(cp, vsub(P, cp)); /* GetPrimaryRayNoDOF */
+            const aidata d = trace_reproject(&c, &r, j->p->max_bounces);
+            const v3 ip = ray_point(&r); /* RayDataReproject::GetRayInfo */
+            float* a = j->alb + 4 * (uint64_t)i;
+            float* l = j->ill + 4 * (uint64_t)i;
+            float* q = j->rd + 4 * (uint64_t)i;
+            a[0] = d.albedo.x, a[1] = d.albedo.y, a[2] = d.albedo.z, a[3] = 0;
+            l[0] = d.illum.x, l[1] = d.illum.y, l[2] = d.illum.z, l[3] = 0;
+            q[0] = ip.x, q[1] = ip.y, q[2] = ip.z, q[3] = u2f_bits(r.mat);
+            continue;
+        }
+        /* second loop (renderer.cpp:2024-2098) */
+        const float* q = j->rd + 4 * (uint64_t)i;
+        const v3 P = V3(q[0], q[1], q[2]);
+        const uint32_t mt = f2u_bits(q[3]);
+        const v3 ns = v3f(j->ill + 4 * (uint64_t)i);
+        v3 fin = ns;
+        const v3 pc = v3f(j->prev->cam_pos);
+        const v3 delta = vsub(P, pc); /* Camera::PointToUV, camera.h:33-49 */
+        const float ld = vdot(v3f(j->prev->left_normal), delta), rdd = vdot(v3f(j->prev->right_normal), delta);
+        const float td = vdot(v3f(j->prev->top_normal), delta), bd = vdot(v3f(j->prev->bottom_normal), delta);
+        const float hw = 1.0f / (float)W / 2.0f, hh = 1.0f / (float)H / 2.0f; /* HALF_PIXEL_W/H */
+        const float uu = ld / (ld + rdd) + hw, vv = td / (td + bd) + hh;
+        int use = uu >= 0.0f && uu < 1.0f && vv >= 0.0f && vv < 1.0f; /* IsValid */
+        if (use) { /* IsOccludedPrevFrame, renderer.cpp:767-774 */
+            const v3 dn = vnormalize(vsub(P, pc));
+            const v3 pos = offset_ray(P, vneg(dn));
+            ray_t occ = make_ray(pc, dn);
+            occ.t = vlength(vsub(pos, pc));
+            if (shadow_occluded(&c, &occ)) use = 0;
+        }
+        if (use) {
+            /* SampleHistory, renderer.cpp:777-830 */
+            const float ux = uu - hw, uy = vv - hh;
+            const float ptx = ux * (float)W, pty = uy * (float)H;
+            const int tlx = f2i_trunc(ptx), tly = f2i_trunc(pty);
+            const float fx = ptx - (float)tlx, fy = pty - (float)tly;
+            const float gx = 1 - fx, gy = 1 - fy;
+            const int v1 = on_screen(tlx, tly, W, H), v2 = on_screen(tlx + 1, tly, W, H);
+            const int v3_ = on_screen(tlx, tly + 1, W, H), v4 = on_screen(tlx + 1, tly + 1, W, H);
+            float w1 = v1 ? gx * gy : 0.0f, w2 = v2 ? fx * gy : 0.0f, w3 = v3_ ? gx * fy : 0.0f, w4 = v4 ? fx * fy : 0.0f;
+            const float tw = w1 + w2 + w3 + w4;
+            const float rtw = 1.0f / tw;
+            w1 *= rtw, w2 *= rtw, w3 *= rtw, w4 *= rtw;
+            v3 hs = V3(0, 0, 0);
+            if (v1) hs = vadd(hs, vmuls(v3f(j->hist + 4 * ((uint64_t)tly * W + tlx)), w1));
+            if (v2) hs = vadd(hs, vmuls(v3f(j->hist + 4 * ((uint64_t)tly * W + tlx + 1)), w2));
+            if (v3_) hs = vadd(hs, vmuls(v3f(j->hist + 4 * ((uint64_t)(tly + 1) * W + tlx)), w3));
+            if (v4) hs = vadd(hs, vmuls(v3f(j->hist + 4 * ((uint64_t)(tly + 1) * W + tlx + 1)), w4));
+            /* ClampHistory, renderer.cpp:856-910 */
+            const v3 nsy = ycocg(ns);
+            v3 hy = ycocg(hs);
+            uint32_t nvalid = 1;
+            v3 avg = nsy, var = vmul(nsy, nsy);
+            static const int ox[8] = {-1, 0, 1, -1, 1, -1, 0, 1}, oy[8] = {-1, -1, -1, 0, 0, 1, 1, 1};
+            for (int k = 0; k < 8; k++) {
+                const int qx = (int)x + ox[k], qy = (int)y + oy[k];
+                if (on_screen(qx, qy, W, H)) {
+                    const v3 fe = ycocg(v3f(j->ill + 4 * ((uint64_t)qx + (uint64_t)qy * W)));
+                    avg = vadd(avg, fe);
+                    var = vadd(var, vmul(fe, fe));
+                    nvalid++;
+                }
+            }
+            const float inv = 1.0f / (float)nvalid;
+            avg = vmuls(avg, inv), var = vmuls(var, inv);
+            const v3 sg = V3(sqrtf(smax(0.0f, var.x - avg.x * avg.x)), sqrtf(smax(0.0f, var.y - avg.y * avg.y)),
+                             sqrtf(smax(0.0f, var.z - avg.z * avg.z)));
+            const v3 lo = vsub(avg, vmuls(sg, 0.75f)), hi = vadd(avg, vmuls(sg, 0.75f));
+            hy = V3(fmaxf(lo.x, fminf(hy.x, hi.x)), fmaxf(lo.y, fminf(hy.y, hi.y)), fmaxf(lo.z, fminf(hy.z, hi.z)));
+            v3 hr = ycocg_rgb(hy);
+            hr = V3(fmaxf(hr.x, 0.0f), fmaxf(hr.y, 0.0f), fmaxf(hr.z, 0.0f));
+            float wt = 0.9f; /* material weights, renderer.cpp:2050-2088 */
+            if (mt <= 4) wt = 0.8f;
+            else if (mt <= 7) wt = 0.5f;
+            else if (mt == VPX_MAT_GLASS) wt = 0.5f;
+            else if (mt == VPX_MAT_EMISSIVE) wt = 0.0f;
+            fin = vadd(ns, vmuls(vsub(hr, ns), wt)); /* lerp, tmpl8math.h:2220-2223 */
+        }
+        float* t = j->temp + 4 * (uint64_t)i;
+        t[0] = fin.x, t[1] = fin.y, t[2] = fin.z, t[3] = 0;
+        if (j->rgb8) {
+            const v3 col = vmul(v3f(j->alb + 4 * (uint64_t)i), fin);
+            const float px[4] = {col.x, col.y, col.z, 0.0f};
+            j->rgb8[i] = tonemap_pack(px);
+        }
+    }
+    j->shadow = c.shadow_rays, j->nearest = c.nearest_calls, j->cells = c.dda_cells;
+    fp_leave(fs);
+    return NULL;
+}
+
+int oracle_render_reproject(const oracle_scene* sc, const vpx_frame_params* p, const vpx_prev_camera* prev,
+                            float* history, uint32_t* rgb8, vpx_stats* stats, int threads)
+{
+    if (!sc || !p || !prev || !history) return VPX_E_INVALID;
+    const uint64_t npx = (uint64_t)p->width * p->height;
+    float* buf = (float*)malloc(sizeof(float) * 4 * 4 * npx);
+    if (!buf) return VPX_E_NOMEM;
+    if (threads <= 0) {
+        const long hc = sysconf(_SC_NPROCESSORS_ONLN);
+        threads = hc > 0 ? (int)hc : 1;
+    }
+    if (threads > 256) threads = 256;
+    rjob_t jobs[256];
+    pthread_t th[256];
+    if (stats) memset(stats, 0, sizeof(*stats));
+    for (int pass = 0; pass < 2; pass++) {
+        for (int t = 0; t < threads; t++)
+            jobs[t] = (rjob_t){sc, p, prev, buf, buf + 4 * npx, buf + 8 * npx, history, buf + 12 * npx, rgb8,
+                               pass, (uint32_t)t, (uint32_t)threads, 0, 0, 0};
+        int started = 0;
+        for (int t = 1; t < threads; t++) {
+            if (pthread_create(&th[t], NULL, reproject_worker, &jobs[t]) != 0) break;
+            started = t;
+        }
+        for (int t = started + 1; t < threads; t++) reproject_worker(&jobs[t]);
+        reproject_worker(&jobs[0]);
+        for (int t = 1; t <= started; t++) pthread_join(th[t], NULL);
+        if (stats)
+            for (int t = 0; t < threads; t++) {
+                stats->shadow_rays += jobs[t].shadow;
+                stats->bounce_rays += jobs[t].nearest;
+                stats->dda_cells += jobs[t].cells;
+            }
+    }
+    if (stats) {
+        stats->primary_rays = npx;
+        stats->bounce_rays -= p->max_bounces >= 0 ? npx : 0;
+    }
+    memcpy(history, buf + 12 * npx, sizeof(float) * 4 * npx); /* illuminationHistoryBuffer = temp */
+    free(buf);
+    return VPX_OK;
+}
+
 /* Focus ray of Renderer::Tick (renderer.cpp:1987-1991): GetPrimaryRay(W/2, H/2) with DOF
    jitter is not applied here (integer centre, circle drawn from the thread RNG in the
    reference); the ray is tested against every Scene in WORLD space (reference quirk). */

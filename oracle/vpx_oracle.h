@@ -98,6 +98,12 @@ void oracle_offset_ray(const float p[3], const float n[3], float out[3]);
 float oracle_cube_intersect(const float b0[3], const float b1[3], const float o[3],
                             const float d[3], const float rd[3]);
 
+/* Static-camera path: one frame of Renderer::Tick's static branch
+   (renderer.cpp:1996-2101) — TraceReproject per pixel, reprojection into `prev`, history
+   blend.  history: float4[W*H] in/out (illuminationHistoryBuffer); rgb8 may be NULL. */
+int oracle_render_reproject(const oracle_scene* sc, const vpx_frame_params* p, const vpx_prev_camera* prev,
+                            float* history, uint32_t* rgb8, vpx_stats* stats, int threads);
+
 /* World edits: Scene::LoadModelPartial / CreateEmmisiveSphere. */
 void oracle_load_model_partial(const uint8_t* vox, uint32_t sx, uint32_t sy, uint32_t sz, uint32_t n,
                                const float scale_model[3], uint32_t columns, uint32_t thickness, uint8_t* out);

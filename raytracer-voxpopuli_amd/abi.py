@@ -85,13 +85,18 @@ class Stats(C.Structure):
         return {k: getattr(self, k) for k, _ in self._fields_}
 
 
+class PrevCamera(C.Structure):
+    _fields_ = [("cam_pos", f3), ("left_normal", f3), ("right_normal", f3), ("top_normal", f3),
+                ("bottom_normal", f3), ("pad", C.c_float)]
+
+
 class Profile(C.Structure):
     _fields_ = [("stage_ms", C.c_float * 8), ("stage_launches", C.c_uint32 * 8), ("stage_cells", C.c_uint64 * 8)]
 
 
 STAGES = ("primary", "shade", "shadow", "resolve", "bounce", "finish")
 
-STRUCT_SIZES = {Profile: 128, Volume: 160, Material: 32, PointLight: 24, SpotLight: 40, AreaLight: 32, DirLight: 24,
+STRUCT_SIZES = {PrevCamera: 64, Profile: 128, Volume: 160, Material: 32, PointLight: 24, SpotLight: 40, AreaLight: 32, DirLight: 24,
                 Sphere: 32, Triangle: 64, Camera: 80, FrameParams: 48, Ray: 32, Hit: 32, Stats: 40}
 
 
@@ -135,6 +140,10 @@ SIGNATURES = {
     "vpx_grid_fill": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint8]),
     "vpx_grid_write_box": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p] + [C.c_uint32] * 6),
     "vpx_grid_emissive_sphere": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint8, C.c_float]),
+    "vpx_render_reproject": (C.c_int, [C.c_void_p, C.POINTER(FrameParams), C.POINTER(PrevCamera), C.c_void_p,
+                                       C.c_void_p, C.POINTER(Stats)]),
+    "vpx_prev_camera_look_at": (C.c_int, [C.POINTER(C.c_float), C.POINTER(C.c_float), C.c_uint32, C.c_uint32,
+                                          C.POINTER(PrevCamera)]),
     "vpx_profile_enable": (C.c_int, [C.c_void_p, C.c_uint32]),
     "vpx_profile_read": (C.c_int, [C.c_void_p, C.POINTER(Profile), C.c_int]),
     "vpx_find_nearest": (C.c_int, [C.c_void_p, C.POINTER(Ray), C.c_uint32, C.POINTER(Hit)]),

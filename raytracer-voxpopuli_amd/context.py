@@ -96,6 +96,15 @@ class Context:
                                       C.byref(st) if st is not None else None), "vpx_render")
         return st
 
+    def render_reproject(self, params, prev, history_ptr, rgb_ptr=None, stats=False):
+        """One frame of the static-camera path (vpx_render_reproject); history is a DEVICE
+        float4[W*H] pointer (illuminationHistoryBuffer, updated in place)."""
+        st = abi.Stats() if stats else None
+        self._chk(self.lib.vpx_render_reproject(self.h, C.byref(params), C.byref(prev), C.c_void_p(history_ptr),
+                                                C.c_void_p(rgb_ptr or 0), C.byref(st) if st is not None else None),
+                  "vpx_render_reproject")
+        return st
+
     def render_tiles(self, params, rank, n_ranks, packed_ptr, stats=False, tile=16):
         st = abi.Stats() if stats else None
         self._chk(self.lib.vpx_render_tiles(self.h, C.byref(params), tile, tile, rank, n_ranks,

@@ -130,16 +130,13 @@ mat4 to_matrix(const quat& q) {
 extern "C" {
 
 // Camera basis as Camera::HandleInput(0) leaves it with no key held (camera.h:113-181).
-int vpx_camera_look_at(const float pos[3], const float target[3], uint32_t width, uint32_t height,
-                       vpx_camera* out) {
-    if (!pos || !target || !out || !width || !height) return VPX_E_INVALID;
-    const v3 cam = {pos[0], pos[1], pos[2]};
+static void look_at_basis(const float pos[3], const float target[3], v3& cam, v3& ahead, v3& right, v3& up) {
+    cam = {pos[0], pos[1], pos[2]};
     v3 tgt = {target[0], target[1], target[2]};
     const v3 tmp_up = {0, 1, 0};
-    const float aspect = (float)width / (float)height;  // ASPECT, camera.h:183
-    v3 ahead = normalize(sub(tgt, cam));
-    v3 right = normalize(cross(tmp_up, ahead));
-    v3 up = normalize(cross(ahead, right));
+    ahead = normalize(sub(tgt, cam));
+    right = normalize(cross(tmp_up, ahead));
+    up = normalize(cross(ahead, right));
     ahead = normalize(sub(tgt, cam));
     right = normalize(cross(tmp_up, ahead));
     up = normalize(cross(ahead, right));
@@ -147,6 +144,14 @@ int vpx_camera_look_at(const float pos[3], const float target[3], uint32_t width
     ahead = normalize(sub(tgt, cam));
     up = normalize(cross(ahead, right));
     right = normalize(cross(up, ahead));
+}
+
+int vpx_camera_look_at(const float pos[3], const float target[3], uint32_t width, uint32_t height,
+                       vpx_camera* out) {
+    if (!pos || !target || !out || !width || !height) return VPX_E_INVALID;
+    v3 cam, ahead, right, up;
+    look_at_basis(pos, target, cam, ahead, right, up);
+    const float aspect = (float)width / (float)height;  // ASPECT, camera.h:183
     const v3 base = add(cam, mul(ahead, 2.0f));
     put(out->cam_pos, cam);
     put(out->top_left, add(sub(base, mul(right, aspect)), up));
@@ -156,6 +161,24 @@ int vpx_camera_look_at(const float pos[3], const float target[3], uint32_t width
     put(out->up, up);
     out->focal_distance = 1.0f;  // Camera::focalDistance default, camera.h:189
     out->defocus_jitter = 2.0f;  // Camera::defocusJitter default, camera.h:191
+    return VPX_OK;
+}
+
+int vpx_prev_camera_look_at(const float pos[3], const float target[3], uint32_t width, uint32_t height,
+                            vpx_prev_camera* out) {
+    if (!pos || !target || !out || !width || !height) return VPX_E_INVALID;
+    v3 cam, ahead, right, up;
+    look_at_basis(pos, target, cam, ahead, right, up);
+    const float aspect = (float)width / (float)height;
+    const v3 a2 = mul(ahead, 2.0f);  // 2 * ahead
+    const v3 lf = sub(a2, mul(right, aspect)), rf = add(a2, mul(right, aspect));
+    const v3 tf = add(a2, up), bf = sub(a2, up);
+    std::memset(out, 0, sizeof(*out));
+    put(out->cam_pos, cam);
+    put(out->left_normal, cross(up, lf));
+    put(out->right_normal, cross(rf, up));
+    put(out->top_normal, cross(right, tf));
+    put(out->bottom_normal, cross(bf, right));
     return VPX_OK;
 }
 
@@ -225,6 +248,7 @@ static_assert(sizeof(vpx_volume) == 160, "vpx_volume layout");
 static_assert(sizeof(vpx_material) == 32, "vpx_material layout");
 static_assert(sizeof(vpx_point_light) == 24 && sizeof(vpx_spot_light) == 40, "light layout");
 static_assert(sizeof(vpx_profile) == 128, "vpx_profile layout");
+static_assert(sizeof(vpx_prev_camera) == 64, "vpx_prev_camera layout");
 static_assert(sizeof(vpx_area_light) == 32 && sizeof(vpx_dir_light) == 24, "light layout");
 static_assert(sizeof(vpx_sphere) == 32 && sizeof(vpx_triangle) == 64, "shape layout");
 static_assert(sizeof(vpx_camera) == 80 && sizeof(vpx_frame_params) == 48, "camera/frame layout");

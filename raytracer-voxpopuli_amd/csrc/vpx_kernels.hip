@@ -320,6 +320,9 @@ struct vpx_ctx {
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
     // wavefront path state (vpx_wavefront.hpp), grown on demand
     void* d_wave = nullptr;
+    // static-camera path images (float4[W*H] each): albedo, illumination, ray data, temp
+    float4* rp_buf = nullptr;
+    size_t rp_pixels = 0;
     size_t wave_bytes = 0;
     WaveBufs wave{};
 };
@@ -498,15 +501,21 @@ static void prof_mark(vpx_ctx* c, int stage) {
 
 // The frame: primary -> [shade -> shadow -> resolve -> nearest]* -> finish, all on
 // c->stream, one 256-thread workgroup per 16x16 tile in every kernel.
+struct Reproj {  // the static-camera tail (vpx_render_reproject)
+    PrevCam prev;
+    float4 *alb, *ill, *rd, *temp, *hist;
+};
+
 template <bool PACKED>
 int launch_render(vpx_ctx* c, const SceneView& sv, const FrameArgs& f, uint32_t tiles, float4* accum, uint32_t* rgb8,
-                  float4* packed) {
+                  float4* packed, const Reproj* rp = nullptr) {
     const uint32_t P = tiles * (uint32_t)kTilePix;
     const uint32_t L = (uint32_t)std::max(1, f.max_bounces + 1);
     const uint32_t S = (uint32_t)std::max(1, sv.area_samples);
     int rc = ensure_wave(c, P, L, S);
     if (rc) return rc;
-    const WaveBufs w = c->wave;
+    WaveBufs w = c->wave;
+    if (rp) w.RD = rp->rd;
     const dim3 grid(tiles), block(kThreads);
     const size_t slds = sizeof(uint32_t) * S * kThreads * kGroupTiles;
     const dim3 ggrid((tiles + kGroupTiles - 1) / kGroupTiles);
@@ -530,7 +539,17 @@ int launch_render(vpx_ctx* c, const SceneView& sv, const FrameArgs& f, uint32_t 
         }
     }
     prof_mark(c, VPX_STAGE_FINISH);
-    hipLaunchKernelGGL((k_finish<PACKED>), grid, block, 0, c->stream, f, w, accum, rgb8, packed);
+    if (!rp) {
+        hipLaunchKernelGGL((k_finish<PACKED>), grid, block, 0, c->stream, f, w, accum, rgb8, packed);
+    } else {  // Renderer::Tick static branch, second pass (renderer.cpp:2024-2100)
+        hipLaunchKernelGGL(k_finish_reproject, grid, block, 0, c->stream, f, w, rp->alb, rp->ill);
+        hipLaunchKernelGGL(k_reproject_setup, grid, block, 0, c->stream, f, w, rp->prev);
+        hipLaunchKernelGGL(k_shadow_tile, ggrid, block, slds, c->stream, sv, w, c->d_ctr);
+        hipLaunchKernelGGL(k_reproject_resolve, grid, block, 0, c->stream, f, w, rp->alb, rp->ill, rp->hist, rp->temp,
+                           rgb8);
+        VPX_HIP(c, hipMemcpyAsync(rp->hist, rp->temp, sizeof(float4) * (size_t)f.width * f.height,
+                                  hipMemcpyDeviceToDevice, c->stream));  // history = temp
+    }
     prof_mark(c, -1);
     VPX_HIP(c, hipGetLastError());
     return VPX_OK;
@@ -600,6 +619,7 @@ int vpx_destroy(vpx_ctx* c) {
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (hipEvent_t e : c->prof_ev) (void)hipEventDestroy(e);
+    if (c->rp_buf) (void)hipFree(c->rp_buf);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->ev2) (void)hipEventDestroy(c->ev2);
@@ -850,6 +870,49 @@ int vpx_render(vpx_ctx* c, const vpx_frame_params* p, float* accum, uint32_t* rg
     const FrameArgs f = frame_of(c, p, 0, 1);
     if (stats) VPX_HIP(c, hipEventRecord(c->ev0, c->stream));
     if ((rc = launch_render<false>(c, sv, f, f.num_tiles, reinterpret_cast<float4*>(accum), rgb8, nullptr))) return rc;
+    if (stats) {
+        VPX_HIP(c, hipEventRecord(c->ev1, c->stream));
+        unsigned long long after[kCtrWords];
+        if ((rc = snapshot_counters(c, after))) return rc;
+        std::memset(stats, 0, sizeof(*stats));
+        fill_stats(stats, before, after);
+        float ms = 0.f;
+        VPX_HIP(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
+        stats->kernel_ms = ms;
+        stats->total_ms = ms;
+    }
+    return VPX_OK;
+}
+
+int vpx_render_reproject(vpx_ctx* c, const vpx_frame_params* p, const vpx_prev_camera* prev, float* history,
+                         uint32_t* rgb8, vpx_stats* stats) {
+    if (!c) return VPX_E_INVALID;
+    int rc = validate_frame(c, p);
+    if (rc) return rc;
+    if (!prev || !history) return fail(c, VPX_E_INVALID, "prev camera and history (device float4[W*H]) are required");
+    VPX_HIP(c, hipSetDevice(c->device));
+    const size_t pix = (size_t)p->width * p->height;
+    if (pix > c->rp_pixels) {
+        VPX_HIP(c, hipStreamSynchronize(c->stream));
+        if (c->rp_buf) (void)hipFree(c->rp_buf);
+        c->rp_buf = nullptr;
+        c->rp_pixels = 0;
+        VPX_HIP(c, hipMalloc(&c->rp_buf, sizeof(float4) * 4 * pix));
+        c->rp_pixels = pix;
+    }
+    Reproj rp;
+    auto h3 = [](const float* v) { return f3{v[0], v[1], v[2]}; };
+    rp.prev = PrevCam{h3(prev->cam_pos), h3(prev->left_normal), h3(prev->right_normal), h3(prev->top_normal),
+                      h3(prev->bottom_normal)};
+    rp.alb = c->rp_buf, rp.ill = c->rp_buf + pix, rp.rd = c->rp_buf + 2 * pix, rp.temp = c->rp_buf + 3 * pix;
+    rp.hist = reinterpret_cast<float4*>(history);
+    unsigned long long before[kCtrWords] = {};
+    if (stats && (rc = snapshot_counters(c, before))) return rc;
+    const SceneView sv = view_of(c, p->sky, p->area_samples);
+    FrameArgs f = frame_of(c, p, 0, 1);
+    f.flags = (f.flags & ~(VPX_FLAG_AA | VPX_FLAG_DOF)) | kFlagReproject;  // GetPrimaryRayNoDOF
+    if (stats) VPX_HIP(c, hipEventRecord(c->ev0, c->stream));
+    if ((rc = launch_render<false>(c, sv, f, f.num_tiles, nullptr, rgb8, nullptr, &rp))) return rc;
     if (stats) {
         VPX_HIP(c, hipEventRecord(c->ev1, c->stream));
         unsigned long long after[kCtrWords];

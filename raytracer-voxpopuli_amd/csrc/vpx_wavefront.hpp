@@ -30,6 +30,12 @@ constexpr uint32_t kInside = 2u;
 constexpr uint32_t kSlotValid = 1u;
 constexpr uint32_t kSlotDiscard = 2u;  // smoke player probe: traced for the count, result unused
 
+// internal frame flag: the static-camera path (Renderer::TraceReproject + reprojection)
+constexpr uint32_t kFlagReproject = 0x80000000u;
+// pending-light bit: the level adds its light to a zero first (TraceNonMetal's
+// `illumination{0}; illumination += incLight`, renderer.cpp:1343-1357)
+constexpr uint32_t kPendZeroAdd = 1u << 13;
+
 // light kinds of a level's pending incLight
 constexpr uint32_t kLightNone = 0, kLightSingle = 1, kLightArea = 2;
 
@@ -63,6 +69,7 @@ struct WaveBufs {
     float4* SL;    // [S][P] unoccluded contribution of the slot
     float4* SM;    // [P] pending light: xyz = kd (area), w = bits(kind | discard<<3 | count<<4 | level<<8 | lc<<16)
     uint32_t* smask;  // [P] shadow slots emitted this level (bit s = slot s)
+    float4* RD;    // [W*H] reprojection: level-0 intersection point, w = material bits (image order)
     uint32_t P;    // paths (pixels) this call
     uint32_t S;    // shadow slots per path
 };
@@ -262,6 +269,13 @@ __global__ __launch_bounds__(256) void k_shade(SceneView sv, FrameArgs f, WaveBu
             ray.N = mk(hh.y, hh.z, hh.w);
             ray.mat = hm & 0xffu;
             ray.inside = (hm & 0x80000000u) != 0u;
+            if ((f.flags & kFlagReproject) && level == 0) {  // RayDataReproject::GetRayInfo (renderer.h:31-34)
+                uint32_t x, y;
+                if (path_pixel(f, p, x, y)) {
+                    const f3 ip = ray_point(ray);
+                    w.RD[(uint64_t)y * f.width + x] = make_float4(ip.x, ip.y, ip.z, __uint_as_float(ray.mat));
+                }
+            }
             const int32_t vox = (int32_t)((hm >> 8) & 0xffffu) - 2;
             Rng g{__float_as_uint(oo.w)};
             int depth = w.depth[p];
@@ -288,6 +302,15 @@ __global__ __launch_bounds__(256) void k_shade(SceneView sv, FrameArgs f, WaveBu
                     next = make_ray(o, refl + random_sphere_sample(g) * mat.roughness);
                     a = albedo(sv, m);
                     form = kFormMul;
+                } else if (m <= VPX_MAT_NON_METAL_PINK && (f.flags & kFlagReproject)) {
+                    // TraceNonMetal (renderer.cpp:1343-1357): no Schlick branch; Lambertian
+                    // direction first, then Illumination; albedo * ((0 + incLight) + child)
+                    const f3 rdir = ray.N + random_sphere_sample(g);
+                    pending = emit_illumination(sv, ray, g, w, p, false, kd, slots);
+                    if (pending) pending |= kPendZeroAdd;
+                    next = make_ray(offset_ray(ray_point(ray), ray.N), rdir);
+                    a = albedo(sv, m);
+                    form = kFormAddMul;
                 } else if (m <= VPX_MAT_NON_METAL_PINK) {  // :1117-1144
                     if (g.next() > schlick_nonmetal(dot(-ray.D, ray.N))) {
                         const f3 rdir = ray.N + random_sphere_sample(g);
@@ -423,6 +446,7 @@ __global__ __launch_bounds__(256) void k_resolve(SceneView sv, WaveBufs w) {
     f3 inc = acc;
     if (kind == kLightArea) inc = (acc / (float)sv.area_samples) * mk(sm.x, sm.y, sm.z);
     inc = inc * (float)lc;
+    if (pend & kPendZeroAdd) inc = mk(0.f, 0.f, 0.f) + inc;
     w.LB[(uint64_t)lvl * w.P + p] = make_float4(inc.x, inc.y, inc.z, 0.f);
 }
 
@@ -686,6 +710,188 @@ __global__ __launch_bounds__(256) void k_finish(FrameArgs f, WaveBufs w, float4*
             accum[px] = a;
             if (rgb8) rgb8[px] = tonemap_pack(a);
         }
+    }
+}
+
+// ------------------------------------------------------ static-camera reprojection
+// Renderer::Tick's static branch (renderer.cpp:1996-2101): TraceReproject per pixel
+// (albedo and illumination kept apart at the top level), then per pixel: reproject the
+// level-0 intersection into the previous camera, test it against the scene from the
+// previous camera position, sample the illumination history bilinearly, clamp it to the
+// YCoCg neighbourhood box of the new samples, blend by material, tonemap.
+
+struct PrevCam {  // vpx_prev_camera
+    f3 pos, left, right, top, bottom;
+};
+
+// Top level of TraceReproject from the path's records: (albedo, illumination).
+__global__ __launch_bounds__(256) void k_finish_reproject(FrameArgs f, WaveBufs w, float4* __restrict__ alb,
+                                                          float4* __restrict__ ill) {
+    const uint32_t p = blockIdx.x * 256u + threadIdx.x;
+    if (p >= w.P) return;
+    uint32_t x, y;
+    if (!path_pixel(f, p, x, y)) return;
+    const uint64_t px = (uint64_t)y * f.width + x;
+    f3 A = mk(0.f, 0.f, 0.f), I = mk(0.f, 0.f, 0.f);  // TraceReproject(ray, depth < 0) = {0, 0}
+    if (f.max_bounces < 0) {
+        // the ray never reaches FindNearest: GetRayInfo sees t = 1e34, NONE (renderer.cpp:2020)
+        const float4 o = w.O[p], d = w.D[p];
+        const f3 ip = mk(o.x, o.y, o.z) + mk(d.x, d.y, d.z) * kBig;
+        w.RD[px] = make_float4(ip.x, ip.y, ip.z, __uint_as_float(kNone));
+    } else {
+        const float4 lf = w.leaf[p];
+        f3 v = mk(lf.x, lf.y, lf.z);
+        const uint32_t forms = w.forms[p];
+        const int nl = (int)(forms >> 27);
+        if (nl == 0) {  // sky / emissive at the top: {colour, 1} (renderer.cpp:1333, 2330-2333)
+            A = v;
+            I = mk(1.f, 1.f, 1.f);
+        } else {
+            for (int i = nl - 1; i >= 1; --i) {  // children's GetColor() bottom-up
+                const uint32_t form = (forms >> (2 * i)) & 3u;
+                const uint64_t li = (uint64_t)i * w.P + p;
+                const float4 a4 = w.LA[li];
+                const f3 a = mk(a4.x, a4.y, a4.z);
+                if (form == kFormAddMul) {
+                    const float4 b4 = w.LB[li];
+                    v = (v + mk(b4.x, b4.y, b4.z)) * a;
+                } else {
+                    v = v * a;
+                }
+            }
+            const float4 a4 = w.LA[p];
+            A = mk(a4.x, a4.y, a4.z);
+            if ((forms & 3u) == kFormAddMul) {
+                const float4 b4 = w.LB[p];
+                I = v + mk(b4.x, b4.y, b4.z);
+            } else {
+                I = v;
+            }
+        }
+    }
+    alb[px] = make_float4(A.x, A.y, A.z, 0.f);
+    ill[px] = make_float4(I.x, I.y, I.z, 0.f);
+}
+
+// Camera::PointToUV (camera.h:33-49) + the half-pixel offset; IsValid (renderer.cpp:1635-1638);
+// IsOccludedPrevFrame's ray (renderer.cpp:767-774) into shadow slot 0.
+__global__ __launch_bounds__(256) void k_reproject_setup(FrameArgs f, WaveBufs w, PrevCam pc) {
+    const uint32_t p = blockIdx.x * 256u + threadIdx.x;
+    if (p >= w.P) return;
+    uint32_t x, y;
+    uint32_t slots = 0;
+    w.SM[p] = make_float4(0.f, 0.f, 0.f, __uint_as_float(0u));
+    if (path_pixel(f, p, x, y)) {
+        const float4 rd = w.RD[(uint64_t)y * f.width + x];
+        const f3 P = mk(rd.x, rd.y, rd.z);
+        const f3 delta = P - pc.pos;
+        const float ld = dot(pc.left, delta), rdist = dot(pc.right, delta);
+        const float td = dot(pc.top, delta), bd = dot(pc.bottom, delta);
+        const float u = ld / (ld + rdist), v = td / (td + bd);
+        const float hw = (1.0f / (float)f.width) / 2.0f, hh = (1.0f / (float)f.height) / 2.0f;
+        const float uu = u + hw, vv = v + hh;
+        const bool valid = uu >= 0.0f && uu < 1.0f && vv >= 0.0f && vv < 1.0f;
+        w.SM[p] = make_float4(uu, vv, 0.f, __uint_as_float(valid ? 1u : 0u));
+        if (valid) {
+            const f3 dn = normalize(P - pc.pos);
+            const f3 pos = offset_ray(P, -dn);
+            const Ray occ = make_ray(pc.pos, dn);  // Ray{camPos, dir, length(pos - camPos)}
+            put_slot(w, 0, p, occ.O, occ.D, length(pos - pc.pos), mk(0.f, 0.f, 0.f), kSlotValid);
+            slots = 1u;
+        }
+    }
+    w.smask[p] = slots;
+}
+
+__device__ __forceinline__ f3 ld4(const float4* a, uint64_t i) {
+    const float4 v = a[i];
+    return mk(v.x, v.y, v.z);
+}
+__device__ __forceinline__ f3 ycocg(f3 c) {  // RGBToYCoCg (renderer.cpp:833-839)
+    const float k = (0.5f * 256.0f) / 255.0f;
+    return mk(dot(c, mk(1.f, 2.f, 1.f)) * 0.25f, dot(c, mk(2.f, 0.f, -2.f)) * 0.25f + k,
+              dot(c, mk(-1.f, 2.f, -1.f)) * 0.25f + k);
+}
+__device__ __forceinline__ f3 ycocg_rgb(f3 c) {  // YCoCgToRGB (renderer.cpp:842-851)
+    const float k = (0.5f * 256.0f) / 255.0f;
+    const float co = c.y - k, cg = c.z - k;
+    return mk((c.x + co) - cg, c.x + cg, (c.x - co) - cg);
+}
+__device__ __forceinline__ float clampf_ref(float v, float a, float b) { return fmaxf(a, fminf(v, b)); }
+__device__ __forceinline__ bool on_screen(int x, int y, const FrameArgs& f) {  // IsValidScreen
+    return (float)x >= 0.0f && (float)x < (float)f.width && (float)y >= 0.0f && (float)y < (float)f.height;
+}
+
+// SampleHistory (renderer.cpp:777-830), ClampHistory (:856-910), the material weight and
+// lerp (renderer.cpp:2048-2090), ApplyReinhardJodie + RGBF32_to_RGB8.
+__global__ __launch_bounds__(256) void k_reproject_resolve(FrameArgs f, WaveBufs w, const float4* __restrict__ alb,
+                                                           const float4* __restrict__ ill,
+                                                           const float4* __restrict__ hist, float4* __restrict__ temp,
+                                                           uint32_t* __restrict__ rgb8) {
+    const uint32_t p = blockIdx.x * 256u + threadIdx.x;
+    if (p >= w.P) return;
+    uint32_t x, y;
+    if (!path_pixel(f, p, x, y)) return;
+    const uint64_t px = (uint64_t)y * f.width + x;
+    const f3 ns = ld4(ill, px);
+    f3 fin = ns;
+    const float4 uvv = w.SM[p];
+    const bool occluded = (__float_as_uint(w.SD[p].w) & 4u) != 0u;
+    if ((__float_as_uint(uvv.w) & 1u) && !occluded) {
+        // bilinear history
+        const float ux = uvv.x - (1.0f / (float)f.width) / 2.0f, uy = uvv.y - (1.0f / (float)f.height) / 2.0f;
+        const float ptx = ux * (float)f.width, pty = uy * (float)f.height;
+        const int tlx = trunc_i32(ptx), tly = trunc_i32(pty);
+        const float fx = ptx - (float)tlx, fy = pty - (float)tly;
+        const float gx = 1.0f - fx, gy = 1.0f - fy;
+        const bool v1 = on_screen(tlx, tly, f), v2 = on_screen(tlx + 1, tly, f), v3 = on_screen(tlx, tly + 1, f),
+                   v4 = on_screen(tlx + 1, tly + 1, f);
+        float w1 = v1 ? gx * gy : 0.0f, w2 = v2 ? fx * gy : 0.0f, w3 = v3 ? gx * fy : 0.0f, w4 = v4 ? fx * fy : 0.0f;
+        const float tw = ((w1 + w2) + w3) + w4;
+        const float rtw = 1.0f / tw;
+        w1 = w1 * rtw, w2 = w2 * rtw, w3 = w3 * rtw, w4 = w4 * rtw;
+        f3 hs = mk(0.f, 0.f, 0.f);
+        if (v1) hs = hs + ld4(hist, (uint64_t)tly * f.width + tlx) * w1;
+        if (v2) hs = hs + ld4(hist, (uint64_t)tly * f.width + (tlx + 1)) * w2;
+        if (v3) hs = hs + ld4(hist, (uint64_t)(tly + 1) * f.width + tlx) * w3;
+        if (v4) hs = hs + ld4(hist, (uint64_t)(tly + 1) * f.width + (tlx + 1)) * w4;
+        // neighbourhood clamp in YCoCg
+        const f3 nsy = ycocg(ns);
+        f3 hy = ycocg(hs);
+        uint32_t nvalid = 1;
+        f3 avg = nsy, var = nsy * nsy;
+        const int ox[8] = {-1, 0, 1, -1, 1, -1, 0, 1}, oy[8] = {-1, -1, -1, 0, 0, 1, 1, 1};
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int qx = (int)x + ox[i], qy = (int)y + oy[i];
+            if (on_screen(qx, qy, f)) {
+                const f3 fe = ycocg(ld4(ill, (uint64_t)qx + (uint64_t)qy * f.width));
+                avg = avg + fe;
+                var = var + fe * fe;
+                ++nvalid;
+            }
+        }
+        const float inv = 1.0f / (float)nvalid;
+        avg = avg * inv;
+        var = var * inv;
+        const f3 sg = mk(sqrtf(smax(0.0f, var.x - avg.x * avg.x)), sqrtf(smax(0.0f, var.y - avg.y * avg.y)),
+                         sqrtf(smax(0.0f, var.z - avg.z * avg.z)));
+        const f3 lo = avg - sg * 0.75f, hi = avg + sg * 0.75f;
+        hy = mk(clampf_ref(hy.x, lo.x, hi.x), clampf_ref(hy.y, lo.y, hi.y), clampf_ref(hy.z, lo.z, hi.z));
+        f3 hr = ycocg_rgb(hy);
+        hr = mk(fmaxf(hr.x, 0.0f), fmaxf(hr.y, 0.0f), fmaxf(hr.z, 0.0f));
+        const uint32_t mat = __float_as_uint(w.RD[px].w);
+        float wt = 0.9f;
+        if (mat <= VPX_MAT_NON_METAL_PINK) wt = 0.8f;
+        else if (mat <= VPX_MAT_METAL_LOW) wt = 0.5f;
+        else if (mat == VPX_MAT_GLASS) wt = 0.5f;
+        else if (mat == VPX_MAT_EMISSIVE) wt = 0.0f;
+        fin = ns + (hr - ns) * wt;  // lerp(a, b, t) = a + t * (b - a)
+    }
+    temp[px] = make_float4(fin.x, fin.y, fin.z, 0.f);
+    if (rgb8) {  // ApplyReinhardJodie(albedo * final) into a float4 with w = 0, RGBF32_to_RGB8
+        const f3 c = ld4(alb, px) * fin;
+        rgb8[px] = tonemap_pack(make_float4(c.x, c.y, c.z, 0.f));
     }
 }
 

@@ -23,6 +23,8 @@ class Renderer:
         self.antiAliasingStrength = scene.aa_strength     # renderer.h:185
         self.numCheckShadowsAreaLight = scene.area_samples  # renderer.h:205
         self.staticCamera = False
+        self.prevCamera = None             # renderer.h:182 (vpx_prev_camera)
+        self.illuminationHistory = None    # renderer.h:242, float4[W*H] in HBM
         self.accumulator = None
         self.screen = None
         self.last_stats = None
@@ -52,13 +54,34 @@ class Renderer:
         self.numRenderedFrames += 1
         return self.last_stats
 
+    def CopyToPrevCamera(self):  # renderer.cpp:1893-1902
+        from .scene import prev_camera
+        self.prevCamera = prev_camera(self.scene._cam_pos, self.scene._cam_target, self.scene.width, self.scene.height)
+
     def Tick(self, deltaTime=0.0, stats=False):
         if not self.staticCamera:
             if self.scene.flags & abi.VPX_FLAG_DOF:  # focus ray, renderer.cpp:1987-1991
                 self.scene.camera.focal_distance = self.ctx.focus_distance(self.scene.width, self.scene.height)
                 self.ctx.set_camera(self.scene.camera)
             return self.Update(stats=stats)
-        raise NotImplementedError("static-camera reprojection path is out of scope (SURVEY.md §8(f) rank 1)")
+        # static branch (renderer.cpp:1996-2101): TraceReproject + history reprojection
+        if self.prevCamera is None:
+            self.CopyToPrevCamera()
+        if self.illuminationHistory is None:
+            w, h = self.scene.width, self.scene.height
+            self.illuminationHistory = torch.zeros(w * h * 4, dtype=torch.float32, device=self.device)
+            torch.cuda.synchronize(self.device)  # allocated on torch's stream; the library uses its own
+        p = self.scene.frame_params(frame_index=self.numRenderedFrames)
+        p.max_bounces = self.maxBounces
+        p.area_samples = self.numCheckShadowsAreaLight
+        st = self.ctx.render_reproject(p, self.prevCamera, self.illuminationHistory.data_ptr(), self.screen.data_ptr(),
+                                       stats=stats)
+        self.numRenderedFrames += 1
+        return st
+
+    def history_host(self):
+        self.synchronize()
+        return self.illuminationHistory.cpu().numpy().reshape(self.scene.height, self.scene.width, 4)
 
     def synchronize(self):
         self.stream.synchronize()

@@ -223,6 +223,16 @@ def look_at(pos, target, width, height):
     return cam
 
 
+def prev_camera(pos, target, width, height):
+    """Renderer::prevCamera after CopyToPrevCamera (renderer.cpp:710-711, 1893-1902)."""
+    lib = abi.load_library()
+    pc = abi.PrevCamera()
+    p = (C.c_float * 3)(*pos)
+    t = (C.c_float * 3)(*target)
+    abi.check(lib, None, lib.vpx_prev_camera_look_at(p, t, width, height, C.byref(pc)), "vpx_prev_camera_look_at")
+    return pc
+
+
 def volume(position=(0.0, 0.0, 0.0), scale=(1.0, 1.0, 1.0), rotation=(0.0, 0.0, 0.0), grid_id=0):
     lib = abi.load_library()
     v = abi.Volume()
