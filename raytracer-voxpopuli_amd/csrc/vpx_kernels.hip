@@ -173,21 +173,16 @@ __global__ void build_l1_k(const uint8_t* __restrict__ cells, uint32_t n, uint32
 }
 
 // One level up: the word of parent block P (np parents per axis, linear P) ORs the 64
-// consecutive child words child[P*64 + j] into bit j.  Output blocked by grandparent
-// (ngp per axis, words ngp^3 * 64) or linear (ngp == 0, words np^3).
+// consecutive child words child[P*64 + j] into bit j (child words are fresh cell masks).
+// Output blocked by grandparent (ngp per axis, words ngp^3 * 64).
 __global__ void build_up_k(const uint64_t* __restrict__ child, uint32_t np, uint32_t ngp, uint64_t* __restrict__ out) {
-    const uint64_t total = ngp ? (uint64_t)ngp * ngp * ngp * 64 : (uint64_t)np * np * np;
+    const uint64_t total = (uint64_t)ngp * ngp * ngp * 64;
     for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < total; s += (uint64_t)gridDim.x * blockDim.x) {
-        uint32_t px, py, pz;
-        if (ngp) {
-            const uint64_t gp = s >> 6;
-            const uint32_t j = (uint32_t)(s & 63u);
-            px = (uint32_t)(gp % ngp) * 4 + (j & 3u);
-            py = (uint32_t)((gp / ngp) % ngp) * 4 + ((j >> 2) & 3u);
-            pz = (uint32_t)(gp / ((uint64_t)ngp * ngp)) * 4 + (j >> 4);
-        } else {
-            px = (uint32_t)(s % np), py = (uint32_t)((s / np) % np), pz = (uint32_t)(s / ((uint64_t)np * np));
-        }
+        const uint64_t gp = s >> 6;
+        const uint32_t j = (uint32_t)(s & 63u);
+        const uint32_t px = (uint32_t)(gp % ngp) * 4 + (j & 3u);
+        const uint32_t py = (uint32_t)((gp / ngp) % ngp) * 4 + ((j >> 2) & 3u);
+        const uint32_t pz = (uint32_t)(gp / ((uint64_t)ngp * ngp)) * 4 + (j >> 4);
         uint64_t m = 0;
         if (px < np && py < np && pz < np) {
             const uint64_t* c = child + (((uint64_t)pz * np + py) * np + px) * 64;
@@ -230,8 +225,30 @@ __global__ void build_up_box_k(const uint64_t* __restrict__ child, uint32_t np, 
         const uint64_t* c = child + (((uint64_t)pz * np + py) * np + px) * 64;
         uint64_t m = 0;
         for (uint32_t j = 0; j < 64; ++j) m |= (c[j] != 0ull ? 1ull : 0ull) << j;
-        out[ngp ? skip::blk_index(px, py, pz, ngp) : (uint32_t)(((uint64_t)pz * np + py) * np + px)] = m;
+        out[skip::blk_index(px, py, pz, ngp)] = m;
     }
+}
+
+// One plane fx + fy + fz = s of the distance-field sweep (build_df), thread = (fx, fy,
+// octant o); (fx, fy, fz) are brick coordinates flipped so that octant o's "ahead" is +1.
+// Reads bytes o of the words on planes s+1..s+3 (earlier launches), writes plane s.
+__global__ void df_plane_k(uint8_t* __restrict__ l1b, const uint64_t* __restrict__ l2, uint32_t nb1, uint32_t nb2,
+                           uint32_t nb3, uint32_t s) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t o = (uint32_t)(t & 7u);
+    const uint64_t q = t >> 3;
+    const uint32_t fx = (uint32_t)(q % nb1), fy = (uint32_t)(q / nb1);
+    if (fy >= nb1 || fx + fy > s || s - fx - fy >= nb1) return;
+    const uint32_t fz = s - fx - fy;
+    const uint32_t x = (o & 1u) ? nb1 - 1u - fx : fx, y = (o & 2u) ? nb1 - 1u - fy : fy, z = (o & 4u) ? nb1 - 1u - fz : fz;
+    auto occ = [&](uint32_t a, uint32_t b, uint32_t c) -> bool {
+        return (l2[skip::blk_index(a >> 2, b >> 2, c >> 2, nb3)] >> ((a & 3u) | ((b & 3u) << 2) | ((c & 3u) << 4))) & 1ull;
+    };
+    if (occ(x, y, z)) return;
+    auto get = [&](uint32_t a, uint32_t b, uint32_t c, uint32_t oo) -> uint32_t {
+        return l1b[(size_t)skip::blk_index(a, b, c, nb2) * 8 + oo];
+    };
+    l1b[(size_t)skip::blk_index(x, y, z, nb2) * 8 + o] = skip::df_value(x, y, z, o, nb1, occ, get);
 }
 
 // Scatter a staged box (x fastest) into the grid.
@@ -290,7 +307,6 @@ struct vpx_ctx {
         uint8_t* ptr = nullptr;
         uint64_t* l1 = nullptr;
         uint64_t* l2 = nullptr;
-        uint64_t* l3 = nullptr;
         uint32_t n = 0, nb1 = 0, nb2 = 0, nb3 = 0;
     };
     std::vector<GridBuf> grids;
@@ -386,7 +402,7 @@ int sync_grids(vpx_ctx* c) {
     std::vector<DevGrid> h(n);
     for (uint32_t i = 0; i < n; ++i) {
         const auto& g = c->grids[i];
-        h[i] = DevGrid{g.ptr, g.l1, g.l2, g.l3, g.n, g.nb1, g.nb2, g.nb3};
+        h[i] = DevGrid{g.ptr, g.l1, g.l2, g.n, g.nb1, g.nb2, g.nb3};
     }
     if (n) VPX_HIP(c, hipMemcpy(c->d_grids, h.data(), sizeof(DevGrid) * n, hipMemcpyHostToDevice));
     return VPX_OK;
@@ -612,7 +628,6 @@ int vpx_destroy(vpx_ctx* c) {
         if (g.ptr) (void)hipFree(g.ptr);
         if (g.l1) (void)hipFree(g.l1);
         if (g.l2) (void)hipFree(g.l2);
-        if (g.l3) (void)hipFree(g.l3);
     }
     void* ptrs[] = {c->d_grids, c->d_volumes, c->d_materials, c->d_points, c->d_spots, c->d_areas,
                     c->d_spheres, c->d_triangles, c->d_ctr, c->d_sum, c->d_scratch, c->d_wave};
@@ -654,8 +669,7 @@ static int alloc_grid(vpx_ctx* c, uint32_t id, uint32_t n) {
         (void)hipFree(g.ptr);
         (void)hipFree(g.l1);
         (void)hipFree(g.l2);
-        (void)hipFree(g.l3);
-        g.ptr = nullptr, g.l1 = nullptr, g.l2 = nullptr, g.l3 = nullptr;
+        g.ptr = nullptr, g.l1 = nullptr, g.l2 = nullptr;
     }
     g.n = n;
     g.nb1 = (n + 3) / 4;
@@ -665,30 +679,45 @@ static int alloc_grid(vpx_ctx* c, uint32_t id, uint32_t n) {
         VPX_HIP(c, hipMalloc(&g.ptr, bytes));
         VPX_HIP(c, hipMalloc(&g.l1, sizeof(uint64_t) * (size_t)g.nb2 * g.nb2 * g.nb2 * 64));
         VPX_HIP(c, hipMalloc(&g.l2, sizeof(uint64_t) * (size_t)g.nb3 * g.nb3 * g.nb3 * 64));
-        VPX_HIP(c, hipMalloc(&g.l3, sizeof(uint64_t) * (size_t)g.nb3 * g.nb3 * g.nb3));
     }
     return sync_grids(c);
 }
 
-// Rebuild the occupancy hierarchy after the grid bytes changed.
+// The distance-field words of every empty brick (recurrence: skip::df_value), one
+// anti-diagonal plane per launch from the far corner — all 8 octants at once, each in its
+// own flipped coordinates and its own byte of the word.  Needs l2 (occupancy) current.
+static int build_df(vpx_ctx* c, const vpx_ctx::GridBuf& g) {
+    const uint64_t threads = (uint64_t)g.nb1 * g.nb1 * 8;
+    const unsigned blocks = (unsigned)((threads + 255) / 256);
+    for (uint32_t s = 3 * (g.nb1 - 1) + 1; s-- > 0;) {
+        hipLaunchKernelGGL(df_plane_k, dim3(blocks), dim3(256), 0, c->stream, (uint8_t*)g.l1, g.l2, g.nb1, g.nb2, g.nb3, s);
+        VPX_HIP(c, hipGetLastError());
+    }
+    return VPX_OK;
+}
+
+// Rebuild the occupancy levels and the distance field after the grid bytes changed.
 static int build_masks(vpx_ctx* c, uint32_t id) {
     auto& g = c->grids[id];
     hipLaunchKernelGGL(build_l1_k, dim3(2048), dim3(256), 0, c->stream, g.ptr, g.n, g.nb1, g.nb2, g.l1);
     VPX_HIP(c, hipGetLastError());
     hipLaunchKernelGGL(build_up_k, dim3(512), dim3(256), 0, c->stream, g.l1, g.nb2, g.nb3, g.l2);
     VPX_HIP(c, hipGetLastError());
-    hipLaunchKernelGGL(build_up_k, dim3(64), dim3(256), 0, c->stream, g.l2, g.nb3, 0u, g.l3);
-    VPX_HIP(c, hipGetLastError());
+    if (int r = build_df(c, g)) return r;
     VPX_HIP(c, hipStreamSynchronize(c->stream));
     return VPX_OK;
 }
 
-// Refresh the occupancy levels for the cells [x0, x1) x [y0, y1) x [z0, z1) only.
+// Refresh the occupancy levels for the macros that hold the cells [x0, x1) x [y0, y1) x
+// [z0, z1) (their bricks' words are recomputed whole, so the l2 words see fresh masks
+// only), then the distance field (an edit can change it far behind the box).
 static int build_masks_box(vpx_ctx* c, uint32_t id, uint32_t x0, uint32_t y0, uint32_t z0, uint32_t x1, uint32_t y1,
                            uint32_t z1) {
     auto& g = c->grids[id];
     if (x0 >= x1 || y0 >= y1 || z0 >= z1) return VPX_OK;
-    uint32_t lo[3] = {x0 >> 2, y0 >> 2, z0 >> 2}, hi[3] = {(x1 - 1) >> 2, (y1 - 1) >> 2, (z1 - 1) >> 2};
+    uint32_t lo[3] = {(x0 >> 4) * 4, (y0 >> 4) * 4, (z0 >> 4) * 4};
+    uint32_t hi[3] = {((x1 - 1) >> 4) * 4 + 3, ((y1 - 1) >> 4) * 4 + 3, ((z1 - 1) >> 4) * 4 + 3};
+    for (int k = 0; k < 3; ++k) hi[k] = hi[k] < g.nb1 - 1 ? hi[k] : g.nb1 - 1;
     auto blocks = [](uint64_t a, uint64_t b, uint64_t cc) { return (unsigned)std::min<uint64_t>(4096, (a * b * cc + 255) / 256); };
     hipLaunchKernelGGL(build_l1_box_k, dim3(blocks(hi[0] - lo[0] + 1, hi[1] - lo[1] + 1, hi[2] - lo[2] + 1)), dim3(256), 0,
                        c->stream, g.ptr, g.n, g.nb2, g.l1, lo[0], lo[1], lo[2], hi[0] - lo[0] + 1, hi[1] - lo[1] + 1,
@@ -699,11 +728,7 @@ static int build_masks_box(vpx_ctx* c, uint32_t id, uint32_t x0, uint32_t y0, ui
                        c->stream, g.l1, g.nb2, g.nb3, g.l2, lo[0], lo[1], lo[2], hi[0] - lo[0] + 1, hi[1] - lo[1] + 1,
                        hi[2] - lo[2] + 1);
     VPX_HIP(c, hipGetLastError());
-    for (int k = 0; k < 3; ++k) lo[k] >>= 2, hi[k] >>= 2;  // supers
-    hipLaunchKernelGGL(build_up_box_k, dim3(blocks(hi[0] - lo[0] + 1, hi[1] - lo[1] + 1, hi[2] - lo[2] + 1)), dim3(256), 0,
-                       c->stream, g.l2, g.nb3, 0u, g.l3, lo[0], lo[1], lo[2], hi[0] - lo[0] + 1, hi[1] - lo[1] + 1,
-                       hi[2] - lo[2] + 1);
-    VPX_HIP(c, hipGetLastError());
+    if (int r = build_df(c, g)) return r;
     VPX_HIP(c, hipStreamSynchronize(c->stream));
     return VPX_OK;
 }

@@ -13,11 +13,13 @@
 // instead of O(k) — exactly, bit for bit.  Ties, stagnation, non-positive or non-finite
 // values fall back to single IEEE additions (or to the cell-by-cell march).
 //
-// walk_skip() uses that to cross boxes of empty cells (empty 16^3 macros and 64^3
-// super-bricks of the occupancy hierarchy) in one jump: it finds the merged event that
-// leaves the box, counts the events before it per axis, and lands on the reference state
-// just before that event, adding the skipped cells to the count.  Cells in non-empty
-// macros are marched one by one.  Results equal the cell-by-cell march exactly.
+// walk_skip() uses that to cross boxes of empty cells in one jump: it finds the merged
+// event that leaves the box, counts the events before it per axis, and lands on the
+// reference state just before that event, adding the skipped cells to the count.  The
+// boxes come from a directional distance field over 4^3 bricks (an empty brick stores,
+// per ray octant, the side of the largest empty cube of bricks that starts at it and
+// grows in that octant's direction).  Cells in non-empty bricks are marched one by one.
+// Results equal the cell-by-cell march exactly.
 #pragma once
 
 #include <stdint.h>
@@ -231,13 +233,16 @@ VPX_HD uint32_t count_below2(float a, float d, float T, bool strict, uint32_t km
 namespace vpx {
 namespace skip {
 
-// A grid as the skipping walker sees it: the MatType bytes and the occupancy hierarchy
-// l1 (4^3 bricks: cell bits), l2 (16^3 macros: brick bits), l3 (64^3 supers: macro bits).
+// A grid as the skipping walker sees it: the MatType bytes and two occupancy levels.
+// l2 (16^3 macros): bit per child brick, set <=> the brick holds a solid cell.
+// l1 (4^3 bricks): for an occupied brick, bit lx + 4ly + 16lz per solid cell; for an
+// empty brick, its distance-field word: byte o (octant o = [sx<0] | [sy<0]<<1 | [sz<0]<<2)
+// = k >= 1 such that the k^3 bricks from this one toward the octant are all empty (bricks
+// outside the grid count as empty), capped at 255.
 struct GridView {
     const uint8_t* cells;
     const uint64_t* l1;
     const uint64_t* l2;
-    const uint64_t* l3;
     uint32_t n, nb1, nb2, nb3;
 };
 
@@ -246,17 +251,24 @@ struct Walk {
     float t, tx, ty, tz;
     float dx, dy, dz;
     int32_t sx, sy, sz;
-    uint32_t k1, k2, k3;
-    uint64_t m1, m2, m3;
+    uint32_t k1, k2;
+    uint32_t osh;  // 8 x the ray's octant: the shift of its byte in a distance-field word
+    uint64_t m1, m2;
 };
+
+// Reset the cached level words and set the octant (after X..sz are set).
+VPX_HD void walk_begin(Walk& w) {
+    w.k1 = w.k2 = 0xffffffffu;
+    w.m1 = w.m2 = 0ull;
+    w.osh = ((w.sx < 0 ? 1u : 0u) | (w.sy < 0 ? 2u : 0u) | (w.sz < 0 ? 4u : 0u)) * 8u;
+}
 
 VPX_HD uint32_t pack3(uint32_t a, uint32_t b, uint32_t c) { return a | (b << 11) | (c << 22); }
 
 // Occupancy-level layout.  l1 (bricks) and l2 (macros) are stored BLOCKED: the 64 words
 // of one parent (a 4x4x4 group of blocks) are contiguous, parents in linear order.  A
-// wave's rays then share 128-byte lines across y/z neighbours too, and a parent's word
-// is the OR-reduction of 64 consecutive child words.  l3 is linear.  `np` = parents per
-// axis.  np <= 256 (grids up to 4096^3): every product fits the 24-bit multiplier.
+// wave's rays then share 128-byte lines across y/z neighbours too, and a parent's bits
+// come from 64 consecutive child words.  `np` = parents per axis.  np <= 256 (grids up to 4096^3): every product fits the 24-bit multiplier.
 VPX_HD uint32_t blk_index(uint32_t bx, uint32_t by, uint32_t bz, uint32_t np) {
 #if defined(__HIP_DEVICE_COMPILE__)
     const uint32_t parent = __umul24(bz >> 2, __umul24(np, np)) + __umul24(by >> 2, np) + (bx >> 2);
@@ -282,35 +294,46 @@ VPX_HD uint32_t lin_index(uint32_t x, uint32_t y, uint32_t z, uint32_t nb) {
 #endif
 }
 
-// 0: solid cell, 1: empty cell, 2: inside an empty 16^3 macro, 3: inside an empty 64^3 super.
-// Each level's word is cached by key; a step re-reads nothing unless it changed blocks.
-// (Checking only the brick key and walking the hierarchy on brick changes was measured
-// slower on the device: the per-wave divergence of that branch costs more than it saves.)
+#ifndef VPX_MIN_CUBE
+#define VPX_MIN_CUBE 2
+#endif
+// Smallest distance-field cube (in bricks) worth a skip; smaller ones are stepped through.
+constexpr uint32_t kMinCube = VPX_MIN_CUBE;
+
+// 0: solid cell, 1: empty cell (step), 2: empty brick with a distance-field cube of at
+// least kMinCube bricks (skip it: df_box).  The level words are cached by key; the l2 and
+// l1 loads are independent, so a brick change costs one load latency.
 VPX_HD int classify(Walk& w, const GridView& g) {
     const uint32_t X = w.X, Y = w.Y, Z = w.Z;
-
-    const uint32_t k3 = pack3(X >> 6, Y >> 6, Z >> 6);
-    if (k3 != w.k3) {
-        w.k3 = k3;
-        w.m3 = load_mask(g.l3, lin_index(X >> 6, Y >> 6, Z >> 6, g.nb3));
-    }
-    if (w.m3 == 0) return 3;
-    const uint32_t mb = ((X >> 4) & 3u) | (((Y >> 4) & 3u) << 2) | (((Z >> 4) & 3u) << 4);
-    if (!((w.m3 >> mb) & 1ull)) return 2;
     const uint32_t k2 = pack3(X >> 4, Y >> 4, Z >> 4);
     if (k2 != w.k2) {
         w.k2 = k2;
         w.m2 = load_mask(g.l2, blk_index(X >> 4, Y >> 4, Z >> 4, g.nb3));
     }
-    const uint32_t bb = ((X >> 2) & 3u) | (((Y >> 2) & 3u) << 2) | (((Z >> 2) & 3u) << 4);
-    if (!((w.m2 >> bb) & 1ull)) return 1;
     const uint32_t k1 = pack3(X >> 2, Y >> 2, Z >> 2);
     if (k1 != w.k1) {
         w.k1 = k1;
         w.m1 = load_mask(g.l1, blk_index(X >> 2, Y >> 2, Z >> 2, g.nb2));
     }
+    const uint32_t bb = ((X >> 2) & 3u) | (((Y >> 2) & 3u) << 2) | (((Z >> 2) & 3u) << 4);
+    if (!((w.m2 >> bb) & 1ull)) return ((uint32_t)(w.m1 >> w.osh) & 255u) >= kMinCube ? 2 : 1;
     const uint32_t cb = (X & 3u) | ((Y & 3u) << 2) | ((Z & 3u) << 4);
     return ((w.m1 >> cb) & 1ull) ? 0 : 1;
+}
+
+// The empty box of a class-2 cell: its brick's distance-field cube toward the ray's
+// octant, clipped to the grid.  Only the faces ahead of the ray matter to skip_box, so the
+// faces behind are put at the current cell.
+VPX_HD void df_box(const Walk& w, uint32_t n, uint32_t lo[3], uint32_t hi[3]) {
+    const uint32_t k4 = ((uint32_t)(w.m1 >> w.osh) & 255u) * 4u;
+    const uint32_t c[3] = {w.X, w.Y, w.Z};
+    const int32_t sg[3] = {w.sx, w.sy, w.sz};
+    for (int k = 0; k < 3; ++k) {
+        const uint32_t b = c[k] & ~3u;
+        const uint32_t up = b + k4 - 1u, dn = b + 4u > k4 ? b + 4u - k4 : 0u;
+        lo[k] = sg[k] > 0 ? c[k] : dn;
+        hi[k] = sg[k] > 0 ? (up < n - 1u ? up : n - 1u) : c[k];
+    }
 }
 
 // One reference step (scene.cpp:773-802), branch-free; false = left the grid.
@@ -343,7 +366,7 @@ VPX_HD int skip_box(Walk& w, const uint32_t lo[3], const uint32_t hi[3], float b
     for (int k = 0; k < 3; ++k) {
         if (!(h[k] > 0.0f) || !(d[k] > 0.0f)) return 2;  // NaN, zero or negative: march instead
         e[k] = s[k] > 0 ? hi[k] - c[k] + 1u : c[k] - lo[k] + 1u;
-        // A(e-1) ~ h + (e-1) d, relative error < (e+1) 2^-24 (<= 4e-6 for e <= 64)
+        // A(e-1) ~ h + (e-1) d, relative error < (e+1) 2^-24 (< 6.2e-5 for e <= 1024)
         approx[k] = e[k] > 1u ? h[k] + (float)(e[k] - 1u) * d[k] : h[k];
     }
     // leaving event = smallest A_k(e_k - 1), ties -> z, then y, then x.  Decide on the
@@ -354,7 +377,7 @@ VPX_HD int skip_box(Walk& w, const uint32_t lo[3], const uint32_t hi[3], float b
     const float amin = approx[a];
     bool close = false;
     for (int k = 0; k < 3; ++k)
-        if (k != a && !(approx[k] > amin * 1.0001f)) close = true;
+        if (k != a && !(approx[k] > amin * 1.0003f)) close = true;
     if (close) {
         for (int k = 0; k < 3; ++k) {
             count_below2(h[k], d[k], 3.4e38f, true, e[k] - 1u, V[k], Vp[k]);
@@ -426,18 +449,18 @@ struct Seq2 {
     uint32_t b2, c2, e2;
 };
 
-VPX_HD bool seq2_init(float a, float d, uint32_t last, Seq2& q) {  // last <= 63
+VPX_HD bool seq2_init(float a, float d, uint32_t last, Seq2& q) {  // last <= 1023
     if (!seg_params(a, d, q.b1, q.c1, q.e1)) return false;
     const uint32_t room = 0xffffffu - q.b1;
     q.b2 = q.c2 = q.e2 = 0u;
-    if (last * q.c1 <= room) {  // c1 <= 2^23: no overflow for last <= 63
+    if ((uint64_t)last * q.c1 <= room) {
         q.m1 = last;
         return true;
     }
     q.m1 = udiv(room, q.c1);
     const float A = seg_value(q.b1 + q.m1 * q.c1, q.e1) + d;
     if (!seg_params(A, d, q.b2, q.c2, q.e2)) return false;
-    return (last - q.m1 - 1u) * q.c2 <= 0xffffffu - q.b2;
+    return (uint64_t)(last - q.m1 - 1u) * q.c2 <= 0xffffffu - q.b2;
 }
 
 VPX_HD float seq2_at(const Seq2& q, uint32_t i) {
@@ -531,7 +554,8 @@ VPX_HD int skip_box_fast(Walk& w, const uint32_t lo[3], const uint32_t hi[3], fl
 // skip_box in straight-line integer code for the common case: every axis sequence is in
 // closed form over the box with at most one binade change (no tie, not stuck).  Anything
 // else returns 2 and the lane takes skip_any later (the caller batches those lanes).
-// All products are < 2^24 x 2^6, so they use the full-rate 24-bit multiplier.
+// Boxes span at most 1024 cells per axis.  Every product formed is below 2^32 with both
+// factors below 2^24, so it uses the full-rate 24-bit multiplier.
 
 VPX_HD uint32_t mul24(uint32_t a, uint32_t b) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -570,30 +594,32 @@ VPX_HD bool seg_params_nb(float a, float d, uint32_t& b, uint32_t& c, uint32_t& 
     return (ea - 1u < 254u) & (ed - 1u < 254u) & (ed < ea) & (sh <= 24u) & (c != 0u);
 }
 
-// ceil(p / c) clamped to 65 (p <= 2^24 + 1, c >= 1).
-VPX_HD uint32_t ceil_div_65(uint32_t p, uint32_t c) {
+// ceil(p / c) clamped to 1025 (p <= 2^24 + 1, 1 <= c < 2^24).  q's error is far below 1
+// (relative 2^-22, q <= 1024.5), so one correction each way makes it exact; the products
+// stay below 2^25 (j ~ p / c, or c < 2^14 when clamped).
+VPX_HD uint32_t ceil_div_cap(uint32_t p, uint32_t c) {
     const float q = (float)p * rcp_approx((float)c);
-    uint32_t j = (uint32_t)(q < 64.5f ? q : 64.5f) + 1u;  // ceil(p/c) or one off, <= 65
+    uint32_t j = (uint32_t)(q < 1024.5f ? q : 1024.5f) + 1u;  // ceil(p/c) or one off, <= 1025
     j -= mul24(j - 1u, c) >= p ? 1u : 0u;
     j += mul24(j, c) < p ? 1u : 0u;
-    return j < 65u ? j : 65u;
+    return j < 1025u ? j : 1025u;
 }
 
-// floor(r / c) clamped to 64 (r < 2^24, c >= 1).
-VPX_HD uint32_t floor_div_64(uint32_t r, uint32_t c) {
+// floor(r / c) clamped to 1024 (r < 2^24, 1 <= c < 2^24).
+VPX_HD uint32_t floor_div_cap(uint32_t r, uint32_t c) {
     const float q = (float)r * rcp_approx((float)c);
-    uint32_t m = (uint32_t)(q < 64.5f ? q : 64.5f);
+    uint32_t m = (uint32_t)(q < 1024.5f ? q : 1024.5f);
     m -= (m && mul24(m, c) > r) ? 1u : 0u;
     m += mul24(m + 1u, c) <= r ? 1u : 0u;
-    return m < 64u ? m : 64u;
+    return m < 1024u ? m : 1024u;
 }
 
-// First j >= 0 with (b + j c) u not below T (strict: >= T, else > T), clamped to 65.
-VPX_HD uint32_t seg_first65(uint32_t b, uint32_t c, uint32_t e, float T, bool strict) {
+// First j >= 0 with (b + j c) u not below T (strict: >= T, else > T), clamped to 1025.
+VPX_HD uint32_t seg_first_cap(uint32_t b, uint32_t c, uint32_t e, float T, bool strict) {
     const uint32_t tb = fbits(T), te = tb >> 23;
     const uint32_t need = ((tb & 0x7fffffu) | 0x800000u) + (strict ? 0u : 1u);
-    const uint32_t f = need <= b ? 0u : ceil_div_65(need - b, c);
-    return te == e ? f : (te < e ? 0u : 65u);
+    const uint32_t f = need <= b ? 0u : ceil_div_cap(need - b, c);
+    return te == e ? f : (te < e ? 0u : 1025u);
 }
 
 // One axis over the box: A(0..l) as one or two closed-form segments: A(i) = (b1 + i c1) u1
@@ -606,8 +632,9 @@ VPX_HD bool axis_init(float h, float d, uint32_t l, Axis& a) {
     const bool ok1 = seg_params_nb(h, d, a.b1, a.c1, a.e1);
     // A(i), 1 <= i <= m1, stay below 2^24 u (a tie base may be 2^24 itself: m1 = 0)
     const uint32_t room = a.b1 <= 0xffffffu ? 0xffffffu - a.b1 : 0u;
-    const bool cross = mul24(l, a.c1) > room;  // l <= 63, c1 <= 2^23 when ok1
-    a.m1 = cross ? floor_div_64(room, a.c1 | 1u) : l;
+    const uint32_t fit1 = floor_div_cap(room, a.c1 | 1u);  // last i with i c1 <= room (l <= 1023)
+    const bool cross = l > fit1;
+    a.m1 = cross ? fit1 : l;
     const float Am = a.m1 ? bitsf((a.e1 << 23) | ((a.b1 + mul24(a.m1, a.c1)) & 0x7fffffu)) : h;
     const float A = Am + d;  // the plain IEEE step into the next binade
     uint32_t b2;
@@ -615,7 +642,8 @@ VPX_HD bool axis_init(float h, float d, uint32_t l, Axis& a) {
     // the second segment starts at A itself: its closed form must hold from j = 0
     const bool exact2 = b2 == ((fbits(A) & 0x7fffffu) | 0x800000u);
     a.b2 = b2;
-    const bool fit2 = mul24(l - a.m1 - 1u, a.c2) <= 0xffffffu - a.b2;
+    const uint32_t room2 = a.b2 <= 0xffffffu ? 0xffffffu - a.b2 : 0u;
+    const bool fit2 = l - a.m1 - 1u <= floor_div_cap(room2, a.c2 | 1u);
     // no event inside the box (l == 0): only A(0) = h is read
     return (h > 0.0f) & (d > 0.0f) & (l == 0u || (ok1 & (!cross || (ok2 & exact2 & fit2))));
 }
@@ -627,18 +655,18 @@ VPX_HD float axis_at(const Axis& a, float h, uint32_t i) {
     return i ? v : h;
 }
 
-// #{ i < cap : A(i) below T } (A increasing), cap <= 63.
+// #{ i < cap : A(i) below T } (A increasing), cap <= 1023.
 VPX_HD uint32_t axis_count(const Axis& a, float h, float T, bool strict, uint32_t cap) {
     const bool h_below = strict ? h < T : h <= T;
-    uint32_t f1 = seg_first65(a.b1, a.c1, a.e1, T, strict);
+    uint32_t f1 = seg_first_cap(a.b1, a.c1, a.e1, T, strict);
     f1 = h_below ? (f1 > 1u ? f1 : 1u) : 0u;  // index 0 is h itself
-    const uint32_t f2 = a.m1 + 1u + seg_first65(a.b2, a.c2, a.e2, T, strict);
+    const uint32_t f2 = a.m1 + 1u + seg_first_cap(a.b2, a.c2, a.e2, T, strict);
     const uint32_t f = f1 > a.m1 ? f2 : f1;
     return f < cap ? f : cap;
 }
 
 VPX_HD int skip_box_fast1(Walk& w, const uint32_t lo[3], const uint32_t hi[3], float bound, uint32_t& cells) {
-    const uint32_t lx = (w.sx > 0 ? hi[0] - w.X : w.X - lo[0]);  // events inside the box, <= 63
+    const uint32_t lx = (w.sx > 0 ? hi[0] - w.X : w.X - lo[0]);  // events inside the box, <= 1023
     const uint32_t ly = (w.sy > 0 ? hi[1] - w.Y : w.Y - lo[1]);
     const uint32_t lz = (w.sz > 0 ? hi[2] - w.Z : w.Z - lo[2]);
     Axis ax, ay, az;
@@ -699,11 +727,9 @@ VPX_HD int walk_skip_some(const GridView& g, Walk& w, float bound, uint32_t& cel
             ++cells;
             return 1;
         }
-        if (cls >= 2) {
-            const uint32_t m = cls == 3 ? 63u : 15u;
-            const uint32_t lo[3] = {w.X & ~m, w.Y & ~m, w.Z & ~m};
-            uint32_t hi[3] = {lo[0] + m, lo[1] + m, lo[2] + m};
-            for (int k = 0; k < 3; ++k) hi[k] = hi[k] < g.n - 1u ? hi[k] : g.n - 1u;
+        if (cls == 2) {
+            uint32_t lo[3], hi[3];
+            df_box(w, g.n, lo, hi);
             if (skip_any(w, lo, hi, bound, cells) == 1) return 2;
         }
         ++cells;
@@ -722,11 +748,9 @@ VPX_HD bool walk_skip(const GridView& g, Walk& w, float bound, uint32_t& cells) 
             ++cells;
             return true;
         }
-        if (cls >= 2) {
-            const uint32_t m = cls == 3 ? 63u : 15u;
-            const uint32_t lo[3] = {w.X & ~m, w.Y & ~m, w.Z & ~m};
-            uint32_t hi[3] = {lo[0] + m, lo[1] + m, lo[2] + m};
-            for (int k = 0; k < 3; ++k) hi[k] = hi[k] < g.n - 1u ? hi[k] : g.n - 1u;
+        if (cls == 2) {
+            uint32_t lo[3], hi[3];
+            df_box(w, g.n, lo, hi);
             if (skip_any(w, lo, hi, bound, cells) == 1) return false;
         }
         ++cells;  // visit the (empty) current cell
@@ -734,14 +758,30 @@ VPX_HD bool walk_skip(const GridView& g, Walk& w, float bound, uint32_t& cells) 
     }
 }
 
+// Distance-field byte of an empty brick (x, y, z) for octant o from its 7 neighbours
+// ahead (the recurrence both builders use): 1 + the minimum over the neighbours (0 for an
+// occupied one, 255 outside [0, nb1)), capped at 255.  The k^3 cube at a brick is empty
+// iff the brick and the (k-1)^3 cubes at its 7 neighbours ahead are.
+template <class Occ, class Get>
+VPX_HD uint8_t df_value(uint32_t x, uint32_t y, uint32_t z, uint32_t o, uint32_t nb1, Occ occ, Get get) {
+    const int32_t s[3] = {(o & 1u) ? -1 : 1, (o & 2u) ? -1 : 1, (o & 4u) ? -1 : 1};
+    uint32_t mn = 255;
+    for (uint32_t j = 1; j < 8; ++j) {
+        const uint32_t a = x + ((j & 1u) ? (uint32_t)s[0] : 0u), b = y + ((j & 2u) ? (uint32_t)s[1] : 0u),
+                       c = z + ((j & 4u) ? (uint32_t)s[2] : 0u);
+        const uint32_t v = (a < nb1 && b < nb1 && c < nb1) ? (occ(a, b, c) ? 0u : get(a, b, c, o)) : 255u;
+        mn = v < mn ? v : mn;
+    }
+    return (uint8_t)(mn < 255u ? mn + 1u : 255u);
+}
+
 #if !defined(__HIP_DEVICE_COMPILE__)
-// Host builder of the same hierarchy (tests and tools).  Sizes: l1 nb2^3*64, l2 nb3^3*64,
-// l3 nb3^3 words (nb1 = ceil(n/4), nb2 = ceil(nb1/4), nb3 = ceil(nb2/4)).
-inline void build_masks_host(const uint8_t* cells, uint32_t n, uint64_t* l1, uint64_t* l2, uint64_t* l3) {
+// Host builder of the same levels (tests and tools).  Sizes: l1 nb2^3*64 words, l2
+// nb3^3*64 words (nb1 = ceil(n/4), nb2 = ceil(nb1/4), nb3 = ceil(nb2/4)).
+inline void build_masks_host(const uint8_t* cells, uint32_t n, uint64_t* l1, uint64_t* l2) {
     const uint32_t nb1 = (n + 3) / 4, nb2 = (nb1 + 3) / 4, nb3 = (nb2 + 3) / 4;
     std::memset(l1, 0, 8ull * nb2 * nb2 * nb2 * 64);
     std::memset(l2, 0, 8ull * nb3 * nb3 * nb3 * 64);
-    std::memset(l3, 0, 8ull * nb3 * nb3 * nb3);
     for (uint64_t z = 0; z < n; ++z)
         for (uint64_t y = 0; y < n; ++y)
             for (uint64_t x = 0; x < n; ++x)
@@ -753,11 +793,21 @@ inline void build_masks_host(const uint8_t* cells, uint32_t n, uint64_t* l1, uin
             for (uint32_t x = 0; x < nb1; ++x)
                 if (l1[blk_index(x, y, z, nb2)])
                     l2[blk_index(x >> 2, y >> 2, z >> 2, nb3)] |= 1ull << ((x & 3) + 4 * (y & 3) + 16 * (z & 3));
-    for (uint32_t z = 0; z < nb2; ++z)
-        for (uint32_t y = 0; y < nb2; ++y)
-            for (uint32_t x = 0; x < nb2; ++x)
-                if (l2[blk_index(x, y, z, nb3)])
-                    l3[lin_index(x >> 2, y >> 2, z >> 2, nb3)] |= 1ull << ((x & 3) + 4 * (y & 3) + 16 * (z & 3));
+    auto occ = [&](uint32_t x, uint32_t y, uint32_t z) {
+        return (l2[blk_index(x >> 2, y >> 2, z >> 2, nb3)] >> ((x & 3) + 4 * (y & 3) + 16 * (z & 3))) & 1ull;
+    };
+    uint8_t* bytes = reinterpret_cast<uint8_t*>(l1);
+    auto get = [&](uint32_t x, uint32_t y, uint32_t z, uint32_t o) -> uint32_t {
+        return bytes[(size_t)blk_index(x, y, z, nb2) * 8 + o];
+    };
+    for (uint32_t o = 0; o < 8; ++o)  // sweep each octant from its far corner
+        for (uint32_t fz = nb1; fz-- > 0;)
+            for (uint32_t fy = nb1; fy-- > 0;)
+                for (uint32_t fx = nb1; fx-- > 0;) {
+                    const uint32_t x = (o & 1u) ? nb1 - 1 - fx : fx, y = (o & 2u) ? nb1 - 1 - fy : fy,
+                                   z = (o & 4u) ? nb1 - 1 - fz : fz;
+                    if (!occ(x, y, z)) bytes[(size_t)blk_index(x, y, z, nb2) * 8 + o] = df_value(x, y, z, o, nb1, occ, get);
+                }
 }
 #endif
 

@@ -29,21 +29,20 @@ constexpr float kBig = 1e34f;
 constexpr int kMaxLevels = 16;                     // max_bounces <= 14 -> 15 levels
 
 // ----------------------------------------------------------------------- device view
-// A voxel grid as the device walks it: the dense MatType bytes (x + y*N + z*N^2) plus a
-// two-level occupancy hierarchy built from them (build_masks): l1 = one 64-bit mask per
-// 4x4x4 brick (bit lx + 4ly + 16lz set <=> cell != NONE), l2 = one 64-bit mask per 16^3
-// macro brick (bit per child brick with a non-zero l1 mask).  The hierarchy only decides
-// WHETHER a cell must be read; the march still visits every cell in the reference order
-// with the reference float arithmetic, so t / cells / normals are unchanged.
+// A voxel grid as the device walks it: the dense MatType bytes (x + y*N + z*N^2) plus
+// two levels built from them (build_masks, layout in vpx_skip.hpp GridView): l2 = one
+// 64-bit brick-occupancy mask per 16^3 macro, l1 = per 4^3 brick its cell mask (occupied)
+// or its directional distance-field word (empty).  They only decide WHETHER a cell must
+// be read; the march still visits every cell in the reference order with the reference
+// float arithmetic, so t / cells / normals are unchanged.
 struct DevGrid {
     const uint8_t* cells;
     const uint64_t* l1;
     const uint64_t* l2;
-    const uint64_t* l3;
     uint32_t n;
     uint32_t nb1;  // bricks per axis  = ceil(n / 4)
     uint32_t nb2;  // macros per axis  = ceil(nb1 / 4)
-    uint32_t nb3;  // supers per axis  = ceil(nb2 / 4)
+    uint32_t nb3;  // macro parents per axis (l2 blocking) = ceil(nb2 / 4)
 };
 
 struct SceneView {
@@ -264,8 +263,8 @@ __device__ __forceinline__ T* uni_ptr(T* p) {
     return (T*)(((uint64_t)uni((uint32_t)(v >> 32)) << 32) | uni((uint32_t)v));
 }
 __device__ __forceinline__ skip::GridView grid_view(const DevGrid& g) {
-    return skip::GridView{uni_ptr(g.cells), uni_ptr(g.l1), uni_ptr(g.l2), uni_ptr(g.l3),
-                          uni(g.n), uni(g.nb1), uni(g.nb2), uni(g.nb3)};
+    return skip::GridView{uni_ptr(g.cells), uni_ptr(g.l1), uni_ptr(g.l2), uni(g.n), uni(g.nb1), uni(g.nb2),
+                          uni(g.nb3)};
 }
 __device__ __forceinline__ skip::Walk to_walk(const Dda& s) {
     skip::Walk w;
@@ -274,8 +273,7 @@ __device__ __forceinline__ skip::Walk to_walk(const Dda& s) {
     w.tx = s.tmax.x, w.ty = s.tmax.y, w.tz = s.tmax.z;
     w.dx = s.tdelta.x, w.dy = s.tdelta.y, w.dz = s.tdelta.z;
     w.sx = s.sx, w.sy = s.sy, w.sz = s.sz;
-    w.k1 = w.k2 = w.k3 = 0xffffffffu;
-    w.m1 = w.m2 = w.m3 = 0ull;
+    skip::walk_begin(w);
     return w;
 }
 
@@ -307,17 +305,9 @@ __device__ unsigned long long g_phase[32];
 #define VPX_PH(...)
 #endif
 
-__device__ __forceinline__ void skip_box_of(const skip::Walk& w, int level, uint32_t n, uint32_t lo[3], uint32_t hi[3]) {
-    const uint32_t m = level == 3 ? 63u : 15u;
-    lo[0] = w.X & ~m, lo[1] = w.Y & ~m, lo[2] = w.Z & ~m;
-    hi[0] = (w.X | m) < n - 1u ? (w.X | m) : n - 1u;
-    hi[1] = (w.Y | m) < n - 1u ? (w.Y | m) : n - 1u;
-    hi[2] = (w.Z | m) < n - 1u ? (w.Z | m) : n - 1u;
-}
-
-// Lane modes: kStep wants a cell step, kSkip an empty-box skip, kMiss / kHit are done.
-// Phases are wave-uniform: cell steps while >= kStepThreshold lanes want one (or nobody
-// waits to skip), then the waiting lanes skip together.  Each lane runs exactly
+// Lane modes: kStep wants a cell step, kSkip an empty-box skip (the distance-field cube
+// of its brick, skip::df_box), kMiss / kHit are done.  Phases are wave-uniform: cell steps
+// while enough lanes want one (see SKIPW), then the waiting lanes skip together.  Each lane runs exactly
 // skip::walk_skip's sequence (the reference's cells with the reference's floats).
 // Skip tiers: with LEAN the straight-line lean tier (skip_box_fast1) goes first, else
 // skip_box_fast (closed form, <= 1 binade change), then the general skip_box.
@@ -331,7 +321,7 @@ __device__ __forceinline__ void skip_box_of(const skip::Walk& w, int level, uint
 template <bool LEAN, int PHK = 0, uint32_t SKIPW = 0>
 __device__ __forceinline__ bool walk_wave(const skip::GridView& g, skip::Walk& w, float bound, uint32_t& cells) {
     enum : int { kStep = 0, kSkip = 1, kMiss = 2, kHit = 3 };
-    int mode = kStep, pending = 0;
+    int mode = kStep;
     VPX_PH(uint64_t cs = 0, ck = 0, ns = 0, nk = 0, ls = 0, lk = 0, fb = 0, cf = 0;)
     for (;;) {
         VPX_PH(uint64_t t0 = __builtin_amdgcn_s_memtime();)
@@ -352,9 +342,8 @@ __device__ __forceinline__ bool walk_wave(const skip::GridView& g, skip::Walk& w
                     if (cls == 0) {
                         ++cells;
                         mode = kHit;
-                    } else if (cls >= 2) {
+                    } else if (cls == 2) {
                         mode = kSkip;
-                        pending = cls;
                     } else {
                         ++cells;
                         if (!skip::step1(w, g.n)) mode = kMiss;
@@ -371,7 +360,7 @@ __device__ __forceinline__ bool walk_wave(const skip::GridView& g, skip::Walk& w
         VPX_PH(++nk; lk += __popcll(skipping);)
         if (mode == kSkip) {
             uint32_t lo[3], hi[3];
-            skip_box_of(w, pending, g.n, lo, hi);
+            skip::df_box(w, g.n, lo, hi);
             int sr = LEAN ? skip::skip_box_fast1(w, lo, hi, bound, cells) : 2;
             if (!LEAN && sr == 2) sr = skip::skip_box_fast(w, lo, hi, bound, cells);  // (a subset of the lean tier)
             if (sr == 2) sr = skip::skip_box(w, lo, hi, bound, cells);

@@ -110,7 +110,7 @@ int fast_check() {
     long bad = 0, handled = 0, handled1 = 0, total = 0;
     for (long i = 0; i < 4000000; ++i) {
         Walk w{};
-        const uint32_t m = (i & 1) ? 63u : 15u;
+        const uint32_t m = (i & 3) == 0 ? 15u : (i & 3) == 1 ? 63u : (i & 3) == 2 ? 255u : 1023u;  // box sides up to 1024
         uint32_t lo[3], hi[3];
         uint32_t* C3[3] = {&w.X, &w.Y, &w.Z};
         float* H3[3] = {&w.tx, &w.ty, &w.tz};
@@ -118,7 +118,7 @@ int fast_check() {
         int32_t* S3[3] = {&w.sx, &w.sy, &w.sz};
         float tmin = 1e30f;
         for (int k = 0; k < 3; ++k) {
-            lo[k] = (uint32_t)(r() % 8) * (m + 1);
+            lo[k] = (uint32_t)(r() % 4) * (m + 1);
             hi[k] = lo[k] + m;
             *C3[k] = lo[k] + (uint32_t)(r() % (m + 1));
             *S3[k] = (r() & 1) ? 1 : -1;

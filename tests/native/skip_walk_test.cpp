@@ -15,8 +15,8 @@ using namespace vpx::skip;
 struct World {
     uint32_t n, nb1, nb2, nb3;
     std::vector<uint8_t> cells;
-    std::vector<uint64_t> l1, l2, l3;
-    GridView view() const { return GridView{cells.data(), l1.data(), l2.data(), l3.data(), n, nb1, nb2, nb3}; }
+    std::vector<uint64_t> l1, l2;
+    GridView view() const { return GridView{cells.data(), l1.data(), l2.data(), n, nb1, nb2, nb3}; }
 };
 
 static World make_world(uint32_t n, uint64_t seed, double density) {
@@ -36,8 +36,7 @@ static World make_world(uint32_t n, uint64_t seed, double density) {
     w.nb1 = (n + 3) / 4, w.nb2 = (w.nb1 + 3) / 4, w.nb3 = (w.nb2 + 3) / 4;
     w.l1.assign((size_t)w.nb2 * w.nb2 * w.nb2 * 64, 0);
     w.l2.assign((size_t)w.nb3 * w.nb3 * w.nb3 * 64, 0);
-    w.l3.assign((size_t)w.nb3 * w.nb3 * w.nb3, 0);
-    build_masks_host(w.cells.data(), n, w.l1.data(), w.l2.data(), w.l3.data());
+    build_masks_host(w.cells.data(), n, w.l1.data(), w.l2.data());
     return w;
 }
 
@@ -83,7 +82,7 @@ static bool setup(uint32_t n, const float O[3], const float D[3], Walk& w) {
     w.tx = tm[0], w.ty = tm[1], w.tz = tm[2];
     w.dx = td[0], w.dy = td[1], w.dz = td[2];
     w.sx = st[0], w.sy = st[1], w.sz = st[2];
-    w.k1 = w.k2 = w.k3 = 0xffffffffu;
+    walk_begin(w);
     return true;
 }
 
@@ -111,11 +110,9 @@ static void debug_walk(const GridView& g, Walk w, float bound) {
         if (!(w.t < bound)) return;
         const int cls = classify(w, g);
         if (cls == 0) return;
-        if (cls >= 2) {
-            const uint32_t m = cls == 3 ? 63u : 15u;
-            const uint32_t lo[3] = {w.X & ~m, w.Y & ~m, w.Z & ~m};
-            uint32_t hi[3] = {lo[0] + m, lo[1] + m, lo[2] + m};
-            for (int k = 0; k < 3; ++k) hi[k] = hi[k] < g.n - 1u ? hi[k] : g.n - 1u;
+        if (cls == 2) {
+            uint32_t lo[3], hi[3];
+            df_box(w, g.n, lo, hi);
             Walk a = w, b = w;
             uint32_t ca = 0, cb = 0;
             const int ra = skip_box_fast1(a, lo, hi, bound, ca), rb = skip_box(b, lo, hi, bound, cb);
@@ -138,9 +135,10 @@ int main(int argc, char** argv) {
     const long rays = argc > 1 ? atol(argv[1]) : 20000;
     long bad = 0, total = 0;
     uint64_t cells_all = 0;
-    const uint32_t sizes[] = {64, 100, 128, 256};
+    const uint32_t sizes[] = {64, 100, 128, 256, 1024};  // 1024: distance-field cubes up to 1020 cells
     for (uint32_t n : sizes) {
         for (double dens : {0.02, 0.2, 1.0}) {
+            if (n > 256 && dens > 0.5) continue;
             World W = make_world(n, n * 31 + (uint64_t)(dens * 100), dens);
             std::mt19937_64 r(n + 7);
             std::uniform_real_distribution<float> U(0.f, 1.f);

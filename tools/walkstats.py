@@ -9,16 +9,15 @@ subprocess.run(["g++", "-O2", "-shared", "-fPIC", "-std=c++17", "-ffp-contract=o
                 f"{REPO}/tools/native/walkstats.cpp", "-o", so], check=True)
 lib = C.CDLL(so)
 V = C.c_void_p
-lib.build_masks.argtypes = [V, C.c_uint32, V, V, V]
-lib.walk_stats.argtypes = [V, V, V, V, C.c_uint32, V, V, C.c_uint32, C.c_float, V]
+lib.build_masks.argtypes = [V, C.c_uint32, V, V]
 pkg, orc = g.load_package(), g.load_oracle()
 cfg = sys.argv[1] if len(sys.argv) > 1 else "C1"
 d = pkg.scene.CONFIGS[cfg]()
 o = orc.Oracle(pkg.abi, d)
 cells = o.cells[0]; n = d.grids[0].n
 nb = [(n + 3) // 4]; nb.append((nb[0] + 3) // 4); nb.append((nb[1] + 3) // 4)
-l1, l2, l3 = np.zeros(nb[1] ** 3 * 64, np.uint64), np.zeros(nb[2] ** 3 * 64, np.uint64), np.zeros(nb[2] ** 3, np.uint64)
-lib.build_masks(cells.ctypes.data, n, l1.ctypes.data, l2.ctypes.data, l3.ctypes.data)
+l1, l2 = np.zeros(nb[1] ** 3 * 64, np.uint64), np.zeros(nb[2] ** 3 * 64, np.uint64)
+lib.build_masks(cells.ctypes.data, n, l1.ctypes.data, l2.ctypes.data)
 # primary rays -> DDA setup (numpy float32, identity volume)
 rng = np.random.default_rng(0)
 W, H = d.width, d.height
@@ -44,23 +43,12 @@ tdel = (cell * step.astype(np.float32)) * rD
 tmax = ((np.ceil(pos) - ds) * cell - cp) * rD
 st = np.concatenate([t0[:, None], tmax, tdel], 1).astype(np.float32)
 si = np.concatenate([P0, step], 1).astype(np.int32)
-out = np.zeros(8, np.uint64)
-lib.walk_stats(cells.ctypes.data, l1.ctypes.data, l2.ctypes.data, l3.ctypes.data, n, np.ascontiguousarray(st).ctypes.data,
-               np.ascontiguousarray(si).ctypes.data, len(st), C.c_float(1e34), out.ctypes.data)
-R = len(st)
-print(f"{cfg}: rays entering grid {R}/{m}; per ray: cells {out[0]/R:.1f} iters {out[1]/R:.1f} steps {out[2]/R:.1f} "
-      f"skip16 {out[3]/R:.2f} skip64 {out[4]/R:.2f} zero-skips {out[5]/R:.2f} max iters {out[6]} fast-path skips {out[7]/max(out[3]+out[4],1):.3f}")
-wy = np.zeros(8, np.uint64)
-lib.why_out.argtypes = [V]
-lib.why_out(wy.ctypes.data)
-print("fast-path failures by axis reason (nonnormal, d>=2^E, tie/stuck, 2nd crossing):", wy[:4])
-
 # ---- box-choice simulation on primary rays and shadow rays toward the lights
-lib.walk_sim.argtypes = [V, V, V, V, C.c_uint32, V, V, V, C.c_uint32, C.c_int, V, V]
-def sim(st_, si_, bnd, opt, tout=None):
+lib.walk_sim.argtypes = [V, V, V, C.c_uint32, V, V, V, C.c_uint32, V, V]
+def sim(st_, si_, bnd, tout=None):
     o = np.zeros(8, np.uint64)
-    lib.walk_sim(cells.ctypes.data, l1.ctypes.data, l2.ctypes.data, l3.ctypes.data, n, np.ascontiguousarray(st_).ctypes.data,
-                 np.ascontiguousarray(si_).ctypes.data, np.ascontiguousarray(bnd, np.float32).ctypes.data, len(st_), opt,
+    lib.walk_sim(cells.ctypes.data, l1.ctypes.data, l2.ctypes.data, n, np.ascontiguousarray(st_).ctypes.data,
+                 np.ascontiguousarray(si_).ctypes.data, np.ascontiguousarray(bnd, np.float32).ctypes.data, len(st_),
                  o.ctypes.data, None if tout is None else tout.ctypes.data)
     return o
 def dda_state(org, dirs):
@@ -80,7 +68,7 @@ def dda_state(org, dirs):
     s2 = np.concatenate([P0, stp], 1).astype(np.int32)
     return s1[ok], s2[ok], ok
 th = np.zeros(len(st), np.float32)
-base = sim(st, si, np.full(len(st), 1e34, np.float32), 0, th)
+base = sim(st, si, np.full(len(st), 1e34, np.float32), th)
 hitp = (cp + D * th[:, None])[th > 0].astype(np.float32)
 Dh = D[th > 0]
 org = (hitp - Dh * np.float32(2e-4)).astype(np.float32)
@@ -95,13 +83,8 @@ s1, s2, ok = dda_state(org, np.broadcast_to(dd, org.shape).astype(np.float32).co
 sets["shadow-dir"] = (s1, s2, np.full(ok.sum(), 1e34, np.float32))
 for name, (a, b, bnd) in sets.items():
     R = len(a)
-    line = []
-    ref = None
-    for opt in (0,):
-        o = sim(a, b, bnd, opt)
-        if ref is None: ref = o
-        assert o[0] == ref[0] and o[3] == ref[3] and o[4] == ref[4] and o[5] == ref[5], (name, opt)  # same cells / hits / end state
-        line.append(f"opt{opt}: steps {o[1]/R:.1f} skips {o[2]/R:.1f} lean-miss {o[6]/max(o[2],1):.4f} (+16 retry {o[7]/max(o[2],1):.4f}) cost {(o[1] + 5.8 * o[2]) / R:.0f}")
-    print(f"{name} ({R} rays, cells {ref[0]/R:.0f}): " + " | ".join(line))
+    o = sim(a, b, bnd)
+    print(f"{name} ({R} rays): cells {o[0]/R:.0f} steps {o[1]/R:.1f} skips {o[2]/R:.1f} (max {o[7]}) "
+          f"lean-refused {o[6]/max(o[2],1):.4f} cost {(o[1] + 5.8 * o[2]) / R:.0f}")
     cr = np.zeros(16, np.uint64); lib.cross_out.argtypes = [V]; lib.cross_out(cr.ctypes.data)
-    print("   lean failures by binade crossings (max over axes):", cr[:10])
+    print("   lean refusals by binade crossings (max over axes):", cr[:10])
