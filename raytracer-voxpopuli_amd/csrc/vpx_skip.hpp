@@ -709,6 +709,35 @@ VPX_HD int skip_box_fast1(Walk& w, const uint32_t lo[3], const uint32_t hi[3], f
     return 1;
 }
 
+// Largest l for which axis_init(h, d, l) holds (the events the two closed-form segments
+// reach, <= 2048); 0 when not even the first segment applies.
+VPX_HD uint32_t lean_limit(float h, float d) {
+    uint32_t b1, c1, e1, b2, c2, e2;
+    const bool ok1 = seg_params_nb(h, d, b1, c1, e1);
+    const uint32_t room = b1 <= 0xffffffu ? 0xffffffu - b1 : 0u;
+    const uint32_t fit1 = floor_div_cap(room, c1 | 1u);
+    const float Am = fit1 ? bitsf((e1 << 23) | ((b1 + mul24(fit1, c1)) & 0x7fffffu)) : h;
+    const float A = Am + d;
+    const bool ok2 = seg_params_nb(A, d, b2, c2, e2);
+    const bool exact2 = b2 == ((fbits(A) & 0x7fffffu) | 0x800000u);
+    const uint32_t room2 = b2 <= 0xffffffu ? 0xffffffu - b2 : 0u;
+    const uint32_t fit2 = floor_div_cap(room2, c2 | 1u);
+    return ((h > 0.0f) & (d > 0.0f) & ok1) ? ((ok2 & exact2) ? fit1 + 1u + fit2 : fit1) : 0u;
+}
+
+// The largest sub-box of [lo, hi] around the current cell that the lean tier accepts on
+// every axis's sequence (it may still refuse a tie or a stuck sequence).
+VPX_HD void lean_clip(const Walk& w, uint32_t lo[3], uint32_t hi[3]) {
+    const float h[3] = {w.tx, w.ty, w.tz}, d[3] = {w.dx, w.dy, w.dz};
+    const int32_t sg[3] = {w.sx, w.sy, w.sz};
+    const uint32_t c[3] = {w.X, w.Y, w.Z};
+    for (int k = 0; k < 3; ++k) {
+        const uint32_t lim = lean_limit(h[k], d[k]);
+        if (sg[k] > 0) hi[k] = hi[k] - c[k] > lim ? c[k] + lim : hi[k];
+        else lo[k] = c[k] - lo[k] > lim ? c[k] - lim : lo[k];
+    }
+}
+
 // skip_box_fast, else the general skip_box.
 VPX_HD int skip_any(Walk& w, const uint32_t lo[3], const uint32_t hi[3], float bound, uint32_t& cells) {
     int r = skip_box_fast1(w, lo, hi, bound, cells);

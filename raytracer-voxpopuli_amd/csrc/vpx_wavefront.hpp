@@ -485,12 +485,12 @@ __device__ __forceinline__ uint32_t block_scan(uint32_t cnt, uint32_t& total, ui
     return base + off;
 }
 
-template <uint32_t SKIPW = VPX_SKIPW_NEAREST>
+template <uint32_t SKIPW = VPX_SKIPW_NEAREST, bool CLIP = VPX_CLIP_PRIMARY != 0>
 __device__ __forceinline__ void nearest_record(SceneView sv, const WaveBufs& w, uint32_t p, Ray& r, Counters& k) {
     r.t = kBig;
     r.mat = kNone;
     r.N = mk(0.f, 0.f, 0.f);
-    const int32_t vox = find_nearest<SKIPW>(sv, r, k);
+    const int32_t vox = find_nearest<SKIPW, CLIP>(sv, r, k);
     w.H[p] = make_float4(r.t, r.N.x, r.N.y, r.N.z);
     w.HM[p] = r.mat | ((uint32_t)(vox + 2) << 8) | (r.inside ? 0x80000000u : 0u);
 }
@@ -606,7 +606,7 @@ __global__ __launch_bounds__(256) VPX_WPE(VPX_WPE_NEAREST) void k_nearest_tile(S
         r.O = mk(o.x, o.y, o.z);
         r.D = mk(d.x, d.y, d.z);
         r.inside = (__float_as_uint(d.w) & kInside) != 0u;
-        nearest_record<VPX_SKIPW_BOUNCE>(sv, w, q, r, k);
+        nearest_record<VPX_SKIPW_BOUNCE, VPX_CLIP_BOUNCE != 0>(sv, w, q, r, k);
     }
     flush_counters(k, 0u, ctr, VPX_STAGE_BOUNCE);
 }

@@ -5,7 +5,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 import __graft_entry__ as g
 so = "/tmp/walkstats.so"
-subprocess.run(["g++", "-O2", "-shared", "-fPIC", "-std=c++17", "-ffp-contract=off", "-I", f"{REPO}/raytracer-voxpopuli_amd/csrc",
+subprocess.run(["g++", "-O2", *sys.argv[2:], "-shared", "-fPIC", "-std=c++17", "-ffp-contract=off", "-I", f"{REPO}/raytracer-voxpopuli_amd/csrc",
                 f"{REPO}/tools/native/walkstats.cpp", "-o", so], check=True)
 lib = C.CDLL(so)
 V = C.c_void_p
@@ -81,10 +81,22 @@ sets["shadow-point"] = (s1, s2, dist[ok])
 dd = np.float32([0.3, 1.0, 0.2]); dd = dd / np.sqrt((dd * dd).sum())
 s1, s2, ok = dda_state(org, np.broadcast_to(dd, org.shape).astype(np.float32).copy())
 sets["shadow-dir"] = (s1, s2, np.full(ok.sum(), 1e34, np.float32))
-for name, (a, b, bnd) in sets.items():
+nbk = nb[0]
+bocc = np.ascontiguousarray((np.pad(cells.reshape(n, n, n), [(0, nbk * 4 - n)] * 3, constant_values=255)
+                            .reshape(nbk, 4, nbk, 4, nbk, 4) != 255).any(axis=(1, 3, 5)).astype(np.uint8))
+lib.build_slabs.argtypes = [V, C.c_uint32]
+lib.build_slabs(bocc.ctypes.data, nbk)
+lib.set_mode.argtypes = [C.c_int]
+lib.slab_out.restype = C.c_uint64
+modes = [int(x) for x in os.environ.get("MODES", "0").split()]
+for name, (a, b, bnd), mode in [(nm_, v, md) for nm_, v in sets.items() for md in modes]:
+    lib.set_mode(mode)
     R = len(a)
     o = sim(a, b, bnd)
+    print(f"mode {mode}: slab skips {lib.slab_out() / R:.1f} per ray")
     print(f"{name} ({R} rays): cells {o[0]/R:.0f} steps {o[1]/R:.1f} skips {o[2]/R:.1f} (max {o[7]}) "
           f"lean-refused {o[6]/max(o[2],1):.4f} cost {(o[1] + 5.8 * o[2]) / R:.0f}")
+    lib.small_out.restype = C.c_uint64
+    print(f"   steps in empty bricks with a cube below the skip minimum: {lib.small_out() / R:.1f} per ray")
     cr = np.zeros(16, np.uint64); lib.cross_out.argtypes = [V]; lib.cross_out(cr.ctypes.data)
     print("   lean refusals by binade crossings (max over axes):", cr[:10])
