@@ -303,6 +303,7 @@ constexpr uint32_t kMinCube = VPX_MIN_CUBE;
 // 0: solid cell, 1: empty cell (step), 2: empty brick with a distance-field cube of at
 // least kMinCube bricks (skip it: df_box).  The level words are cached by key; the l2 and
 // l1 loads are independent, so a brick change costs one load latency.
+template <uint32_t MINC = kMinCube>
 VPX_HD int classify(Walk& w, const GridView& g) {
     const uint32_t X = w.X, Y = w.Y, Z = w.Z;
     const uint32_t k2 = pack3(X >> 4, Y >> 4, Z >> 4);
@@ -316,7 +317,7 @@ VPX_HD int classify(Walk& w, const GridView& g) {
         w.m1 = load_mask(g.l1, blk_index(X >> 2, Y >> 2, Z >> 2, g.nb2));
     }
     const uint32_t bb = ((X >> 2) & 3u) | (((Y >> 2) & 3u) << 2) | (((Z >> 2) & 3u) << 4);
-    if (!((w.m2 >> bb) & 1ull)) return ((uint32_t)(w.m1 >> w.osh) & 255u) >= kMinCube ? 2 : 1;
+    if (!((w.m2 >> bb) & 1ull)) return ((uint32_t)(w.m1 >> w.osh) & 255u) >= MINC ? 2 : 1;
     const uint32_t cb = (X & 3u) | ((Y & 3u) << 2) | ((Z & 3u) << 4);
     return ((w.m1 >> cb) & 1ull) ? 0 : 1;
 }
@@ -423,139 +424,15 @@ VPX_HD int skip_box(Walk& w, const uint32_t lo[3], const uint32_t hi[3], float b
     return 1;
 }
 
-// ---------------------------------------------------------------- fast path
-// The common case of skip_box in straight-line integer code: every axis sequence is in
-// closed form over the box (at most one binade change, no tie, not stuck).  Same results.
-
-// Closed-form parameters of A -> fl(A + d) in A's binade: A = b*u, fl(A + d) = A + c*u.
-VPX_HD bool seg_params(float a, float d, uint32_t& b, uint32_t& c, uint32_t& e) {
-    const uint32_t ab = fbits(a), db = fbits(d);
-    const uint32_t ea = ab >> 23, ed = db >> 23;
-    if (ea - 1u >= 254u || ed - 1u >= 254u || ed >= ea) return false;  // sign/zero/denormal/inf/nan, d >= 2^E
-    const uint32_t sh = ea - ed;
-    if (sh > 24u) return false;  // stuck (d < u/2)
-    const uint32_t md = (db & 0x7fffffu) | 0x800000u;
-    const uint32_t rem = md & ((1u << sh) - 1u), half = 1u << (sh - 1u);
-    c = (md >> sh) + (rem > half ? 1u : 0u);
-    b = (ab & 0x7fffffu) | 0x800000u;
-    e = ea;
-    return rem != half && c != 0u;
-}
-
-// A(0..last) as up to two closed-form segments: i <= m1 in A(0)'s binade, i > m1 after the
-// plain IEEE step m1 -> m1+1 (only when last > m1).
-struct Seq2 {
-    uint32_t b1, c1, e1, m1;
-    uint32_t b2, c2, e2;
-};
-
-VPX_HD bool seq2_init(float a, float d, uint32_t last, Seq2& q) {  // last <= 1023
-    if (!seg_params(a, d, q.b1, q.c1, q.e1)) return false;
-    const uint32_t room = 0xffffffu - q.b1;
-    q.b2 = q.c2 = q.e2 = 0u;
-    if ((uint64_t)last * q.c1 <= room) {
-        q.m1 = last;
-        return true;
-    }
-    q.m1 = udiv(room, q.c1);
-    const float A = seg_value(q.b1 + q.m1 * q.c1, q.e1) + d;
-    if (!seg_params(A, d, q.b2, q.c2, q.e2)) return false;
-    return (uint64_t)(last - q.m1 - 1u) * q.c2 <= 0xffffffu - q.b2;
-}
-
-VPX_HD float seq2_at(const Seq2& q, uint32_t i) {
-    const bool one = i <= q.m1;
-    const uint32_t b = one ? q.b1 + i * q.c1 : q.b2 + (i - q.m1 - 1u) * q.c2;
-    return seg_value(b, one ? q.e1 : q.e2);
-}
-
-// ceil(p / c) for p <= 2^24 + 1, c >= 1, from q ~ p / c (relative error < 2^-20); exact
-// when <= 1024, otherwise some value > 1024.
-VPX_HD uint32_t ceil_div_q(uint32_t p, uint32_t c, float q) {
-    if (!(q < 1024.0f)) return 1025u;
-    uint32_t j = (uint32_t)q + 1u;  // q's error is far below 1: j is ceil(p/c) or one off
-    if ((uint64_t)(j - 1u) * c >= p) --j;
-    if ((uint64_t)j * c < p) ++j;
-    return j;
-}
-
-VPX_HD uint32_t ceil_div_small(uint32_t p, uint32_t c) {
-#if defined(__HIP_DEVICE_COMPILE__)
-    return ceil_div_q(p, c, (float)p * __builtin_amdgcn_rcpf((float)c));
-#else
-    return ceil_div_q(p, c, (float)p / (float)c);
-#endif
-}
-
-// First j >= 0 with (b + j c) u not below T (strict: >= T, else > T), T > 0 finite or inf.
-VPX_HD uint32_t seg_first(uint32_t b, uint32_t c, uint32_t e, uint32_t tb, bool strict) {
-    const uint32_t te = tb >> 23;
-    if (te < e) return 0u;
-    if (te > e) return 1025u;  // every term of the binade is below T
-    const uint32_t need = ((tb & 0x7fffffu) | 0x800000u) + (strict ? 0u : 1u);
-    return need <= b ? 0u : ceil_div_small(need - b, c);
-}
-
-// #{ i <= last : A(i) below T } clamped to `cap` (A is increasing).
-VPX_HD uint32_t seq2_count(const Seq2& q, float T, bool strict, uint32_t cap) {
-    const uint32_t tb = fbits(T);
-    uint32_t f = seg_first(q.b1, q.c1, q.e1, tb, strict);
-    if (f > q.m1 && q.e2 != 0u) {
-        const uint32_t f2 = seg_first(q.b2, q.c2, q.e2, tb, strict);
-        f = q.m1 + 1u + (f2 < 1025u ? f2 : 1025u);
-    }
-    return f < cap ? f : cap;
-}
-
-// skip_box for boxes whose three sequences pass seq2_init; 2 = use skip_box.
-VPX_HD int skip_box_fast(Walk& w, const uint32_t lo[3], const uint32_t hi[3], float bound, uint32_t& cells) {
-    const uint32_t ex = w.sx > 0 ? hi[0] - w.X + 1u : w.X - lo[0] + 1u;
-    const uint32_t ey = w.sy > 0 ? hi[1] - w.Y + 1u : w.Y - lo[1] + 1u;
-    const uint32_t ez = w.sz > 0 ? hi[2] - w.Z + 1u : w.Z - lo[2] + 1u;
-    Seq2 qx, qy, qz;
-    const bool okx = seq2_init(w.tx, w.dx, ex - 1u, qx);
-    const bool oky = seq2_init(w.ty, w.dy, ey - 1u, qy);
-    const bool okz = seq2_init(w.tz, w.dz, ez - 1u, qz);
-    if (!(okx && oky && okz)) return 2;
-    // the leaving event: smallest A_k(e_k - 1), ties -> z, then y, then x
-    const float Vx = seq2_at(qx, ex - 1u), Vy = seq2_at(qy, ey - 1u), Vz = seq2_at(qz, ez - 1u);
-    const int a = (Vz <= Vx && Vz <= Vy) ? 2 : (Vy <= Vx ? 1 : 0);
-    const float vs = a == 2 ? Vz : (a == 1 ? Vy : Vx);
-    // events of the other axes before it (axis k precedes a on ties iff k > a)
-    const uint32_t nx = a == 0 ? ex - 1u : seq2_count(qx, vs, true, ex - 1u);
-    const uint32_t ny = a == 1 ? ey - 1u : seq2_count(qy, vs, a == 2, ey - 1u);
-    const uint32_t nz = a == 2 ? ez - 1u : seq2_count(qz, vs, false, ez - 1u);
-    if (vs < bound) {
-        float tl = w.t;
-        bool moved = false;
-        if (nx) tl = seq2_at(qx, nx - 1u), moved = true;
-        if (ny) {
-            const float p = seq2_at(qy, ny - 1u);
-            tl = moved ? (tl < p ? p : tl) : p;
-            moved = true;
-        }
-        if (nz) {
-            const float p = seq2_at(qz, nz - 1u);
-            tl = moved ? (tl < p ? p : tl) : p;
-        }
-        w.t = tl;
-        w.tx = seq2_at(qx, nx), w.ty = seq2_at(qy, ny), w.tz = seq2_at(qz, nz);
-        w.X += nx * (uint32_t)w.sx;
-        w.Y += ny * (uint32_t)w.sy;
-        w.Z += nz * (uint32_t)w.sz;
-        cells += nx + ny + nz;
-        return 0;
-    }
-    cells += 1u + seq2_count(qx, bound, true, nx) + seq2_count(qy, bound, true, ny) + seq2_count(qz, bound, true, nz);
-    return 1;
-}
-
 // ------------------------------------------------------- lean tier
-// skip_box in straight-line integer code for the common case: every axis sequence is in
-// closed form over the box with at most one binade change (no tie, not stuck).  Anything
-// else returns 2 and the lane takes skip_any later (the caller batches those lanes).
-// Boxes span at most 1024 cells per axis.  Every product formed is below 2^32 with both
-// factors below 2^24, so it uses the full-rate 24-bit multiplier.
+// skip_box in straight-line integer code.  Each axis's sequence is put in closed form as
+// up to two segments (its own binade, then the next one after one plain IEEE step), and
+// the box is first clipped, per axis, to the events those two segments reach.  So every
+// box is taken: where a sequence crosses more binades (rays that start near t = 0) the
+// lane skips the clipped part now and the rest in later iterations.  Only a non-positive
+// or NaN head is refused (2: the caller takes a plain step instead).  Boxes span at most
+// 1024 cells per axis; every product formed is below 2^32 with both factors below 2^24,
+// so it uses the full-rate 24-bit multiplier.
 
 VPX_HD uint32_t mul24(uint32_t a, uint32_t b) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -564,6 +441,21 @@ VPX_HD uint32_t mul24(uint32_t a, uint32_t b) {
     return a * b;
 #endif
 }
+
+// a * b + c with a, b < 2^24 (full-rate v_mad_u32_u24; left to itself the compiler picks
+// the quarter-rate 64-bit multiply-add for these).
+VPX_HD uint32_t mad24(uint32_t a, uint32_t b, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    uint32_t r;
+    asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+#else
+    return a * b + c;
+#endif
+}
+
+// The lean tier below names every operand before selecting between them: a conditional
+// whose arm holds arithmetic becomes a divergent branch on the device, a select does not.
 
 VPX_HD float rcp_approx(float x) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -597,83 +489,91 @@ VPX_HD bool seg_params_nb(float a, float d, uint32_t& b, uint32_t& c, uint32_t& 
 // ceil(p / c) clamped to 1025 (p <= 2^24 + 1, 1 <= c < 2^24).  q's error is far below 1
 // (relative 2^-22, q <= 1024.5), so one correction each way makes it exact; the products
 // stay below 2^25 (j ~ p / c, or c < 2^14 when clamped).
-VPX_HD uint32_t ceil_div_cap(uint32_t p, uint32_t c) {
-    const float q = (float)p * rcp_approx((float)c);
+VPX_HD uint32_t ceil_div_cap_r(uint32_t p, uint32_t c, float rc) {  // rc ~ 1/c (2^-22 relative)
+    const float q = (float)p * rc;
     uint32_t j = (uint32_t)(q < 1024.5f ? q : 1024.5f) + 1u;  // ceil(p/c) or one off, <= 1025
     j -= mul24(j - 1u, c) >= p ? 1u : 0u;
     j += mul24(j, c) < p ? 1u : 0u;
     return j < 1025u ? j : 1025u;
 }
+VPX_HD uint32_t ceil_div_cap(uint32_t p, uint32_t c) { return ceil_div_cap_r(p, c, rcp_approx((float)c)); }
 
 // floor(r / c) clamped to 1024 (r < 2^24, 1 <= c < 2^24).
-VPX_HD uint32_t floor_div_cap(uint32_t r, uint32_t c) {
-    const float q = (float)r * rcp_approx((float)c);
+VPX_HD uint32_t floor_div_cap_r(uint32_t r, uint32_t c, float rc) {
+    const float q = (float)r * rc;
     uint32_t m = (uint32_t)(q < 1024.5f ? q : 1024.5f);
-    m -= (m && mul24(m, c) > r) ? 1u : 0u;
+    m -= ((m != 0u) & (mul24(m, c) > r)) ? 1u : 0u;
     m += mul24(m + 1u, c) <= r ? 1u : 0u;
     return m < 1024u ? m : 1024u;
 }
+VPX_HD uint32_t floor_div_cap(uint32_t r, uint32_t c) { return floor_div_cap_r(r, c, rcp_approx((float)c)); }
 
 // First j >= 0 with (b + j c) u not below T (strict: >= T, else > T), clamped to 1025.
 VPX_HD uint32_t seg_first_cap(uint32_t b, uint32_t c, uint32_t e, float T, bool strict) {
     const uint32_t tb = fbits(T), te = tb >> 23;
     const uint32_t need = ((tb & 0x7fffffu) | 0x800000u) + (strict ? 0u : 1u);
-    const uint32_t f = need <= b ? 0u : ceil_div_cap(need - b, c);
+    const uint32_t q = ceil_div_cap(need - b, c);
+    const uint32_t f = need <= b ? 0u : q;
     return te == e ? f : (te < e ? 0u : 1025u);
 }
 
 // One axis over the box: A(0..l) as one or two closed-form segments: A(i) = (b1 + i c1) u1
 // for i <= m1, then (b2 + (i - m1 - 1) c2) u2 after the plain IEEE step m1 -> m1 + 1.
 struct Axis {
-    uint32_t b1, c1, e1, m1, b2, c2, e2;
+    uint32_t b1, c1, e1, m1, b2, c2, e2, l;
 };
 
-VPX_HD bool axis_init(float h, float d, uint32_t l, Axis& a) {
+// l = the events wanted inside the box, clipped to what the two segments reach (0 when
+// not even the first applies: then only A(0) = h is read).
+VPX_HD void axis_setup(float h, float d, uint32_t l, Axis& a) {
     const bool ok1 = seg_params_nb(h, d, a.b1, a.c1, a.e1);
-    // A(i), 1 <= i <= m1, stay below 2^24 u (a tie base may be 2^24 itself: m1 = 0)
+    // A(i), 1 <= i <= fit1, stay below 2^24 u (a tie base may be 2^24 itself: fit1 = 0)
     const uint32_t room = a.b1 <= 0xffffffu ? 0xffffffu - a.b1 : 0u;
-    const uint32_t fit1 = floor_div_cap(room, a.c1 | 1u);  // last i with i c1 <= room (l <= 1023)
-    const bool cross = l > fit1;
-    a.m1 = cross ? fit1 : l;
-    const float Am = a.m1 ? bitsf((a.e1 << 23) | ((a.b1 + mul24(a.m1, a.c1)) & 0x7fffffu)) : h;
-    const float A = Am + d;  // the plain IEEE step into the next binade
+    const uint32_t fit1 = floor_div_cap(room, a.c1 ? a.c1 : 1u);  // (c1 == 0: not ok1)
+    const uint32_t amc = (a.e1 << 23) | (mad24(fit1, a.c1, a.b1) & 0x7fffffu);
+    const uint32_t am = fit1 ? amc : fbits(h);
+    const float A = bitsf(am) + d;  // the plain IEEE step into the next binade
     uint32_t b2;
     const bool ok2 = seg_params_nb(A, d, b2, a.c2, a.e2);
-    // the second segment starts at A itself: its closed form must hold from j = 0
-    const bool exact2 = b2 == ((fbits(A) & 0x7fffffu) | 0x800000u);
+    const bool exact2 = b2 == ((fbits(A) & 0x7fffffu) | 0x800000u);  // closed form from j = 0
     a.b2 = b2;
-    const uint32_t room2 = a.b2 <= 0xffffffu ? 0xffffffu - a.b2 : 0u;
-    const bool fit2 = l - a.m1 - 1u <= floor_div_cap(room2, a.c2 | 1u);
-    // no event inside the box (l == 0): only A(0) = h is read
-    return (h > 0.0f) & (d > 0.0f) & (l == 0u || (ok1 & (!cross || (ok2 & exact2 & fit2))));
+    const uint32_t room2 = b2 <= 0xffffffu ? 0xffffffu - b2 : 0u;
+    const uint32_t fit2 = floor_div_cap(room2, a.c2 ? a.c2 : 1u);
+    const uint32_t lim = ok1 ? ((ok2 & exact2) ? fit1 + 1u + fit2 : fit1) : 0u;
+    a.l = l < lim ? l : lim;
+    a.m1 = a.l < fit1 ? a.l : fit1;
 }
 
 VPX_HD float axis_at(const Axis& a, float h, uint32_t i) {
     const bool one = i <= a.m1;
-    const uint32_t b = one ? a.b1 + mul24(i, a.c1) : a.b2 + mul24(i - a.m1 - 1u, a.c2);
-    const float v = bitsf(((one ? a.e1 : a.e2) << 23) | (b & 0x7fffffu));
-    return i ? v : h;
+    const uint32_t b1 = mad24(i, a.c1, a.b1), b2 = mad24(i - a.m1 - 1u, a.c2, a.b2);
+    const uint32_t v = ((one ? a.e1 : a.e2) << 23) | ((one ? b1 : b2) & 0x7fffffu);
+    return bitsf(i ? v : fbits(h));
 }
 
-// #{ i < cap : A(i) below T } (A increasing), cap <= 1023.
+// #{ i < cap : A(i) below T } (A increasing), cap <= a.l.  T's binade picks the segment.
 VPX_HD uint32_t axis_count(const Axis& a, float h, float T, bool strict, uint32_t cap) {
     const bool h_below = strict ? h < T : h <= T;
-    uint32_t f1 = seg_first_cap(a.b1, a.c1, a.e1, T, strict);
-    f1 = h_below ? (f1 > 1u ? f1 : 1u) : 0u;  // index 0 is h itself
-    const uint32_t f2 = a.m1 + 1u + seg_first_cap(a.b2, a.c2, a.e2, T, strict);
-    const uint32_t f = f1 > a.m1 ? f2 : f1;
+    const bool s2 = (fbits(T) >> 23) > a.e1;  // every A(1..m1) is below T
+    uint32_t f = seg_first_cap(s2 ? a.b2 : a.b1, s2 ? a.c2 : a.c1, s2 ? a.e2 : a.e1, T, strict);
+    f = s2 ? a.m1 + 1u + f : (f < a.m1 + 1u ? f : a.m1 + 1u);
+    f = h_below ? (f > 1u ? f : 1u) : 0u;  // index 0 is h itself
     return f < cap ? f : cap;
 }
 
-VPX_HD int skip_box_fast1(Walk& w, const uint32_t lo[3], const uint32_t hi[3], float bound, uint32_t& cells) {
-    const uint32_t lx = (w.sx > 0 ? hi[0] - w.X : w.X - lo[0]);  // events inside the box, <= 1023
-    const uint32_t ly = (w.sy > 0 ? hi[1] - w.Y : w.Y - lo[1]);
-    const uint32_t lz = (w.sz > 0 ? hi[2] - w.Z : w.Z - lo[2]);
+// Cross the empty box [lo, hi] around the current cell, clipped per axis as above (lo / hi
+// receive the clipped box).  0: landed just before the event that leaves the clipped box
+// (cells += skipped visits); 1: the walk ends inside it (cells += visits); 2: refused.
+VPX_HD int skip_box_lean(Walk& w, uint32_t lo[3], uint32_t hi[3], float bound, uint32_t& cells) {
+    if (!((w.tx > 0.0f) & (w.ty > 0.0f) & (w.tz > 0.0f))) return 2;
     Axis ax, ay, az;
-    const bool okx = axis_init(w.tx, w.dx, lx, ax);
-    const bool oky = axis_init(w.ty, w.dy, ly, ay);
-    const bool okz = axis_init(w.tz, w.dz, lz, az);
-    if (!(okx && oky && okz)) return 2;
+    axis_setup(w.tx, w.dx, w.sx > 0 ? hi[0] - w.X : w.X - lo[0], ax);
+    axis_setup(w.ty, w.dy, w.sy > 0 ? hi[1] - w.Y : w.Y - lo[1], ay);
+    axis_setup(w.tz, w.dz, w.sz > 0 ? hi[2] - w.Z : w.Z - lo[2], az);
+    const uint32_t lx = ax.l, ly = ay.l, lz = az.l;
+    if (w.sx > 0) hi[0] = w.X + lx; else lo[0] = w.X - lx;
+    if (w.sy > 0) hi[1] = w.Y + ly; else lo[1] = w.Y - ly;
+    if (w.sz > 0) hi[2] = w.Z + lz; else lo[2] = w.Z - lz;
     const float Vx = axis_at(ax, w.tx, lx), Vy = axis_at(ay, w.ty, ly), Vz = axis_at(az, w.tz, lz);
     const int a = (Vz <= Vx && Vz <= Vy) ? 2 : (Vy <= Vx ? 1 : 0);
     const float vs = a == 2 ? Vz : (a == 1 ? Vy : Vx);
@@ -701,7 +601,7 @@ VPX_HD int skip_box_fast1(Walk& w, const uint32_t lo[3], const uint32_t hi[3], f
         cells += nx + ny + nz;
         return 0;
     }
-    // case B: the counts relative to the leaving event bound the counts below `bound`
+    // the counts relative to the leaving event bound the counts below `bound`
     const uint32_t cx = a == 0 ? lx : axis_count(ax, w.tx, vs, true, lx);
     const uint32_t cy = a == 1 ? ly : axis_count(ay, w.ty, vs, a == 2, ly);
     const uint32_t cz = a == 2 ? lz : axis_count(az, w.tz, vs, false, lz);
@@ -709,66 +609,9 @@ VPX_HD int skip_box_fast1(Walk& w, const uint32_t lo[3], const uint32_t hi[3], f
     return 1;
 }
 
-// Largest l for which axis_init(h, d, l) holds (the events the two closed-form segments
-// reach, <= 2048); 0 when not even the first segment applies.
-VPX_HD uint32_t lean_limit(float h, float d) {
-    uint32_t b1, c1, e1, b2, c2, e2;
-    const bool ok1 = seg_params_nb(h, d, b1, c1, e1);
-    const uint32_t room = b1 <= 0xffffffu ? 0xffffffu - b1 : 0u;
-    const uint32_t fit1 = floor_div_cap(room, c1 | 1u);
-    const float Am = fit1 ? bitsf((e1 << 23) | ((b1 + mul24(fit1, c1)) & 0x7fffffu)) : h;
-    const float A = Am + d;
-    const bool ok2 = seg_params_nb(A, d, b2, c2, e2);
-    const bool exact2 = b2 == ((fbits(A) & 0x7fffffu) | 0x800000u);
-    const uint32_t room2 = b2 <= 0xffffffu ? 0xffffffu - b2 : 0u;
-    const uint32_t fit2 = floor_div_cap(room2, c2 | 1u);
-    return ((h > 0.0f) & (d > 0.0f) & ok1) ? ((ok2 & exact2) ? fit1 + 1u + fit2 : fit1) : 0u;
-}
-
-// The largest sub-box of [lo, hi] around the current cell that the lean tier accepts on
-// every axis's sequence (it may still refuse a tie or a stuck sequence).
-VPX_HD void lean_clip(const Walk& w, uint32_t lo[3], uint32_t hi[3]) {
-    const float h[3] = {w.tx, w.ty, w.tz}, d[3] = {w.dx, w.dy, w.dz};
-    const int32_t sg[3] = {w.sx, w.sy, w.sz};
-    const uint32_t c[3] = {w.X, w.Y, w.Z};
-    for (int k = 0; k < 3; ++k) {
-        const uint32_t lim = lean_limit(h[k], d[k]);
-        if (sg[k] > 0) hi[k] = hi[k] - c[k] > lim ? c[k] + lim : hi[k];
-        else lo[k] = c[k] - lo[k] > lim ? c[k] - lim : lo[k];
-    }
-}
-
-// skip_box_fast, else the general skip_box.
-VPX_HD int skip_any(Walk& w, const uint32_t lo[3], const uint32_t hi[3], float bound, uint32_t& cells) {
-    int r = skip_box_fast1(w, lo, hi, bound, cells);
-    if (r != 2) return r;
-    r = skip_box_fast(w, lo, hi, bound, cells);
-    return r != 2 ? r : skip_box(w, lo, hi, bound, cells);
-}
-
-// Resumable form: at most `budget` loop iterations.  0 = not finished, 1 = solid cell
-// reached (w.t / w.X,Y,Z describe it), 2 = finished without a solid cell.
-VPX_HD int walk_skip_some(const GridView& g, Walk& w, float bound, uint32_t& cells, int budget) {
-    for (int it = 0; it < budget; ++it) {
-        if (!(w.t < bound)) return 2;
-        const int cls = classify(w, g);
-        if (cls == 0) {
-            ++cells;
-            return 1;
-        }
-        if (cls == 2) {
-            uint32_t lo[3], hi[3];
-            df_box(w, g.n, lo, hi);
-            if (skip_any(w, lo, hi, bound, cells) == 1) return 2;
-        }
-        ++cells;
-        if (!step1(w, g.n)) return 2;
-    }
-    return 0;
-}
-
 // Scene::FindNearest (MODE nearest) / Scene::IsOccluded walk from an initialised state.
-// Returns true at the first solid cell (w.t / w.X,Y,Z describe it).  Exact.
+// Returns true at the first solid cell (w.t / w.X,Y,Z describe it).  Exact.  The device
+// walker (walk_wave, vpx_trace.hpp) runs the same per-lane sequence.
 VPX_HD bool walk_skip(const GridView& g, Walk& w, float bound, uint32_t& cells) {
     for (;;) {
         if (!(w.t < bound)) return false;
@@ -780,7 +623,7 @@ VPX_HD bool walk_skip(const GridView& g, Walk& w, float bound, uint32_t& cells) 
         if (cls == 2) {
             uint32_t lo[3], hi[3];
             df_box(w, g.n, lo, hi);
-            if (skip_any(w, lo, hi, bound, cells) == 1) return false;
+            if (skip_box_lean(w, lo, hi, bound, cells) == 1) return false;
         }
         ++cells;  // visit the (empty) current cell
         if (!step1(w, g.n)) return false;

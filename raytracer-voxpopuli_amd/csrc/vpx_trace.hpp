@@ -281,7 +281,7 @@ __device__ __forceinline__ skip::Walk to_walk(const Dda& s) {
 // classify / skip_box / step1 as skip::walk_skip (so results are identical), but the long
 // skip_box is executed in batches — only when few lanes of the wave still want to take
 // plain cell steps — instead of inside every step iteration of the wave.
-// Skip-phase weights (measured on C1 / C3: FindNearest 2, IsOccluded 4).
+// Skip-phase weights (measured on C1 / C3 / C2: FindNearest 2, IsOccluded 4, bounces 2).
 #ifndef VPX_SKIPW_NEAREST
 #define VPX_SKIPW_NEAREST 2
 #endif
@@ -289,12 +289,27 @@ __device__ __forceinline__ skip::Walk to_walk(const Dda& s) {
 #define VPX_SKIPW_BOUNCE 2
 #endif
 #ifndef VPX_SKIPW_SHADOW
-#define VPX_SKIPW_SHADOW 8
+#define VPX_SKIPW_SHADOW 4
 #endif
 #ifndef VPX_STEP_THRESHOLD
 #define VPX_STEP_THRESHOLD 16
 #endif
 constexpr uint32_t kStepThreshold = VPX_STEP_THRESHOLD;
+#ifndef VPX_STEP_UNROLL
+#define VPX_STEP_UNROLL 2
+#endif
+// Smallest distance-field cube worth a skip per walk kind (C1, ms: FindNearest 0.430 with
+// 2 / 0.435 with 1; IsOccluded 0.383 with 2 / 0.354 with 1).
+#ifndef VPX_MINC_NEAREST
+#define VPX_MINC_NEAREST 2
+#endif
+#ifndef VPX_MINC_BOUNCE
+#define VPX_MINC_BOUNCE 2
+#endif
+#ifndef VPX_MINC_SHADOW
+#define VPX_MINC_SHADOW 1
+#endif
+constexpr int kStepUnroll = VPX_STEP_UNROLL;  // cell steps per step-phase iteration
 
 #ifdef VPX_ASM_MARKS  // analysis builds only: label the walk phases in the ISA listing
 #define VPX_MARK(s) asm volatile("; MARK " s)
@@ -312,35 +327,11 @@ __device__ unsigned long long g_phase[32];
 #endif
 
 // Lane modes: kStep wants a cell step, kSkip an empty-box skip (the distance-field cube
-// of its brick, skip::df_box), kMiss / kHit are done.  Phases are wave-uniform: cell steps
-// while enough lanes want one (see SKIPW), then the waiting lanes skip together.  Each lane runs exactly
-// skip::walk_skip's sequence (the reference's cells with the reference's floats).
-// Skip tiers: with LEAN the straight-line lean tier (skip_box_fast1) goes first, else
-// skip_box_fast (closed form, <= 1 binade change), then the general skip_box.
-#ifndef VPX_LEAN_NEAREST
-#define VPX_LEAN_NEAREST 1
-#endif
-#ifndef VPX_LEAN_SHADOW
-#define VPX_LEAN_SHADOW 1
-#endif
-
-// CLIP: where the lean tier refuses the box, skip the largest sub-box it accepts first
-// (lean_clip) and leave the rest of the box to later iterations; the general tier then
-// only sees ties and stuck sequences.
-// Measured on C1 / C3 (ms per frame): shadow rays 0.78 -> 0.67 / 10.8 -> 8.3 with CLIP;
-// primary rays (rarely refused) 0.50 -> 0.53 with it.  Bounce rays start on a surface like
-// shadow rays.
-#ifndef VPX_CLIP_PRIMARY
-#define VPX_CLIP_PRIMARY 0
-#endif
-#ifndef VPX_CLIP_BOUNCE
-#define VPX_CLIP_BOUNCE 1
-#endif
-#ifndef VPX_CLIP_SHADOW
-#define VPX_CLIP_SHADOW 1
-#endif
-
-template <bool LEAN, int PHK = 0, uint32_t SKIPW = 0, bool CLIP = false>
+// of its brick, skip::df_box, through skip::skip_box_lean), kMiss / kHit are done.
+// Phases are wave-uniform: cell steps while enough lanes want one (see SKIPW), then the
+// waiting lanes skip together.  Each lane runs exactly skip::walk_skip's sequence (the
+// reference's cells with the reference's floats).
+template <int PHK = 0, uint32_t SKIPW = 0, uint32_t MINC = skip::kMinCube>
 __device__ __forceinline__ bool walk_wave(const skip::GridView& g, skip::Walk& w, float bound, uint32_t& cells) {
     enum : int { kStep = 0, kSkip = 1, kMiss = 2, kHit = 3 };
     int mode = kStep;
@@ -357,19 +348,22 @@ __device__ __forceinline__ bool walk_wave(const skip::GridView& g, skip::Walk& w
                 break;
             VPX_PH(++ns; ls += __popcll(stepping);)
             VPX_MARK("step body");
-            if (mode == kStep) {
-                if (!(w.t < bound)) {
-                    mode = kMiss;
-                } else {
-                    const int cls = skip::classify(w, g);
-                    if (cls == 0) {
-                        ++cells;
-                        mode = kHit;
-                    } else if (cls == 2) {
-                        mode = kSkip;
+#pragma unroll
+            for (int u = 0; u < kStepUnroll; ++u) {
+                if (mode == kStep) {
+                    if (!(w.t < bound)) {
+                        mode = kMiss;
                     } else {
-                        ++cells;
-                        if (!skip::step1(w, g.n)) mode = kMiss;
+                        const int cls = skip::classify<MINC>(w, g);
+                        if (cls == 0) {
+                            ++cells;
+                            mode = kHit;
+                        } else if (cls == 2) {
+                            mode = kSkip;
+                        } else {
+                            ++cells;
+                            if (!skip::step1(w, g.n)) mode = kMiss;
+                        }
                     }
                 }
             }
@@ -386,17 +380,9 @@ __device__ __forceinline__ bool walk_wave(const skip::GridView& g, skip::Walk& w
         if (mode == kSkip) {
             uint32_t lo[3], hi[3];
             skip::df_box(w, g.n, lo, hi);
-            int sr = LEAN ? skip::skip_box_fast1(w, lo, hi, bound, cells) : 2;
-            if (LEAN && CLIP && sr == 2) {
-                skip::lean_clip(w, lo, hi);
-                sr = skip::skip_box_fast1(w, lo, hi, bound, cells);
-            }
-            if (!LEAN && sr == 2) sr = skip::skip_box_fast(w, lo, hi, bound, cells);  // (a subset of the lean tier)
-            VPX_PH(const uint64_t t2 = __builtin_amdgcn_s_memtime(); fb += __popcll(__ballot(sr == 2));)
-            VPX_MARK("general tier");
-            if (sr == 2) sr = skip::skip_box(w, lo, hi, bound, cells);
-            VPX_MARK("general tier end");
-            VPX_PH(cf += __builtin_amdgcn_s_memtime() - t2;)
+            const int sr = skip::skip_box_lean(w, lo, hi, bound, cells);  // 2 (refused): a plain step
+            VPX_MARK("skip end");
+            VPX_PH(fb += __popcll(__ballot(sr == 2));)
             if (sr == 1) {
                 mode = kMiss;
             } else {
@@ -572,7 +558,7 @@ struct Counters {
 
 // Renderer::FindNearest, renderer.cpp:946-1018.  Linear loop over the volumes with the
 // SSE transforms; a later volume wins only with a strictly smaller t (ties -> lowest index).
-template <uint32_t SKIPW = VPX_SKIPW_NEAREST, bool CLIP = VPX_CLIP_PRIMARY != 0>
+template <uint32_t SKIPW = VPX_SKIPW_NEAREST, uint32_t MINC = VPX_MINC_NEAREST>
 __device__ __forceinline__ int32_t find_nearest(const SceneView& sv, Ray& r, Counters& k) {
     int32_t vox = -2;
     ++k.nearest;
@@ -586,7 +572,7 @@ __device__ __forceinline__ int32_t find_nearest(const SceneView& sv, Ray& r, Cou
         Dda s;
         if (!dda_setup(vol, g.n, o, s)) continue;
         skip::Walk w = to_walk(s);
-        if (walk_wave<VPX_LEAN_NEAREST != 0, 0, SKIPW, CLIP>(grid_view(g), w, r.t, k.cells)) {
+        if (walk_wave<0, SKIPW, MINC>(grid_view(g), w, r.t, k.cells)) {
             r.t = w.t;
             r.N = normal_voxel(o, w.t, g.n, vol.matrix);
             r.mat = g.cells[(uint64_t)w.X + (uint64_t)w.Y * g.n + (uint64_t)w.Z * ((uint64_t)g.n * g.n)];
@@ -620,8 +606,7 @@ __device__ __forceinline__ bool is_occluded(const SceneView& sv, const Ray& r, C
         Dda s;
         if (!dda_setup(vol, g.n, o, s)) continue;
         skip::Walk w = to_walk(s);
-        if (walk_wave<VPX_LEAN_SHADOW != 0, 16, VPX_SKIPW_SHADOW, VPX_CLIP_SHADOW != 0>(grid_view(g), w, r.t, k.cells))
-            return true;  // first solid cell, t < bound
+        if (walk_wave<16, VPX_SKIPW_SHADOW, VPX_MINC_SHADOW>(grid_view(g), w, r.t, k.cells)) return true;  // first solid cell, t < bound
     }
     for (uint32_t i = 0; i < sv.num_spheres; ++i)
         if (sphere_is_hit(sv.spheres[i], r)) return true;

@@ -1,5 +1,6 @@
 // Exhaustive-random check of vpx::skip::jump / count_below against plain IEEE accumulation.
 // Build: g++ -O2 -std=c++17 -ffp-contract=off -I raytracer-voxpopuli_amd/csrc tests/native/skip_math_test.cpp
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -77,25 +78,32 @@ int udiv_check() {
 }
 static int _udiv = (udiv_check() ? (exit(1), 1) : 0);
 
-// (appended) ceil_div_q with perturbed quotients, as the device forms them (rcp * p)
+// (appended) ceil_div_cap / floor_div_cap with perturbed reciprocals, as the device forms
+// them (v_rcp_f32 is within 1 ulp)
 int ceil_check() {
     std::mt19937_64 r(11);
     long bad = 0;
     for (long i = 0; i < 20000000; ++i) {
         const uint32_t c = 1 + (uint32_t)(r() % ((i % 3) ? (1u << 23) : 64u));
-        const uint32_t p = 1 + (uint32_t)(r() % ((i % 2) ? (1u << 24) : (uint64_t)c * 70));
-        const double eps = ((double)(r() % 2001) - 1000.0) * 1e-9;
-        const float q = (float)(((double)p / c) * (1.0 + eps));
-        const uint64_t want = ((uint64_t)p + c - 1) / c;
-        const uint32_t got = vpx::skip::ceil_div_q(p, c, q);
-        if (want <= 1024 ? got != want : got <= 1024) { if (bad < 5) printf("ceil bad %u/%u got %u\n", p, c, got); ++bad; }
+        const uint32_t p = 1 + (uint32_t)(r() % ((i % 2) ? (1u << 24) : std::min<uint64_t>((uint64_t)c * 1100, 1u << 24)));
+        const double eps = ((double)(r() % 2001) - 1000.0) * 2.4e-10;  // +-2^-22 relative
+        const float rc = (float)((1.0 / c) * (1.0 + eps));
+        const uint64_t wc = ((uint64_t)p + c - 1) / c, wf = (uint64_t)p / c;
+        const uint32_t gc = vpx::skip::ceil_div_cap_r(p, c, rc);
+        const uint32_t gf = vpx::skip::floor_div_cap_r(p < (1u << 24) ? p : (1u << 24) - 1, c, rc);
+        const uint64_t wf2 = (uint64_t)(p < (1u << 24) ? p : (1u << 24) - 1) / c;
+        if (gc != (wc < 1025 ? wc : 1025) || gf != (wf2 < 1024 ? wf2 : 1024)) {
+            if (bad < 5) printf("div bad p=%u c=%u ceil %u/%llu floor %u/%llu\n", p, c, gc, (unsigned long long)wc, gf,
+                                (unsigned long long)wf);
+            ++bad;
+        }
     }
-    printf("ceil_div bad=%ld\n", bad);
+    printf("ceil/floor div bad=%ld\n", bad);
     return bad != 0;
 }
 static int _ceil = (ceil_check() ? (exit(1), 1) : 0);
 
-// (appended) skip_box_fast against the general skip_box on random and adversarial states
+// (appended) skip_box_lean against the general skip_box (on the box the lean tier clipped to)
 static float rnd_head(std::mt19937_64& r, std::uniform_real_distribution<double>& U, int kind) {
     switch (kind) {
         case 0: return (float)std::exp(std::log(1e-3) + U(r) * (std::log(8.0) - std::log(1e-3)));
@@ -138,38 +146,28 @@ int fast_check() {
         const float hmax = w.tx > w.ty ? (w.tx > w.tz ? w.tx : w.tz) : (w.ty > w.tz ? w.ty : w.tz);
         const int bk = (int)(r() % 4);
         const float bound = bk == 0 ? 1e34f : bk == 1 ? INFINITY : (float)(tmin + U(r) * (hmax * 4 - tmin));
-        Walk a = w, b = w, a1 = w;
-        uint32_t ca = 7, cb = 7, c1 = 7;
-        const int ra = skip_box_fast(a, lo, hi, bound, ca);
-        const int r1 = skip_box_fast1(a1, lo, hi, bound, c1);
+        Walk a1 = w, b1 = w;
+        uint32_t lo1[3] = {lo[0], lo[1], lo[2]}, hi1[3] = {hi[0], hi[1], hi[2]};
+        uint32_t c1 = 7, cb1 = 7;
+        const int r1 = skip_box_lean(a1, lo1, hi1, bound, c1);
         ++total;
-        if (r1 != 2) {
-            ++handled1;
-            Walk b1 = w;
-            uint32_t cb1 = 7;
-            const int rb1 = skip_box(b1, lo, hi, bound, cb1);
-            if (!(r1 == rb1 && c1 == cb1 && (r1 == 1 || !memcmp(&a1, &b1, sizeof(Walk))))) {
-                if (bad < 10)
-                    printf("fast1 mismatch r %d/%d cells %u/%u t %a/%a\n  in: X %u %u %u s %d %d %d lo %u %u %u hi %u %u %u t %a h %a %a %a d %a %a %a bound %a\n"
-                           "  out fast1: h %a %a %a XYZ %u %u %u | ref: h %a %a %a XYZ %u %u %u\n",
-                           r1, rb1, c1, cb1, a1.t, b1.t, w.X, w.Y, w.Z, w.sx, w.sy, w.sz, lo[0], lo[1], lo[2], hi[0], hi[1], hi[2], w.t,
-                           w.tx, w.ty, w.tz, w.dx, w.dy, w.dz, bound, a1.tx, a1.ty, a1.tz, a1.X, a1.Y, a1.Z, b1.tx, b1.ty, b1.tz, b1.X,
-                           b1.Y, b1.Z);
-                ++bad;
-            }
-        }
-        if (ra == 2) continue;
+        if (r1 == 2) continue;
         ++handled;
-        const int rb = skip_box(b, lo, hi, bound, cb);
-        const bool same = ra == rb && ca == cb && (ra == 1 || (!memcmp(&a, &b, sizeof(Walk))));
-        if (!same) {
+        bool clipped = false;
+        for (int k = 0; k < 3; ++k) clipped |= lo1[k] != lo[k] || hi1[k] != hi[k];
+        handled1 += !clipped;
+        const int rb1 = skip_box(b1, lo1, hi1, bound, cb1);
+        if (!(r1 == rb1 && c1 == cb1 && (r1 == 1 || !memcmp(&a1, &b1, sizeof(Walk))))) {
             if (bad < 10)
-                printf("fast mismatch r %d/%d cells %u/%u t %a/%a h (%a %a %a)/(%a %a %a) XYZ (%u %u %u)/(%u %u %u)\n", ra, rb, ca, cb, a.t, b.t,
-                       a.tx, a.ty, a.tz, b.tx, b.ty, b.tz, a.X, a.Y, a.Z, b.X, b.Y, b.Z);
+                printf("lean mismatch r %d/%d cells %u/%u t %a/%a\n  in: X %u %u %u s %d %d %d lo %u %u %u hi %u %u %u t %a h %a %a %a d %a %a %a bound %a\n"
+                       "  out lean: h %a %a %a XYZ %u %u %u | ref: h %a %a %a XYZ %u %u %u\n",
+                       r1, rb1, c1, cb1, a1.t, b1.t, w.X, w.Y, w.Z, w.sx, w.sy, w.sz, lo1[0], lo1[1], lo1[2], hi1[0], hi1[1], hi1[2], w.t,
+                       w.tx, w.ty, w.tz, w.dx, w.dy, w.dz, bound, a1.tx, a1.ty, a1.tz, a1.X, a1.Y, a1.Z, b1.tx, b1.ty, b1.tz, b1.X,
+                       b1.Y, b1.Z);
             ++bad;
         }
     }
-    printf("skip_box_fast: %ld/%ld handled (single-segment tier %ld), bad=%ld\n", handled, total, handled1, bad);
+    printf("skip_box_lean: %ld/%ld taken (%ld unclipped), bad=%ld\n", handled, total, handled1, bad);
     return bad != 0;
 }
 static int _fast = (fast_check() ? (exit(1), 1) : 0);

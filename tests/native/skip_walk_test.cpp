@@ -115,17 +115,19 @@ static void debug_walk(const GridView& g, Walk w, float bound) {
             df_box(w, g.n, lo, hi);
             Walk a = w, b = w;
             uint32_t ca = 0, cb = 0;
-            const int ra = skip_box_fast1(a, lo, hi, bound, ca), rb = skip_box(b, lo, hi, bound, cb);
+            const int ra = skip_box_lean(a, lo, hi, bound, ca), rb = skip_box(b, lo, hi, bound, cb);
             if (ra != 2 && (ra != rb || ca != cb || (ra == 0 && memcmp(&a, &b, sizeof(Walk))))) {
                 printf("  first bad skip: r %d/%d cells %u/%u X %u %u %u s %d %d %d lo %u %u %u hi %u %u %u\n"
-                       "   t %a h %a %a %a d %a %a %a bound %a\n   fast1 t %a h %a %a %a XYZ %u %u %u\n   ref   t %a h %a %a %a XYZ %u %u %u\n",
+                       "   t %a h %a %a %a d %a %a %a bound %a\n   lean t %a h %a %a %a XYZ %u %u %u\n   ref  t %a h %a %a %a XYZ %u %u %u\n",
                        ra, rb, ca, cb, w.X, w.Y, w.Z, w.sx, w.sy, w.sz, lo[0], lo[1], lo[2], hi[0], hi[1], hi[2], w.t, w.tx, w.ty,
                        w.tz, w.dx, w.dy, w.dz, bound, a.t, a.tx, a.ty, a.tz, a.X, a.Y, a.Z, b.t, b.tx, b.ty, b.tz, b.X, b.Y, b.Z);
                 return;
             }
-            uint32_t c = 0;
-            if (skip_box(w, lo, hi, bound, c) == 1) return;
+            if (ra == 2) goto step;
+            w = a;
+            if (ra == 1) return;
         }
+    step:
         if (!step1(w, g.n)) return;
     }
 }

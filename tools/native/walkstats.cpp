@@ -127,23 +127,32 @@ extern "C" void walk_sim(const uint8_t* cells, const uint64_t* l1, const uint64_
                 uint32_t lo[3], hi[3];
                 df_box(w, n, lo, hi);
                 if (slab) for (int q = 0; q < 3; ++q) lo[q] = slo[q], hi[q] = shi[q];
+                const uint32_t olo[3] = {lo[0], lo[1], lo[2]}, ohi[3] = {hi[0], hi[1], hi[2]};
                 Walk t = w;
                 uint32_t cc = 0;
-                if (skip_box_fast1(t, lo, hi, bound, cc) == 2) {
+                const int sr = skip_box_lean(t, lo, hi, bound, cc);
+                bool clipped = false;
+                for (int k = 0; k < 3; ++k) clipped |= lo[k] != olo[k] || hi[k] != ohi[k];
+                if (sr == 2 || clipped) {
                     ++out[6];
                     const float hh[3] = {w.tx, w.ty, w.tz}, dd[3] = {w.dx, w.dy, w.dz};
                     const int32_t sg[3] = {w.sx, w.sy, w.sz};
                     const uint32_t c3[3] = {w.X, w.Y, w.Z};
                     uint32_t worst = 0;
                     for (int k = 0; k < 3; ++k) {
-                        const uint32_t l = sg[k] > 0 ? hi[k] - c3[k] : c3[k] - lo[k];
+                        const uint32_t l = sg[k] > 0 ? ohi[k] - c3[k] : c3[k] - olo[k];
                         if (!l || !(hh[k] > 0) || !(dd[k] > 0)) continue;
                         const uint32_t crs = (fbits(jump(hh[k], dd[k], l)) >> 23) - (fbits(hh[k]) >> 23);
                         worst = crs > worst ? crs : worst;
                     }
                     g_cross[worst < 15 ? worst : 15]++;
                 }
-                if (skip_box(w, lo, hi, bound, c) == 1) break;
+                if (sr == 2) { ++c; if (!step1(w, n)) break; continue; }
+                w = t; c += cc;
+                if (sr == 1) break;
+                ++c;
+                if (!step1(w, n)) break;
+                continue;
             } else {
                 ++steps;
                 const uint32_t bb = ((w.X >> 2) & 3u) | (((w.Y >> 2) & 3u) << 2) | (((w.Z >> 2) & 3u) << 4);

@@ -95,8 +95,8 @@ for name, (a, b, bnd), mode in [(nm_, v, md) for nm_, v in sets.items() for md i
     o = sim(a, b, bnd)
     print(f"mode {mode}: slab skips {lib.slab_out() / R:.1f} per ray")
     print(f"{name} ({R} rays): cells {o[0]/R:.0f} steps {o[1]/R:.1f} skips {o[2]/R:.1f} (max {o[7]}) "
-          f"lean-refused {o[6]/max(o[2],1):.4f} cost {(o[1] + 5.8 * o[2]) / R:.0f}")
+          f"lean-clipped {o[6]/max(o[2],1):.4f} cost {(o[1] + 5.8 * o[2]) / R:.0f}")
     lib.small_out.restype = C.c_uint64
     print(f"   steps in empty bricks with a cube below the skip minimum: {lib.small_out() / R:.1f} per ray")
     cr = np.zeros(16, np.uint64); lib.cross_out.argtypes = [V]; lib.cross_out(cr.ctypes.data)
-    print("   lean refusals by binade crossings (max over axes):", cr[:10])
+    print("   clipped boxes by binade crossings of the full box (max over axes):", cr[:10])
