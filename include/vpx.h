@@ -30,6 +30,7 @@
  *   vpx_set_lights        point/spot/area/dirLight    renderer.h:193-197
  *   vpx_set_shapes        Renderer::spheres/triangles renderer.h:207-208
  *   vpx_set_camera        Renderer::camera            renderer.h:181, template/camera.h:14-192
+ *   vpx_set_sky           Renderer::skyPixels (+ SampleSky) renderer.cpp:691, 2308-2326
  * Host-side helpers that restate reference host code (no GPU needed):
  *   vpx_camera_look_at       Camera::HandleInput basis   template/camera.h:113-181
  *   vpx_volume_set_transform Scene::SetTransform         template/scene.cpp:373-405
@@ -70,6 +71,7 @@ extern "C" {
 #define VPX_FLAG_AA 0x1u        /* sub-pixel jitter x+RandomFloat()*aa (renderer.cpp:1682-1708)   */
 #define VPX_FLAG_DOF 0x2u       /* thin-lens jitter (template/camera.h:68-83)                    */
 #define VPX_FLAG_NO_TONEMAP 0x4u /* skip accumulate/tonemap: write raw radiance to accum (tests) */
+#define VPX_FLAG_SKY 0x8u       /* activateSky: misses sample the vpx_set_sky texture (renderer.cpp:2308-2326) */
 
 /* ---- POD scene description -------------------------------------------------------- */
 
@@ -226,6 +228,13 @@ int vpx_set_lights(vpx_ctx* ctx,
 int vpx_set_shapes(vpx_ctx* ctx, const vpx_sphere* spheres, uint32_t n_spheres,
                    const vpx_triangle* triangles, uint32_t n_triangles);
 int vpx_set_camera(vpx_ctx* ctx, const vpx_camera* camera);
+/* Sky dome: Renderer::skyPixels / skyWidth / skyHeight (stbi_loadf RGB floats of the
+   equirectangular HDR, renderer.cpp:691; renderer.h:224-226) and HDRLightContribution.
+   Texel (u, v) at rgb[3*(u + v*width)].  Used by SampleSky (renderer.cpp:2308-2326) when a
+   frame sets VPX_FLAG_SKY, and by vpx_trace when its sky argument is NULL.
+   rgb == NULL (or a zero size) removes the texture. */
+int vpx_set_sky(vpx_ctx* ctx, const float* rgb, uint32_t width, uint32_t height,
+                float hdr_contribution);
 
 /* ---- the hot path -------------------------------------------------------------------- */
 /* One frame: primary rays, Trace(ray, max_bounces) per pixel, running-average accumulate
@@ -297,7 +306,8 @@ int vpx_profile_read(vpx_ctx* ctx, vpx_profile* out, int reset);
 /* ---- unit entries (host pointers; mirror the reference per-ray functions) ---------- */
 int vpx_find_nearest(vpx_ctx* ctx, const vpx_ray* rays, uint32_t n, vpx_hit* hits);
 int vpx_is_occluded(vpx_ctx* ctx, const vpx_ray* rays, uint32_t n, uint8_t* occluded);
-/* Trace(ray, depth) with an explicit xorshift32 state per ray; radiance = float3[n]. */
+/* Trace(ray, depth) with an explicit xorshift32 state per ray; radiance = float3[n].
+   sky: the constant SampleSky colour (activateSky == false), or NULL for the texture. */
 int vpx_trace(vpx_ctx* ctx, const vpx_ray* rays, const uint32_t* seeds, uint32_t n,
               int32_t depth, const float sky[3], int32_t area_samples, float* radiance);
 /* Focus ray of Renderer::Tick (world-space ray against every Scene::FindNearest). */

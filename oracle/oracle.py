@@ -80,7 +80,9 @@ def _scene_struct(abi):
                     ("dir", abi.DirLight),
                     ("spheres", C.POINTER(abi.Sphere)), ("num_spheres", C.c_uint32),
                     ("triangles", C.POINTER(abi.Triangle)), ("num_triangles", C.c_uint32),
-                    ("camera", abi.Camera)]
+                    ("camera", abi.Camera),
+                    ("sky_pixels", C.c_void_p), ("sky_w", C.c_uint32), ("sky_h", C.c_uint32),
+                    ("sky_hdr", C.c_float)]
     return OracleScene
 
 
@@ -112,6 +114,16 @@ class Oracle:
         s.camera = desc.camera
         self._keep += [grids, pts, sps, ars, sph, tri]
         self.s = s
+        self.set_sky(getattr(desc, "sky_texture", None), getattr(desc, "sky_hdr", 1.0))
+
+    def set_sky(self, rgb, hdr_contribution=1.0):
+        if rgb is None:
+            self.s.sky_pixels, self.s.sky_w, self.s.sky_h = None, 0, 0
+            return
+        a = np.ascontiguousarray(rgb, np.float32)
+        self._sky = a
+        self.s.sky_pixels, self.s.sky_h, self.s.sky_w = a.ctypes.data, a.shape[0], a.shape[1]
+        self.s.sky_hdr = float(hdr_contribution)
 
     def host_grid(self, spec):
         """Materialise a GridSpec on the host with the oracle's own generator."""
@@ -150,7 +162,7 @@ class Oracle:
         seeds = np.ascontiguousarray(seeds, np.uint32)
         out = np.zeros((max(1, n), 3), np.float32)
         st = self.abi.Stats()
-        assert self.lib.oracle_trace(self.ptr, rays, seeds.ctypes.data, n, depth, self.abi.vec3(sky), area_samples,
+        assert self.lib.oracle_trace(self.ptr, rays, seeds.ctypes.data, n, depth, self.abi.sky_arg(sky), area_samples,
                                      out.ctypes.data, C.byref(st)) == 0
         return out[:n], st
 

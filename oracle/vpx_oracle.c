@@ -199,9 +199,66 @@ typedef struct {
     const oracle_scene* sc;
     uint32_t rng;
     float sky[3];
+    int sky_tex; /* activateSky with a texture: SampleSky reads sc->sky_pixels */
     int area_samples;
     uint64_t shadow_rays, nearest_calls, dda_cells;
 } tctx;
+
+/* atan2_approximation2, template/tmpl8math.cpp:405-426 (ONEQTR_PI = PI / 4.0 in double,
+   stored as float). */
+static float atan2_approximation2(float y, float x)
+{
+    const float ONEQTR_PI = (float)((double)PI_F / 4.0);
+    const float THRQTR_PI = (float)(3.0 * (double)PI_F / 4.0);
+    float r, angle;
+    const float abs_y = fabsf(y) + 1e-10f;
+    if (x < 0.0f) {
+        r = (x + abs_y) / (abs_y - x);
+        angle = THRQTR_PI;
+    } else {
+        r = (x - abs_y) / (x + abs_y);
+        angle = ONEQTR_PI;
+    }
+    angle += (0.1963f * r * r - 0.9817f) * r;
+    return y < 0.0f ? -angle : angle;
+}
+
+/* FastAcos, template/tmpl8math.cpp:429-443 */
+static float fast_acos(float x)
+{
+    const float negate = (float)(x < 0);
+    x = fabsf(x);
+    float ret = (float)-0.0187293;
+    ret = ret * x;
+    ret = ret + 0.0742610f;
+    ret = ret * x;
+    ret = ret - 0.2121144f;
+    ret = ret * x;
+    ret = ret + 1.5707288f;
+    ret = ret * sqrtf(1.0f - x);
+    ret = ret - 2 * negate * ret;
+    return negate * 3.14159265358979f + ret;
+}
+
+/* Renderer::SampleSky, renderer.cpp:2308-2326 (INV2PI / INVPI: common.h:13-14).  The
+   int arithmetic wraps as on x86; an index past the image (only from a NaN direction)
+   is clamped to the last texel instead of reading outside it (reference: UB). */
+static v3 sample_sky(const tctx* c, v3 d)
+{
+    if (!c->sky_tex) return V3(c->sky[0], c->sky[1], c->sky[2]);
+    const oracle_scene* sc = c->sc;
+    const float uf = (float)sc->sky_w * atan2_approximation2(d.z, d.x) * 0.15915494309189533576888f - 0.5f;
+    const int u = f2i_trunc(uf);
+    const float vf = (float)sc->sky_h * fast_acos(d.y) * 0.31830988618379067153777f - 0.5f;
+    const int v = f2i_trunc(vf);
+    const int32_t lin = (int32_t)((uint32_t)u + (uint32_t)v * sc->sky_w);
+    uint32_t idx = lin > 0 ? (uint32_t)lin : 0u;
+    const uint32_t last = sc->sky_w * sc->sky_h - 1u;
+    if (idx > last) idx = last;
+    const float* px = sc->sky_pixels + 3u * (uint64_t)idx;
+    const float h = sc->sky_hdr;
+    return V3(h * px[0], h * px[1], h * px[2]);
+}
 
 typedef struct {
     int sx, sy, sz;  /* step */
@@ -735,7 +792,7 @@ static v3 trace(tctx* c, ray_t* r, int depth)
 {
     if (depth < 0) return V3(0, 0, 0);
     const int32_t vox = renderer_find_nearest(c, r);
-    if (r->mat == NONE_MAT) return V3(c->sky[0], c->sky[1], c->sky[2]); /* SampleSky :2308-2313 */
+    if (r->mat == NONE_MAT) return sample_sky(c, r->D); /* SampleSky :1092-1095 */
     const vpx_material* mat = &c->sc->materials[r->mat];
     switch (r->mat) {
     case 5: case 6: case 7: { /* metals :1103-1114 */
@@ -915,10 +972,12 @@ int oracle_trace(const oracle_scene* sc, const vpx_ray* rays, const uint32_t* se
                  vpx_stats* stats)
 {
     if (!sc || (!rays && n) || (!seeds && n) || (!radiance && n)) return VPX_E_INVALID;
+    if (!sky && !sc->sky_pixels) return VPX_E_STATE;
     const fpstate fs = fp_enter();
     tctx c;
     tctx_init(&c, sc);
     if (sky) c.sky[0] = sky[0], c.sky[1] = sky[1], c.sky[2] = sky[2];
+    c.sky_tex = sky == NULL;
     c.area_samples = area_samples;
     for (uint32_t i = 0; i < n; i++) {
         ray_t r = ray_from_api(&rays[i]);
@@ -1019,6 +1078,7 @@ static void* render_worker(void* arg)
     tctx c;
     tctx_init(&c, j->sc);
     c.sky[0] = j->p->sky[0], c.sky[1] = j->p->sky[1], c.sky[2] = j->p->sky[2];
+    c.sky_tex = (j->p->flags & VPX_FLAG_SKY) && j->sc->sky_pixels;
     c.area_samples = j->p->area_samples;
     const uint32_t W = j->p->width;
     const float w = 1.0f / ((float)j->p->frame_index + 1.0f);
@@ -1108,7 +1168,7 @@ static aidata trace_reproject(tctx* c, ray_t* r, int depth)
     }
     const int32_t vox = renderer_find_nearest(c, r);
     if (r->mat == NONE_MAT) {
-        out.albedo = V3(c->sky[0], c->sky[1], c->sky[2]), out.illum = V3(1, 1, 1);
+        out.albedo = sample_sky(c, r->D), out.illum = V3(1, 1, 1); /* SampleSkyReproject :2328-2346 */
         return out;
     }
     const vpx_material* mat = &c->sc->materials[r->mat];
@@ -1244,6 +1304,7 @@ static void* reproject_worker(void* arg)
     tctx c;
     tctx_init(&c, j->sc);
     c.sky[0] = j->p->sky[0], c.sky[1] = j->p->sky[1], c.sky[2] = j->p->sky[2];
+    c.sky_tex = (j->p->flags & VPX_FLAG_SKY) && j->sc->sky_pixels;
     c.area_samples = j->p->area_samples;
     const uint32_t W = j->p->width, H = j->p->height;
     const vpx_camera* cam = &j->sc->camera;

@@ -47,6 +47,10 @@ typedef struct oracle_scene {
     const vpx_triangle* triangles;
     uint32_t num_triangles;
     vpx_camera camera;
+    /* sky dome (vpx_set_sky): RGB float texels, NULL = none */
+    const float* sky_pixels;
+    uint32_t sky_w, sky_h;
+    float sky_hdr;
 } oracle_scene;
 
 /* Renderer::FindNearest per ray (renderer.cpp:946-1018). */
@@ -54,7 +58,8 @@ int oracle_find_nearest(const oracle_scene* sc, const vpx_ray* rays, uint32_t n,
 /* Renderer::IsOccluded per ray (renderer.cpp:209-243). cells may be NULL. */
 int oracle_is_occluded(const oracle_scene* sc, const vpx_ray* rays, uint32_t n,
                        uint8_t* occluded, uint32_t* cells);
-/* Renderer::Trace(ray, depth) per ray with an explicit xorshift32 state. */
+/* Renderer::Trace(ray, depth) per ray with an explicit xorshift32 state; sky NULL =
+   the scene's sky texture (activateSky). */
 int oracle_trace(const oracle_scene* sc, const vpx_ray* rays, const uint32_t* seeds, uint32_t n,
                  int32_t depth, const float sky[3], int32_t area_samples, float* radiance,
                  vpx_stats* stats);

@@ -16,6 +16,7 @@ VPX_OK = 0
 VPX_FLAG_AA = 0x1
 VPX_FLAG_DOF = 0x2
 VPX_FLAG_NO_TONEMAP = 0x4
+VPX_FLAG_SKY = 0x8  # activateSky: misses sample the vpx_set_sky texture (renderer.cpp:2308-2326)
 MAT_NONE = 255
 SKY_DEFAULT = (0.392, 0.584, 0.829)  # SampleSky with activateSky == false, renderer.cpp:2310-2313
 
@@ -130,6 +131,7 @@ SIGNATURES = {
                                  C.POINTER(AreaLight), C.c_uint32, C.POINTER(DirLight)]),
     "vpx_set_shapes": (C.c_int, [C.c_void_p, C.POINTER(Sphere), C.c_uint32, C.POINTER(Triangle), C.c_uint32]),
     "vpx_set_camera": (C.c_int, [C.c_void_p, C.POINTER(Camera)]),
+    "vpx_set_sky": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_float]),
     "vpx_render": (C.c_int, [C.c_void_p, C.POINTER(FrameParams), C.c_void_p, C.c_void_p, C.POINTER(Stats)]),
     "vpx_render_tiles": (C.c_int, [C.c_void_p, C.POINTER(FrameParams), C.c_uint32, C.c_uint32, C.c_uint32,
                                    C.c_uint32, C.c_void_p, C.POINTER(Stats)]),
@@ -193,3 +195,8 @@ def check(lib, ctx, rc, what):
 
 def vec3(v):
     return f3(*[float(x) for x in v])
+
+
+def sky_arg(sky):
+    """vpx_trace's sky argument: a constant colour, or None = the uploaded sky texture."""
+    return None if sky is None else vec3(sky)

@@ -61,7 +61,20 @@ class Context:
         self._chk(self.lib.vpx_set_shapes(self.h, sph, len(desc.spheres), tri, len(desc.triangles)),
                   "vpx_set_shapes")
         self.set_camera(desc.camera)
+        self.set_sky(desc.sky_texture, desc.sky_hdr)
         self.scene = desc
+
+    def set_sky(self, rgb, hdr_contribution=1.0):
+        """Renderer::skyPixels (float32 (H, W, 3) equirectangular) + HDRLightContribution;
+        None removes the texture."""
+        if rgb is None:
+            self._chk(self.lib.vpx_set_sky(self.h, None, 0, 0, float(hdr_contribution)), "vpx_set_sky")
+            return
+        a = np.ascontiguousarray(rgb, np.float32)
+        h, w, ch = a.shape
+        assert ch == 3, "sky texture must be (H, W, 3) RGB floats"
+        self._chk(self.lib.vpx_set_sky(self.h, a.ctypes.data_as(C.c_void_p), w, h, float(hdr_contribution)),
+                  "vpx_set_sky")
 
     def set_camera(self, cam):
         self._chk(self.lib.vpx_set_camera(self.h, C.byref(cam)), "vpx_set_camera")
@@ -148,10 +161,11 @@ class Context:
         return occ[:n]
 
     def trace(self, rays, seeds, depth, sky=abi.SKY_DEFAULT, area_samples=3):
+        """Renderer::Trace per ray; sky=None samples the sky texture (activateSky)."""
         n = len(rays)
         seeds = np.ascontiguousarray(seeds, np.uint32)
         out = np.zeros((max(1, n), 3), np.float32)
-        self._chk(self.lib.vpx_trace(self.h, rays, seeds.ctypes.data_as(C.c_void_p), n, depth, abi.vec3(sky),
+        self._chk(self.lib.vpx_trace(self.h, rays, seeds.ctypes.data_as(C.c_void_p), n, depth, abi.sky_arg(sky),
                                      area_samples, out.ctypes.data_as(C.c_void_p)), "vpx_trace")
         return out[:n]
 

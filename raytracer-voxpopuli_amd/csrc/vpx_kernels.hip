@@ -325,6 +325,10 @@ struct vpx_ctx {
     vpx_dir_light dir{{1, 0, 0}, {0, 0, 0}};  // DirectionalLight default (DirectionalLight.h:12)
     vpx_camera cam{};
     bool have_materials = false, have_camera = false;
+    // sky dome (vpx_set_sky): RGB float texels, equirectangular
+    float* d_sky = nullptr;
+    uint32_t sky_w = 0, sky_h = 0;
+    float sky_hdr = 1.0f;
     unsigned long long* d_ctr = nullptr;  // striped work counters (vpx_wavefront.hpp flush_counters)
     // per-stage profile: event pairs around stage launches while enabled
     std::vector<hipEvent_t> prof_ev;
@@ -408,7 +412,7 @@ int sync_grids(vpx_ctx* c) {
     return VPX_OK;
 }
 
-SceneView view_of(const vpx_ctx* c, const float sky[3], int32_t area_samples) {
+SceneView view_of(const vpx_ctx* c, const float sky[3], int32_t area_samples, bool sky_tex = false) {
     SceneView sv;
     sv.grids = c->d_grids;
     sv.volumes = c->d_volumes;
@@ -427,6 +431,10 @@ SceneView view_of(const vpx_ctx* c, const float sky[3], int32_t area_samples) {
     sv.dir = c->dir;
     sv.sky[0] = sky[0], sv.sky[1] = sky[1], sv.sky[2] = sky[2];
     sv.area_samples = area_samples;
+    sv.sky_px = c->d_sky;
+    sv.sky_w = c->sky_w, sv.sky_h = c->sky_h;
+    sv.sky_hdr = c->sky_hdr;
+    sv.sky_tex = (sky_tex && c->d_sky) ? 1u : 0u;
     return sv;
 }
 
@@ -459,6 +467,8 @@ int validate_frame(vpx_ctx* c, const vpx_frame_params* p) {
         return fail(c, VPX_E_INVALID, "max_bounces must be in [-1, 14]");
     if (p->area_samples < 0 || p->area_samples > 15) return fail(c, VPX_E_INVALID, "area_samples must be in [0, 15]");
     if (!c->have_camera) return fail(c, VPX_E_STATE, "no camera set (vpx_set_camera)");
+    if ((p->flags & VPX_FLAG_SKY) && !c->d_sky)
+        return fail(c, VPX_E_STATE, "VPX_FLAG_SKY without a sky texture (vpx_set_sky)");
     return check_ready(c);
 }
 
@@ -630,7 +640,7 @@ int vpx_destroy(vpx_ctx* c) {
         if (g.l2) (void)hipFree(g.l2);
     }
     void* ptrs[] = {c->d_grids, c->d_volumes, c->d_materials, c->d_points, c->d_spots, c->d_areas,
-                    c->d_spheres, c->d_triangles, c->d_ctr, c->d_sum, c->d_scratch, c->d_wave};
+                    c->d_spheres, c->d_triangles, c->d_ctr, c->d_sum, c->d_scratch, c->d_wave, c->d_sky};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (hipEvent_t e : c->prof_ev) (void)hipEventDestroy(e);
@@ -876,6 +886,34 @@ int vpx_set_shapes(vpx_ctx* c, const vpx_sphere* s, uint32_t ns, const vpx_trian
     return VPX_OK;
 }
 
+int vpx_set_sky(vpx_ctx* c, const float* rgb, uint32_t width, uint32_t height, float hdr_contribution) {
+    if (!c) return VPX_E_INVALID;
+    VPX_HIP(c, hipSetDevice(c->device));
+    if (!rgb || !width || !height) {  // remove the texture (misses use the constant sky)
+        if (c->d_sky) {
+            VPX_HIP(c, hipStreamSynchronize(c->stream));
+            (void)hipFree(c->d_sky);
+        }
+        c->d_sky = nullptr;
+        c->sky_w = c->sky_h = 0;
+        return VPX_OK;
+    }
+    if ((uint64_t)width * height > (1ull << 28)) return fail(c, VPX_E_INVALID, "sky texture too large");
+    const size_t bytes = sizeof(float) * 3 * (size_t)width * height;
+    if ((size_t)c->sky_w * c->sky_h != (size_t)width * height) {
+        VPX_HIP(c, hipStreamSynchronize(c->stream));
+        if (c->d_sky) (void)hipFree(c->d_sky);
+        c->d_sky = nullptr;
+        c->sky_w = c->sky_h = 0;
+        VPX_HIP(c, hipMalloc(&c->d_sky, bytes));
+    }
+    VPX_HIP(c, hipMemcpyAsync(c->d_sky, rgb, bytes, hipMemcpyHostToDevice, c->stream));
+    VPX_HIP(c, hipStreamSynchronize(c->stream));
+    c->sky_w = width, c->sky_h = height;
+    c->sky_hdr = hdr_contribution;
+    return VPX_OK;
+}
+
 int vpx_set_camera(vpx_ctx* c, const vpx_camera* cam) {
     if (!c || !cam) return fail(c, VPX_E_INVALID, "null argument");
     c->cam = *cam;
@@ -891,7 +929,7 @@ int vpx_render(vpx_ctx* c, const vpx_frame_params* p, float* accum, uint32_t* rg
     VPX_HIP(c, hipSetDevice(c->device));
     unsigned long long before[kCtrWords] = {};
     if (stats && (rc = snapshot_counters(c, before))) return rc;
-    const SceneView sv = view_of(c, p->sky, p->area_samples);
+    const SceneView sv = view_of(c, p->sky, p->area_samples, (p->flags & VPX_FLAG_SKY) != 0);
     const FrameArgs f = frame_of(c, p, 0, 1);
     if (stats) VPX_HIP(c, hipEventRecord(c->ev0, c->stream));
     if ((rc = launch_render<false>(c, sv, f, f.num_tiles, reinterpret_cast<float4*>(accum), rgb8, nullptr))) return rc;
@@ -933,7 +971,7 @@ int vpx_render_reproject(vpx_ctx* c, const vpx_frame_params* p, const vpx_prev_c
     rp.hist = reinterpret_cast<float4*>(history);
     unsigned long long before[kCtrWords] = {};
     if (stats && (rc = snapshot_counters(c, before))) return rc;
-    const SceneView sv = view_of(c, p->sky, p->area_samples);
+    const SceneView sv = view_of(c, p->sky, p->area_samples, (p->flags & VPX_FLAG_SKY) != 0);
     FrameArgs f = frame_of(c, p, 0, 1);
     f.flags = (f.flags & ~(VPX_FLAG_AA | VPX_FLAG_DOF)) | kFlagReproject;  // GetPrimaryRayNoDOF
     if (stats) VPX_HIP(c, hipEventRecord(c->ev0, c->stream));
@@ -968,7 +1006,7 @@ int vpx_render_tiles(vpx_ctx* c, const vpx_frame_params* p, uint32_t tile_w, uin
     VPX_HIP(c, hipSetDevice(c->device));
     unsigned long long before[kCtrWords] = {};
     if (stats && (rc = snapshot_counters(c, before))) return rc;
-    const SceneView sv = view_of(c, p->sky, p->area_samples);
+    const SceneView sv = view_of(c, p->sky, p->area_samples, (p->flags & VPX_FLAG_SKY) != 0);
     const FrameArgs f = frame_of(c, p, rank, n_ranks);
     if (stats) VPX_HIP(c, hipEventRecord(c->ev0, c->stream));
     if ((rc = launch_render<true>(c, sv, f, f.tiles_per_rank, nullptr, nullptr, reinterpret_cast<float4*>(packed))))
@@ -1053,10 +1091,12 @@ int vpx_is_occluded(vpx_ctx* c, const vpx_ray* rays, uint32_t n, uint8_t* occ) {
 
 int vpx_trace(vpx_ctx* c, const vpx_ray* rays, const uint32_t* seeds, uint32_t n, int32_t depth, const float sky[3],
               int32_t area_samples, float* radiance) {
-    if (!c || (n && (!rays || !seeds || !radiance)) || !sky) return fail(c, VPX_E_INVALID, "null argument");
+    if (!c || (n && (!rays || !seeds || !radiance))) return fail(c, VPX_E_INVALID, "null argument");
     if (depth < -1 || depth > kMaxLevels - 2) return fail(c, VPX_E_INVALID, "depth must be in [-1, 14]");
+    if (!sky && !c->d_sky) return fail(c, VPX_E_STATE, "sky == NULL (textured sky) without vpx_set_sky");
     int rc = check_ready(c);
     if (rc) return rc;
+    static const float kNoSky[3] = {0.f, 0.f, 0.f};
     if (n == 0) return VPX_OK;
     const size_t rb = sizeof(vpx_ray) * n, sb = 4ull * n, ob = 12ull * n;
     if ((rc = ensure_scratch(c, rb + sb + ob))) return rc;
@@ -1065,7 +1105,7 @@ int vpx_trace(vpx_ctx* c, const vpx_ray* rays, const uint32_t* seeds, uint32_t n
     float* dout = (float*)((char*)c->d_scratch + rb + sb);
     VPX_HIP(c, hipMemcpyAsync(dr, rays, rb, hipMemcpyHostToDevice, c->stream));
     VPX_HIP(c, hipMemcpyAsync(ds, seeds, sb, hipMemcpyHostToDevice, c->stream));
-    const SceneView sv = view_of(c, sky, area_samples);
+    const SceneView sv = view_of(c, sky ? sky : kNoSky, area_samples, sky == nullptr);
     const dim3 g((n + 255) / 256), b(256);
     if (depth <= 0)
         hipLaunchKernelGGL(trace_k<1>, g, b, 0, c->stream, sv, dr, ds, n, depth, dout);

@@ -58,6 +58,12 @@ struct SceneView {
     vpx_dir_light dir;
     float sky[3];
     int32_t area_samples;
+    // activateSky: an equirectangular HDR (stbi_loadf RGB floats, renderer.cpp:691) with
+    // HDRLightContribution (renderer.h:224-226); sky_tex == 0 -> the constant `sky`.
+    const float* sky_px;
+    uint32_t sky_w, sky_h;
+    float sky_hdr;
+    uint32_t sky_tex;
 };
 
 struct f3 {
@@ -622,6 +628,58 @@ __device__ __forceinline__ bool shadow(const SceneView& sv, const Ray& r, Counte
 
 __device__ __forceinline__ f3 albedo(const SceneView& sv, uint32_t m) { return ld3(sv.materials[m].albedo); }
 
+// atan2_approximation2, template/tmpl8math.cpp:405-426.  ONEQTR_PI / THRQTR_PI are the
+// float PI (common.h:8) divided in double and stored as float.
+__device__ __forceinline__ float atan2_approx(float y, float x) {
+    const float q1 = (float)((double)kPi / 4.0), q3 = (float)(3.0 * (double)kPi / 4.0);
+    const float ay = fabsf(y) + 1e-10f;
+    float r, angle;
+    if (x < 0.0f) {
+        r = __fdiv_rn(x + ay, ay - x);
+        angle = q3;
+    } else {
+        r = __fdiv_rn(x - ay, x + ay);
+        angle = q1;
+    }
+    angle += (0.1963f * r * r - 0.9817f) * r;
+    return y < 0.0f ? -angle : angle;
+}
+
+// FastAcos, template/tmpl8math.cpp:429-443 (float arithmetic; the first constant is a
+// double literal rounded to float).
+__device__ __forceinline__ float fast_acos(float x) {
+    const float negate = (float)(x < 0);
+    x = fabsf(x);
+    float ret = (float)-0.0187293;
+    ret = ret * x;
+    ret = ret + 0.0742610f;
+    ret = ret * x;
+    ret = ret - 0.2121144f;
+    ret = ret * x;
+    ret = ret + 1.5707288f;
+    ret = ret * sqrtf(1.0f - x);
+    ret = ret - 2.0f * negate * ret;
+    return negate * 3.14159265358979f + ret;
+}
+
+// Renderer::SampleSky, renderer.cpp:2308-2326 (and SampleSkyReproject :2328-2346, whose
+// albedo is the same value).  INV2PI / INVPI: common.h:13-14.  The index arithmetic wraps
+// like the x86 reference; the only out-of-range index (a NaN direction, cvttss2si ->
+// INT_MIN) is clamped to the image instead of reading outside it.
+__device__ __forceinline__ f3 sample_sky(const SceneView& sv, f3 d) {
+    if (!sv.sky_tex) return ld3(sv.sky);
+    const float uf = (float)sv.sky_w * atan2_approx(d.z, d.x) * 0.15915494309189533576888f - 0.5f;
+    const int u = trunc_i32(uf);
+    const float vf = (float)sv.sky_h * fast_acos(d.y) * 0.31830988618379067153777f - 0.5f;
+    const int v = trunc_i32(vf);
+    const int32_t lin = (int32_t)((uint32_t)u + (uint32_t)v * sv.sky_w);
+    uint32_t idx = lin > 0 ? (uint32_t)lin : 0u;
+    const uint32_t last = sv.sky_w * sv.sky_h - 1u;
+    idx = idx < last ? idx : last;
+    const float* px = sv.sky_px + 3u * (uint64_t)idx;
+    return mk(sv.sky_hdr * px[0], sv.sky_hdr * px[1], sv.sky_hdr * px[2]);
+}
+
 // RandomDirection (tmpl8math.cpp:76-93), RandomSphereSample (tmpl8math.h:2502-2511),
 // DiffuseReflection (tmpl8math.h:2518-2528; argument order left to right).
 __device__ __forceinline__ f3 random_direction(Rng& g) {
@@ -786,7 +844,7 @@ __device__ __forceinline__ f3 trace_path(const SceneView& sv, Ray ray, int depth
         if (depth < 0) break;  // Trace(depth < 0) returns 0
         const int32_t vox = find_nearest(sv, ray, k);
         if (ray.mat == kNone) {
-            leaf = ld3(sv.sky);
+            leaf = sample_sky(sv, ray.D);
             break;
         }
         const uint32_t m = ray.mat;

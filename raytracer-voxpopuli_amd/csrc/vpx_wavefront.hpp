@@ -283,8 +283,8 @@ __global__ __launch_bounds__(256) void k_shade(SceneView sv, FrameArgs f, WaveBu
             const uint32_t nl = forms >> 27;
             bool done = false;
             f3 leaf = mk(0.f, 0.f, 0.f);
-            if (ray.mat == kNone) {  // SampleSky (activateSky == false), :1092-1095
-                leaf = ld3(sv.sky);
+            if (ray.mat == kNone) {  // SampleSky, :1092-1095
+                leaf = sample_sky(sv, ray.D);
                 done = true;
             } else if (ray.mat == VPX_MAT_EMISSIVE) {  // :1315-1316
                 leaf = albedo(sv, ray.mat) * sv.materials[ray.mat].emissive;

@@ -7,7 +7,9 @@
 //   ground slab y < 2 -> material 0; pillar cells where (x & 15) < 8 and (z & 15) < 8 and
 //   y < 2 + h, h = ((x >> 4) * 7 + (z >> 4) * 13) % 5 * n / 16 -> material 16 + (h % 4).
 //
-// usage: vpx_demo [n] [width] [height] [frames] [max_bounces] [out.rgb8]
+// usage: vpx_demo [n] [width] [height] [frames] [max_bounces] [out.rgb8] [mode]
+//   mode: letters — 's' staticCamera (the reprojection branch of Tick), 'k' activateSky
+//   with the demo sky texture (demo_sky below; tests rebuild it with numpy).
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -32,6 +34,19 @@ static std::vector<uint8_t> pillars(uint32_t n) {
     return g;
 }
 
+// 64x32 RGB float texture: (2u/63, v/31, 0.5 + (u + v) % 7) — exact in float32.
+static std::vector<float> demo_sky(uint32_t w, uint32_t h) {
+    std::vector<float> t((size_t)w * h * 3);
+    for (uint32_t v = 0; v < h; ++v)
+        for (uint32_t u = 0; u < w; ++u) {
+            float* p = &t[3 * ((size_t)v * w + u)];
+            p[0] = (float)u / (float)(w - 1) * 2.0f;
+            p[1] = (float)v / (float)(h - 1);
+            p[2] = 0.5f + (float)((u + v) % 7u);
+        }
+    return t;
+}
+
 #define CHECK(x)                                                                              \
     do {                                                                                      \
         const int rc_ = (x);                                                                  \
@@ -47,7 +62,10 @@ int main(int argc, char** argv) {
     const uint32_t H = argc > 3 ? (uint32_t)atoi(argv[3]) : 360;
     const int frames = argc > 4 ? atoi(argv[4]) : 8;
     const int bounces = argc > 5 ? atoi(argv[5]) : 0;
-    const char* out = argc > 6 ? argv[6] : nullptr;
+    const char* out = argc > 6 && argv[6][0] != '-' ? argv[6] : nullptr;
+    const char* mode = argc > 7 ? argv[7] : "";
+    bool is_static = false, sky = false;
+    for (const char* m = mode; *m; ++m) is_static |= *m == 's', sky |= *m == 'k';
 
     vpxhost::Renderer r(0);
     CHECK(r.Init(W, H));
@@ -67,6 +85,12 @@ int main(int argc, char** argv) {
     const float pos[3] = {1.25f, 0.9f, -0.35f}, target[3] = {0.45f, 0.15f, 0.55f};
     CHECK(r.LookAt(pos, target));
     r.maxBounces = bounces;
+    if (sky) {
+        const std::vector<float> tex = demo_sky(64, 32);
+        CHECK(r.SetSky(tex.data(), 64, 32, 1.5f));
+        r.activateSky = true;
+    }
+    r.staticCamera = is_static;
 
     vpx_stats st{};
     CHECK(r.Tick(0.0f, &st));  // warm-up frame (also frame 0 of the accumulation)

@@ -10,6 +10,7 @@ Renderer::Renderer(int device) : device_(device) { status_ = vpx_create(device, 
 Renderer::~Renderer() {
     if (accumulator_) (void)hipFree(accumulator_);
     if (screen_) (void)hipFree(screen_);
+    if (history_) (void)hipFree(history_);
     if (ctx_) vpx_destroy(ctx_);
 }
 
@@ -63,6 +64,7 @@ int Renderer::LookAt(const float pos[3], const float target[3]) {
     const float keep_focal = camera.focal_distance, keep_jitter = camera.defocus_jitter;
     int rc = vpx_camera_look_at(pos, target, width_, height_, &camera);
     if (rc) return rc;
+    for (int i = 0; i < 3; ++i) camPos_[i] = pos[i], camTarget_[i] = target[i];
     if (keep_focal > 0.0f) camera.focal_distance = keep_focal, camera.defocus_jitter = keep_jitter;
     return vpx_set_camera(ctx_, &camera);
 }
@@ -75,7 +77,7 @@ int Renderer::Update(vpx_stats* stats) {
     p.max_bounces = maxBounces;
     p.frame_index = numRenderedFrames;
     p.seed_base = 0;
-    p.flags = flags;
+    p.flags = (flags & ~VPX_FLAG_SKY) | (activateSky ? VPX_FLAG_SKY : 0u);
     p.aa_strength = antiAliasingStrength;
     p.area_samples = numCheckShadowsAreaLight;
     p.sky[0] = sky[0], p.sky[1] = sky[1], p.sky[2] = sky[2];
@@ -84,12 +86,57 @@ int Renderer::Update(vpx_stats* stats) {
     return rc;
 }
 
+int Renderer::SetSky(const float* rgb, uint32_t width, uint32_t height, float hdr_contribution) {
+    return status_ ? status_ : vpx_set_sky(ctx_, rgb, width, height, hdr_contribution);
+}
+
+int Renderer::CopyToPrevCamera() {
+    if (status_) return status_;
+    const int rc = vpx_prev_camera_look_at(camPos_, camTarget_, width_, height_, &prevCamera);
+    if (rc == VPX_OK) havePrev_ = true;
+    return rc;
+}
+
+// The static branch of Renderer::Tick (renderer.cpp:1996-2101): TraceReproject per pixel,
+// reprojection into prevCamera, SampleHistory / ClampHistory, blend, tonemap, RGB8.
+int Renderer::UpdateStatic(vpx_stats* stats) {
+    if (!history_) {
+        const size_t bytes = sizeof(float) * 4 * (size_t)width_ * height_;
+        if (hipMalloc(&history_, bytes) != hipSuccess || hipMemset(history_, 0, bytes) != hipSuccess) {
+            err_ = "history allocation failed";
+            return VPX_E_NOMEM;
+        }
+    }
+    if (!havePrev_) {
+        const int rc = CopyToPrevCamera();
+        if (rc) return rc;
+    }
+    vpx_frame_params p{};
+    p.width = width_, p.height = height_;
+    p.max_bounces = maxBounces;
+    p.frame_index = numRenderedFrames;
+    p.flags = activateSky ? VPX_FLAG_SKY : 0u;
+    p.aa_strength = antiAliasingStrength;
+    p.area_samples = numCheckShadowsAreaLight;
+    p.sky[0] = sky[0], p.sky[1] = sky[1], p.sky[2] = sky[2];
+    const int rc = vpx_render_reproject(ctx_, &p, &prevCamera, history_, screen_, stats);
+    if (rc == VPX_OK) ++numRenderedFrames;
+    return rc;
+}
+
+int Renderer::CopyHistory(float* host_rgba) const {
+    if (status_) return status_;
+    if (!history_) return VPX_E_STATE;
+    int rc = vpx_synchronize(ctx_);
+    if (rc) return rc;
+    return hipMemcpy(host_rgba, history_, sizeof(float) * 4 * width_ * height_, hipMemcpyDeviceToHost) == hipSuccess
+               ? VPX_OK
+               : VPX_E_DEVICE;
+}
+
 int Renderer::Tick(float /*deltaTime*/, vpx_stats* stats) {
     if (status_) return status_;
-    if (staticCamera) {
-        err_ = "static-camera reprojection is out of scope (SURVEY.md 8(f) rank 1)";
-        return VPX_E_STATE;
-    }
+    if (staticCamera) return UpdateStatic(stats);
     if (flags & VPX_FLAG_DOF) {  // focus ray of Renderer::Tick (renderer.cpp:1987-1991)
         int rc = vpx_focus_distance(ctx_, width_, height_, &camera.focal_distance);
         if (rc) return rc;

@@ -39,14 +39,22 @@ public:
     int SetShapes(const std::vector<vpx_sphere>& spheres, const std::vector<vpx_triangle>& triangles);
     // Camera::camPos / camTarget + HandleInput(0) (template/camera.h:113-181).
     int LookAt(const float pos[3], const float target[3]);
+    // skyPixels / skyWidth / skyHeight (stbi_loadf RGB floats, renderer.cpp:691) and
+    // HDRLightContribution; sampled when activateSky is set.  rgb == nullptr removes it.
+    int SetSky(const float* rgb, uint32_t width, uint32_t height, float hdr_contribution);
+    // prevCamera = the current camera (CopyToPrevCamera, renderer.cpp:1893-1902).
+    int CopyToPrevCamera();
 
     // --- per frame -----------------------------------------------------------------------
     void ResetAccumulator() { numRenderedFrames = 0; }  // renderer.cpp:343-346
     int Update(vpx_stats* stats = nullptr);             // renderer.cpp:1646-1891
+    // Tick: moving camera -> focus ray + Update; staticCamera -> the reprojection branch
+    // (renderer.cpp:1996-2101) through vpx_render_reproject with the history in HBM.
     int Tick(float deltaTime, vpx_stats* stats = nullptr);
     // Surface::pixels (0x00RRGGBB, W*H) for display: device -> host copy of the frame.
     int CopyScreen(uint32_t* host_pixels) const;
     int CopyAccumulator(float* host_rgba) const;
+    int CopyHistory(float* host_rgba) const;  // illuminationHistoryBuffer (static branch)
 
     const char* LastError() const;
     vpx_ctx* Context() const { return ctx_; }
@@ -56,12 +64,18 @@ public:
     uint32_t numRenderedFrames = 0;
     float antiAliasingStrength = 1.0f;
     int32_t numCheckShadowsAreaLight = 3;
-    bool staticCamera = false;  // reprojection branch: out of scope
+    bool staticCamera = false;  // renderer.h:229: Tick takes the reprojection branch
+    bool activateSky = false;   // renderer.h:216 (needs SetSky; the reference's HDR is missing)
     uint32_t flags = 0;         // VPX_FLAG_AA / VPX_FLAG_DOF
     float sky[3] = {0.392f, 0.584f, 0.829f};  // SampleSky, activateSky == false (renderer.cpp:2310-2313)
     vpx_camera camera{};
+    vpx_prev_camera prevCamera{};  // renderer.h:182
 
 private:
+    int UpdateStatic(vpx_stats* stats);
+    float camPos_[3] = {0, 0, 0}, camTarget_[3] = {0, 0, 1};
+    bool havePrev_ = false;
+    float* history_ = nullptr;      // illuminationHistoryBuffer float4[W*H] in HBM
     int status_ = VPX_OK;
     int device_ = 0;
     vpx_ctx* ctx_ = nullptr;

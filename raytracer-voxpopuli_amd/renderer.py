@@ -23,6 +23,9 @@ class Renderer:
         self.antiAliasingStrength = scene.aa_strength     # renderer.h:185
         self.numCheckShadowsAreaLight = scene.area_samples  # renderer.h:205
         self.staticCamera = False
+        self.activateSky = bool(scene.flags & abi.VPX_FLAG_SKY)  # renderer.h:216
+        self.HDRLightContribution = scene.sky_hdr               # renderer.h:224
+        self.skyPixels = scene.sky_texture                      # renderer.h:226 (float32 (H, W, 3))
         self.prevCamera = None             # renderer.h:182 (vpx_prev_camera)
         self.illuminationHistory = None    # renderer.h:242, float4[W*H] in HBM
         self.accumulator = None
@@ -40,16 +43,26 @@ class Renderer:
         self.stream = torch.cuda.Stream(self.device)
         self.ctx.set_stream(self.stream.cuda_stream)
         self.ctx.load_scene(self.scene)
+        self._sky_uploaded = (self.skyPixels, self.HDRLightContribution)
         return self
+
+    def _frame_params(self):
+        p = self.scene.frame_params(frame_index=self.numRenderedFrames)
+        p.max_bounces = self.maxBounces
+        p.area_samples = self.numCheckShadowsAreaLight
+        up_px, up_hdr = self._sky_uploaded
+        if self.skyPixels is not up_px or self.HDRLightContribution != up_hdr:  # ImGui edits, renderer.cpp:2591
+            self.ctx.set_sky(self.skyPixels, self.HDRLightContribution)
+            self._sky_uploaded = (self.skyPixels, self.HDRLightContribution)
+        p.flags = (p.flags & ~abi.VPX_FLAG_SKY) | (abi.VPX_FLAG_SKY if self.activateSky else 0)
+        return p
 
     def ResetAccumulator(self):  # renderer.cpp:343-346
         self.numRenderedFrames = 0
 
     def Update(self, stats=False):
-        p = self.scene.frame_params(frame_index=self.numRenderedFrames)
-        p.max_bounces = self.maxBounces
+        p = self._frame_params()
         p.aa_strength = self.antiAliasingStrength
-        p.area_samples = self.numCheckShadowsAreaLight
         self.last_stats = self.ctx.render(p, self.accumulator.data_ptr(), self.screen.data_ptr(), stats=stats)
         self.numRenderedFrames += 1
         return self.last_stats
@@ -71,9 +84,7 @@ class Renderer:
             w, h = self.scene.width, self.scene.height
             self.illuminationHistory = torch.zeros(w * h * 4, dtype=torch.float32, device=self.device)
             torch.cuda.synchronize(self.device)  # allocated on torch's stream; the library uses its own
-        p = self.scene.frame_params(frame_index=self.numRenderedFrames)
-        p.max_bounces = self.maxBounces
-        p.area_samples = self.numCheckShadowsAreaLight
+        p = self._frame_params()
         st = self.ctx.render_reproject(p, self.prevCamera, self.illuminationHistory.data_ptr(), self.screen.data_ptr(),
                                        stats=stats)
         self.numRenderedFrames += 1

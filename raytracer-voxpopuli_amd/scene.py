@@ -189,6 +189,8 @@ class SceneDesc:
     aa_strength: float = 1.0
     area_samples: int = 3
     sky: tuple = abi.SKY_DEFAULT
+    sky_texture: object = None    # float32 (H, W, 3): Renderer::skyPixels (used with VPX_FLAG_SKY)
+    sky_hdr: float = 1.0          # HDRLightContribution (renderer.h:224)
     spheres: list = dataclasses.field(default_factory=list)
     triangles: list = dataclasses.field(default_factory=list)
     spp: int = 1
@@ -212,6 +214,38 @@ class SceneDesc:
         d.camera = look_at(self._cam_pos, self._cam_target, width, height)
         d._cam_pos, d._cam_target = self._cam_pos, self._cam_target
         return d
+
+
+def synthetic_sky(width=512, height=256, sun=(0.35, 0.25)):
+    """Build-defined stand-in for assets/sky_19.hdr (missing from the reference tree,
+    SURVEY F7): an equirectangular RGB float image laid out like stbi_loadf's output (row v
+    = polar angle acos(D.y) / pi from the zenith, column u = atan2(D.z, D.x) / 2pi).  A
+    zenith-to-horizon gradient, a darker ground half and an HDR sun disc (values up to
+    ~40) so that misses exercise the full float range.  Deterministic (no RNG)."""
+    v = (np.arange(height, dtype=np.float64) + 0.5) / height          # 0 = zenith
+    u = (np.arange(width, dtype=np.float64) + 0.5) / width
+    theta = v[:, None] * np.pi
+    up = np.cos(theta)
+    zen = np.array([0.25, 0.45, 0.95])
+    hor = np.array([0.95, 0.9, 0.85])
+    gnd = np.array([0.18, 0.15, 0.12])
+    a = np.clip(up, 0.0, 1.0)[..., None]
+    sky = np.where((up > 0)[..., None], hor + (zen - hor) * a ** 0.6, gnd * (0.6 + 0.4 * (1 + up[..., None])))
+    img = np.broadcast_to(sky, (height, width, 3)).copy()
+    su, sv = sun
+    du = np.minimum(np.abs(u[None, :] - su), 1 - np.abs(u[None, :] - su)) * 2.0
+    dv = v[:, None] - sv
+    disc = np.exp(-(du * du + dv * dv) / (2 * 0.02 ** 2))
+    img += disc[..., None] * np.array([40.0, 36.0, 30.0])
+    return np.ascontiguousarray(img, np.float32)
+
+
+def with_sky(desc, texture=None, hdr_contribution=1.0):
+    """activateSky = true with a sky texture (Renderer::skyPixels, HDRLightContribution)."""
+    d = dataclasses.replace(desc, sky_texture=synthetic_sky() if texture is None else texture,
+                            sky_hdr=float(hdr_contribution), flags=desc.flags | abi.VPX_FLAG_SKY)
+    d._cam_pos, d._cam_target = desc._cam_pos, desc._cam_target
+    return d
 
 
 def look_at(pos, target, width, height):

@@ -238,6 +238,38 @@ def test_cpp_host_demo_matches_oracle(pkg, orc, tmp_path):
     assert np.array_equal(rgb_cpp, rgb)
 
 
+def demo_sky(w=64, h=32):
+    """host/vpx_demo.cpp demo_sky, restated in float32."""
+    v, u = np.meshgrid(np.arange(h), np.arange(w), indexing="ij")
+    t = np.empty((h, w, 3), np.float32)
+    t[..., 0] = u.astype(np.float32) / np.float32(w - 1) * np.float32(2.0)
+    t[..., 1] = v.astype(np.float32) / np.float32(h - 1)
+    t[..., 2] = np.float32(0.5) + ((u + v) % 7).astype(np.float32)
+    return t
+
+
+def test_cpp_host_demo_static_camera_sky(pkg, orc, tmp_path):
+    """The C++ mirror's static-camera Tick (vpx_render_reproject) with activateSky, against
+    the oracle's static branch: 2 frames, depth 2."""
+    import subprocess
+
+    exe = os.path.join(os.path.dirname(pkg.__file__), "host", "vpx_demo")
+    n, w, h, frames, depth = 64, 80, 48, 2, 2
+    out = tmp_path / "frame.rgb8"
+    r = subprocess.run([exe, str(n), str(w), str(h), str(frames), str(depth), str(out), "sk"], capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    rgb_cpp = np.fromfile(out, np.uint32)
+    sc = pkg.scene
+    desc = sc.with_sky(sc.pillars_scene(n, w, h, depth), texture=demo_sky(), hdr_contribution=1.5)
+    o = orc.Oracle(pkg.abi, desc)
+    prev = sc.prev_camera(desc._cam_pos, desc._cam_target, w, h)
+    hist = np.zeros((w * h, 4), np.float32)
+    for f in range(frames):
+        rgb, _ = o.render_reproject(desc.frame_params(f), prev, hist)
+    assert np.array_equal(rgb_cpp, rgb)
+
+
 def _render_on(pkg, r, desc, frames=1):
     r.ResetAccumulator()
     for _ in range(frames):
@@ -332,3 +364,67 @@ def test_static_camera_reprojection(pkg, orc, name, depth):
         assert np.array_equal(rgb_g, rgb_o), f"frame {f}: rgb8"
         assert (st.shadow_rays, st.bounce_rays, st.dda_cells) == (ost.shadow_rays, ost.bounce_rays, ost.dda_cells)
     r.ctx.close()
+
+
+# ---------------------------------------------------------------- sky dome (§8(f) rank 4)
+@pytest.mark.parametrize("depth", [0, 4])
+def test_trace_rays_sky_texture(pkg, orc, depth):
+    """Trace with activateSky: every miss samples the (synthetic) HDR texture — random
+    rays through the glass room (refraction / reflection chains that leave the grid) and
+    rays that miss from the start."""
+    from test_sky import miss_rays
+
+    sc = pkg.scene
+    desc = sc.with_sky(SCENES["room128_d4"](sc), hdr_contribution=1.3)
+    ctx = make_ctx(pkg, desc)
+    o = orc.Oracle(pkg.abi, desc)
+    org, dirs = random_rays(2048, 23 + depth)
+    mo, md = miss_rays(512, depth)
+    org, dirs = np.concatenate([org, mo]), np.concatenate([dirs, md])
+    rays = pkg.context.make_rays(org, dirs, inside=(np.arange(len(org)) % 5 == 0).astype(np.uint32))
+    seeds = np.random.default_rng(depth).integers(1, 2**32 - 1, len(org), dtype=np.uint64).astype(np.uint32)
+    rg = ctx.trace(rays, seeds, depth, None, desc.area_samples)
+    ro, _ = o.trace(rays, seeds, depth, None, desc.area_samples)
+    assert np.array_equal(bits(rg), bits(ro))
+    ctx.close()
+
+
+@pytest.mark.parametrize("name", ["teapot128", "room128_d4", "cityglass128_d4"])
+def test_render_frame_sky_texture(pkg, orc, name):
+    sc = pkg.scene
+    desc = sc.with_sky(SCENES[name](sc), hdr_contribution=0.8)
+    acc_g, rgb_g, st = render_gpu(pkg, desc)
+    o = orc.Oracle(pkg.abi, desc)
+    acc_o, rgb_o, ost = o.render(desc.frame_params(0))
+    assert np.array_equal(bits(acc_g), bits(acc_o))
+    assert np.array_equal(rgb_g, rgb_o)
+    assert (st[0].shadow_rays, st[0].dda_cells) == (ost.shadow_rays, ost.dda_cells)
+
+
+def test_static_camera_reprojection_sky_texture(pkg, orc):
+    """SampleSkyReproject (renderer.cpp:2328-2346) on the static-camera path."""
+    sc = pkg.scene
+    desc = sc.with_sky(sc.model_scene("roomGlass", 64, 48, 32, 2, city_lights=True))
+    r = pkg.renderer.Renderer(desc, 0)
+    r.Init()
+    r.staticCamera = True
+    o = orc.Oracle(pkg.abi, desc)
+    hist_o = np.zeros((desc.width * desc.height, 4), np.float32)
+    prev = sc.prev_camera(desc._cam_pos, desc._cam_target, desc.width, desc.height)
+    for f in range(2):
+        r.Tick(0.0)
+        torch.cuda.synchronize()
+        rgb_o, _ = o.render_reproject(desc.frame_params(f), prev, hist_o)
+        assert np.array_equal(bits(r.history_host().reshape(-1, 4)), bits(hist_o)), f"frame {f}: history"
+        assert np.array_equal(r.screen_host().reshape(-1), rgb_o), f"frame {f}: rgb8"
+    r.ctx.close()
+
+
+def test_sky_flag_without_texture_is_refused(pkg):
+    desc = SCENES["teapot128"](pkg.scene)
+    desc.flags |= pkg.abi.VPX_FLAG_SKY
+    ctx = make_ctx(pkg, desc)
+    acc = torch.zeros(desc.width * desc.height * 4, dtype=torch.float32, device="cuda")
+    with pytest.raises(pkg.abi.VpxError):
+        ctx.render(desc.frame_params(0), acc.data_ptr())
+    ctx.close()

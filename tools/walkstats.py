@@ -44,12 +44,12 @@ tmax = ((np.ceil(pos) - ds) * cell - cp) * rD
 st = np.concatenate([t0[:, None], tmax, tdel], 1).astype(np.float32)
 si = np.concatenate([P0, step], 1).astype(np.int32)
 # ---- box-choice simulation on primary rays and shadow rays toward the lights
-lib.walk_sim.argtypes = [V, V, V, C.c_uint32, V, V, V, C.c_uint32, V, V]
+lib.walk_sim.argtypes = [V, V, V, C.c_uint32, V, V, V, C.c_uint32, V, V, V]
 def sim(st_, si_, bnd, tout=None):
     o = np.zeros(8, np.uint64)
     lib.walk_sim(cells.ctypes.data, l1.ctypes.data, l2.ctypes.data, n, np.ascontiguousarray(st_).ctypes.data,
                  np.ascontiguousarray(si_).ctypes.data, np.ascontiguousarray(bnd, np.float32).ctypes.data, len(st_),
-                 o.ctypes.data, None if tout is None else tout.ctypes.data)
+                 o.ctypes.data, None if tout is None else tout.ctypes.data, None)
     return o
 def dda_state(org, dirs):
     with np.errstate(divide="ignore", invalid="ignore"):
