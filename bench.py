@@ -8,10 +8,13 @@ with its shadow ray(s), accumulate + tonemap + RGB8, all inside libvpx_hip.so's 
 render kernel.  Inputs (world, tables, accumulator) are resident in HBM before timing.
 
 N > 1 (torchrun, one rank per GPU): weak scaling — the frame grows with N (N x 1920x1080
-pixels), its 16x16 tiles are dealt round-robin to ranks, each rank renders its tiles into a
-packed buffer, an RCCL gather (torch.distributed, backend nccl) brings them to rank 0,
-which composites (unpack + accumulate + tonemap).  Timed region: barrier + sync on both
-sides, max over ranks.  value = all rays of all ranks / that time.
+pixels), its 16x16 tiles are dealt round-robin to ranks.  Default (--gather rgb8): each rank
+accumulates and tonemaps its own tiles (the accumulator is sharded with them) and an RCCL
+gather (torch.distributed, backend nccl) brings the packed RGB8 to rank 0's screen; the
+gather of frame f overlaps the render of frame f+1.  --gather samples: ranks send float4
+samples and rank 0 composites (unpack + accumulate + tonemap) into its full accumulator.
+Timed region: barrier + sync on both sides (the last frame's gather included), max over
+ranks.  value = all rays of all ranks / that time.
 
 roofline: algorithmic bytes of the render kernel per launch = DDA cells read x 1 B +
 W*H*36 B (accumulator float4 read+write + RGB8 write), SURVEY.md §8(d) / DESIGN.md §5,
@@ -134,7 +137,10 @@ def run(args):
     torch.cuda.synchronize()
     acc = torch.zeros(W * H * 4, dtype=torch.float32, device="cuda") if rank == 0 else None
     rgb = torch.zeros(W * H, dtype=torch.int32, device="cuda") if rank == 0 else None
-    if n > 1:
+    sharded = None
+    if n > 1 and args.gather == "rgb8":
+        sharded = pkg.dist.ShardedAccumFrame(ctx, desc, rank, n, torch.device("cuda", dev), host_gather=shared)
+    elif n > 1:
         L = ctx.packed_len(W, H, n)
         packed = torch.zeros(L * 4, dtype=torch.float32, device="cuda")
         gbuf = torch.empty(n * L * 4, dtype=torch.float32, device="cuda") if rank == 0 else None
@@ -151,6 +157,11 @@ def run(args):
             e0.record(stream)
         if n == 1:
             ctx.render(p, acc.data_ptr(), rgb.data_ptr())
+            if record:
+                e1.record(stream)
+        elif sharded is not None:
+            sharded.frame = frame[0]
+            sharded.step()
             if record:
                 e1.record(stream)
         else:
@@ -173,6 +184,8 @@ def run(args):
 
     for _ in range(args.warmup):
         step()
+    if sharded is not None:
+        sharded.flush()
     torch.cuda.synchronize()
     ctx.counters(reset=True)
     # per-stage HIP events on the library's stream (the same stream the kernels run on)
@@ -184,6 +197,8 @@ def run(args):
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step(record=True)
+    if sharded is not None:
+        sharded.flush()  # the last frame's gather + scatter belong to the timed region
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -232,8 +247,9 @@ def run(args):
                                    f"Trace depth {desc.max_bounces} (primary+shadow)",
                        "width": W, "height": H, "world_n": desc.grids[0].n, "max_bounces": desc.max_bounces,
                        "spp": 1, "parallelism": "single GPU" if n == 1 else (
-                           f"tile-shard x{n} + RCCL gather to rank 0" if not shared
-                           else f"REHEARSAL: {n} ranks sharing one GPU, gloo gather via host")},
+                           (f"tile-shard x{n}, accumulator sharded, RCCL gather of RGB8 to rank 0 (overlapped)"
+                            if args.gather == "rgb8" else f"tile-shard x{n} + RCCL gather of samples to rank 0")
+                           if not shared else f"REHEARSAL: {n} ranks sharing one GPU, gloo gather via host")},
             "rays_per_step": {"primary": prim / K, "shadow": shad / K, "dda_cells": cells / K},
             "mpix_per_s": round(prim / elapsed / 1e6, 3),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -261,6 +277,8 @@ def main():
     ap.add_argument("--config", default="C1")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--gather", choices=("rgb8", "samples"), default="rgb8",
+                    help="N>1: sharded accumulator + RGB8 gather (default) or float4 samples to rank 0")
     run(ap.parse_args())
 
 

@@ -252,6 +252,19 @@ int vpx_render_tiles(vpx_ctx* ctx, const vpx_frame_params* params, uint32_t tile
 /* Number of float4 elements one rank's packed buffer holds (all ranks use the max). */
 uint64_t vpx_tiles_packed_len(uint32_t width, uint32_t height, uint32_t tile_w,
                               uint32_t tile_h, uint32_t n_ranks);
+/* Tile-sharded render with the accumulator sharded with the tiles: the rank keeps the
+   running average of ITS tiles in `accum_packed` (float4[vpx_tiles_packed_len], DEVICE,
+   persistent across frames, packed layout as vpx_render_tiles; blended with weight
+   1/(frame_index+1) like vpx_render's accumulator, so start it finite, e.g. zeroed) and
+   tonemaps them into `rgb8_packed` (uint32[len], DEVICE) — the only bytes rank 0 needs
+   for the screen.  Bit-identical to vpx_render's accumulator / screen for those pixels. */
+int vpx_render_tiles_accum(vpx_ctx* ctx, const vpx_frame_params* params, uint32_t tile_w,
+                           uint32_t tile_h, uint32_t rank, uint32_t n_ranks, float* accum_packed,
+                           uint32_t* rgb8_packed, vpx_stats* stats);
+/* Rank 0: scatter n_ranks gathered packed RGB8 buffers (back to back, DEVICE) into the
+   screen rgb8 (uint32[W*H], DEVICE). */
+int vpx_composite_rgb8(vpx_ctx* ctx, const vpx_frame_params* params, uint32_t tile_w,
+                       uint32_t tile_h, uint32_t n_ranks, const uint32_t* gathered, uint32_t* rgb8);
 /* Rank-0 composite: `gathered` = n_ranks packed buffers back to back (DEVICE); unpack,
    accumulate into accum and tonemap into rgb8 exactly like vpx_render's epilogue.      */
 int vpx_composite_tiles(vpx_ctx* ctx, const vpx_frame_params* params, uint32_t tile_w,

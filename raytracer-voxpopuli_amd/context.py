@@ -125,6 +125,18 @@ class Context:
                   "vpx_render_tiles")
         return st
 
+    def render_tiles_accum(self, params, rank, n_ranks, accum_packed_ptr, rgb_packed_ptr, stats=False, tile=16):
+        """This rank's tiles, accumulated into its own packed accumulator + packed RGB8."""
+        st = abi.Stats() if stats else None
+        self._chk(self.lib.vpx_render_tiles_accum(self.h, C.byref(params), tile, tile, rank, n_ranks,
+                                                  C.c_void_p(accum_packed_ptr), C.c_void_p(rgb_packed_ptr),
+                                                  C.byref(st) if st is not None else None), "vpx_render_tiles_accum")
+        return st
+
+    def composite_rgb8(self, params, n_ranks, gathered_ptr, rgb_ptr, tile=16):
+        self._chk(self.lib.vpx_composite_rgb8(self.h, C.byref(params), tile, tile, n_ranks, C.c_void_p(gathered_ptr),
+                                              C.c_void_p(rgb_ptr)), "vpx_composite_rgb8")
+
     def packed_len(self, width, height, n_ranks, tile=16):
         return int(self.lib.vpx_tiles_packed_len(width, height, tile, tile, n_ranks))
 

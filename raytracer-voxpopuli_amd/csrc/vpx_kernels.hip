@@ -5,6 +5,7 @@
 //                                 per bounce level (vpx_wavefront.hpp); one lane per pixel,
 //                                 16x16-pixel tiles per 256-thread workgroup (16x4 wave strips)
 //   composite_tiles               rank-0 unpack + accumulate + tonemap of gathered tiles.
+//   composite_rgb8                rank-0 unpack of gathered RGB8 tiles (sharded accumulator).
 //   find_nearest_k / is_occluded_k / trace_k   per-ray unit entries.
 //   tiled_world_k / checksum_k    world generator and grid checksum.
 #include <hip/hip_runtime.h>
@@ -39,6 +40,18 @@ __global__ __launch_bounds__(kThreads) void composite_tiles(FrameArgs f, const f
     const float4 a = blend(accum[p], mk(s.x, s.y, s.z), f.weight, f.inv_weight);
     accum[p] = a;
     if (rgb8) rgb8[p] = tonemap_pack(a);
+}
+
+// Rank-0 scatter of the gathered packed RGB8 tiles (sharded-accumulator flow).
+__global__ __launch_bounds__(kThreads) void composite_rgb8(FrameArgs f, const uint32_t* __restrict__ gathered,
+                                                           uint32_t* __restrict__ rgb8) {
+    const uint32_t tile = blockIdx.x;
+    const uint32_t lx = threadIdx.x & 15u, ly = threadIdx.x >> 4;
+    const uint32_t x = (tile % f.tiles_x) * kTile + lx;
+    const uint32_t y = (tile / f.tiles_x) * kTile + ly;
+    if (x >= f.width || y >= f.height) return;
+    const uint32_t r = tile % f.n_ranks, j = tile / f.n_ranks;
+    rgb8[(uint64_t)y * f.width + x] = gathered[((uint64_t)r * f.tiles_per_rank + j) * (kTile * kTile) + threadIdx.x];
 }
 
 // ------------------------------------------------------------------ unit entries
@@ -532,7 +545,7 @@ struct Reproj {  // the static-camera tail (vpx_render_reproject)
     float4 *alb, *ill, *rd, *temp, *hist;
 };
 
-template <bool PACKED>
+template <int MODE>
 int launch_render(vpx_ctx* c, const SceneView& sv, const FrameArgs& f, uint32_t tiles, float4* accum, uint32_t* rgb8,
                   float4* packed, const Reproj* rp = nullptr) {
     const uint32_t P = tiles * (uint32_t)kTilePix;
@@ -566,7 +579,7 @@ int launch_render(vpx_ctx* c, const SceneView& sv, const FrameArgs& f, uint32_t 
     }
     prof_mark(c, VPX_STAGE_FINISH);
     if (!rp) {
-        hipLaunchKernelGGL((k_finish<PACKED>), grid, block, 0, c->stream, f, w, accum, rgb8, packed);
+        hipLaunchKernelGGL((k_finish<MODE>), grid, block, 0, c->stream, f, w, accum, rgb8, packed);
     } else {  // Renderer::Tick static branch, second pass (renderer.cpp:2024-2100)
         hipLaunchKernelGGL(k_finish_reproject, grid, block, 0, c->stream, f, w, rp->alb, rp->ill);
         hipLaunchKernelGGL(k_reproject_setup, grid, block, 0, c->stream, f, w, rp->prev);
@@ -932,7 +945,7 @@ int vpx_render(vpx_ctx* c, const vpx_frame_params* p, float* accum, uint32_t* rg
     const SceneView sv = view_of(c, p->sky, p->area_samples, (p->flags & VPX_FLAG_SKY) != 0);
     const FrameArgs f = frame_of(c, p, 0, 1);
     if (stats) VPX_HIP(c, hipEventRecord(c->ev0, c->stream));
-    if ((rc = launch_render<false>(c, sv, f, f.num_tiles, reinterpret_cast<float4*>(accum), rgb8, nullptr))) return rc;
+    if ((rc = launch_render<kFinishImage>(c, sv, f, f.num_tiles, reinterpret_cast<float4*>(accum), rgb8, nullptr))) return rc;
     if (stats) {
         VPX_HIP(c, hipEventRecord(c->ev1, c->stream));
         unsigned long long after[kCtrWords];
@@ -975,7 +988,7 @@ int vpx_render_reproject(vpx_ctx* c, const vpx_frame_params* p, const vpx_prev_c
     FrameArgs f = frame_of(c, p, 0, 1);
     f.flags = (f.flags & ~(VPX_FLAG_AA | VPX_FLAG_DOF)) | kFlagReproject;  // GetPrimaryRayNoDOF
     if (stats) VPX_HIP(c, hipEventRecord(c->ev0, c->stream));
-    if ((rc = launch_render<false>(c, sv, f, f.num_tiles, nullptr, rgb8, nullptr, &rp))) return rc;
+    if ((rc = launch_render<kFinishImage>(c, sv, f, f.num_tiles, nullptr, rgb8, nullptr, &rp))) return rc;
     if (stats) {
         VPX_HIP(c, hipEventRecord(c->ev1, c->stream));
         unsigned long long after[kCtrWords];
@@ -996,21 +1009,27 @@ uint64_t vpx_tiles_packed_len(uint32_t width, uint32_t height, uint32_t tile_w, 
     return ((tiles + n_ranks - 1) / n_ranks) * (uint64_t)(kTile * kTile);
 }
 
-int vpx_render_tiles(vpx_ctx* c, const vpx_frame_params* p, uint32_t tile_w, uint32_t tile_h, uint32_t rank,
-                     uint32_t n_ranks, float* packed, vpx_stats* stats) {
+// Shared body of vpx_render_tiles (packed samples) and vpx_render_tiles_accum (this rank's
+// packed accumulator + RGB8); MODE is a FinishMode.
+static int render_tiles_impl(int MODE, vpx_ctx* c, const vpx_frame_params* p, uint32_t tile_w, uint32_t tile_h,
+                             uint32_t rank, uint32_t n_ranks, float4* accum, uint32_t* rgb8, float4* packed,
+                             vpx_stats* stats) {
     if (!c) return VPX_E_INVALID;
     int rc = validate_frame(c, p);
     if (rc) return rc;
     if (tile_w != kTile || tile_h != kTile) return fail(c, VPX_E_INVALID, "tiles must be 16x16");
-    if (n_ranks == 0 || rank >= n_ranks || !packed) return fail(c, VPX_E_INVALID, "bad rank / packed buffer");
+    if (n_ranks == 0 || rank >= n_ranks) return fail(c, VPX_E_INVALID, "bad rank");
+    if (MODE == kFinishPackedSample ? !packed : (!accum || !rgb8))
+        return fail(c, VPX_E_INVALID, "null packed buffer");
     VPX_HIP(c, hipSetDevice(c->device));
     unsigned long long before[kCtrWords] = {};
     if (stats && (rc = snapshot_counters(c, before))) return rc;
     const SceneView sv = view_of(c, p->sky, p->area_samples, (p->flags & VPX_FLAG_SKY) != 0);
     const FrameArgs f = frame_of(c, p, rank, n_ranks);
     if (stats) VPX_HIP(c, hipEventRecord(c->ev0, c->stream));
-    if ((rc = launch_render<true>(c, sv, f, f.tiles_per_rank, nullptr, nullptr, reinterpret_cast<float4*>(packed))))
-        return rc;
+    rc = MODE == kFinishPackedSample ? launch_render<kFinishPackedSample>(c, sv, f, f.tiles_per_rank, accum, rgb8, packed)
+                                     : launch_render<kFinishPackedAccum>(c, sv, f, f.tiles_per_rank, accum, rgb8, packed);
+    if (rc) return rc;
     if (stats) {
         VPX_HIP(c, hipEventRecord(c->ev1, c->stream));
         unsigned long long after[kCtrWords];
@@ -1022,6 +1041,30 @@ int vpx_render_tiles(vpx_ctx* c, const vpx_frame_params* p, uint32_t tile_w, uin
         stats->kernel_ms = ms;
         stats->total_ms = ms;
     }
+    return VPX_OK;
+}
+
+int vpx_render_tiles(vpx_ctx* c, const vpx_frame_params* p, uint32_t tile_w, uint32_t tile_h, uint32_t rank,
+                     uint32_t n_ranks, float* packed, vpx_stats* stats) {
+    return render_tiles_impl(kFinishPackedSample, c, p, tile_w, tile_h, rank, n_ranks, nullptr, nullptr,
+                                                  reinterpret_cast<float4*>(packed), stats);
+}
+
+int vpx_render_tiles_accum(vpx_ctx* c, const vpx_frame_params* p, uint32_t tile_w, uint32_t tile_h, uint32_t rank,
+                           uint32_t n_ranks, float* accum_packed, uint32_t* rgb8_packed, vpx_stats* stats) {
+    return render_tiles_impl(kFinishPackedAccum, c, p, tile_w, tile_h, rank, n_ranks,
+                                                 reinterpret_cast<float4*>(accum_packed), rgb8_packed, nullptr, stats);
+}
+
+int vpx_composite_rgb8(vpx_ctx* c, const vpx_frame_params* p, uint32_t tile_w, uint32_t tile_h, uint32_t n_ranks,
+                       const uint32_t* gathered, uint32_t* rgb8) {
+    if (!c || !p || !gathered || !rgb8) return fail(c, VPX_E_INVALID, "null argument");
+    if (tile_w != kTile || tile_h != kTile || n_ranks == 0) return fail(c, VPX_E_INVALID, "tiles must be 16x16");
+    if (p->width == 0 || p->height == 0) return fail(c, VPX_E_INVALID, "empty frame");
+    VPX_HIP(c, hipSetDevice(c->device));
+    const FrameArgs f = frame_of(c, p, 0, n_ranks);
+    hipLaunchKernelGGL(composite_rgb8, dim3(f.num_tiles), dim3(kThreads), 0, c->stream, f, gathered, rgb8);
+    VPX_HIP(c, hipGetLastError());
     return VPX_OK;
 }
 

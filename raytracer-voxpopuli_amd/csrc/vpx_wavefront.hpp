@@ -670,9 +670,13 @@ __device__ __forceinline__ float4 blend(float4 acc, f3 px, float w, float iw) {
                        fmaf(iw, acc.w, 0.0f * w));
 }
 
-// Fold the level records bottom-up (the recursion's rounding order) and either
-// accumulate + tonemap in place (PACKED = false) or write the raw sample (PACKED = true).
-template <bool PACKED>
+// k_finish output modes: the image accumulator + screen (one GPU), the raw sample per packed
+// slot (rank-0 composite), or a rank's own packed accumulator + packed RGB8 (the
+// accumulator sharded with the tiles; only the RGB8 travels).
+enum FinishMode : int { kFinishImage = 0, kFinishPackedSample = 1, kFinishPackedAccum = 2 };
+
+// Fold the level records bottom-up (the recursion's rounding order), then write per MODE.
+template <int MODE>
 __global__ __launch_bounds__(256) void k_finish(FrameArgs f, WaveBufs w, float4* __restrict__ accum,
                                                 uint32_t* __restrict__ rgb8, float4* __restrict__ packed) {
     const uint32_t p = blockIdx.x * 256u + threadIdx.x;
@@ -700,8 +704,17 @@ __global__ __launch_bounds__(256) void k_finish(FrameArgs f, WaveBufs w, float4*
             }
         }
     }
-    if (PACKED) {
+    if (MODE == kFinishPackedSample) {
         packed[p] = make_float4(v.x, v.y, v.z, 0.0f);
+    } else if (MODE == kFinishPackedAccum) {  // accum / rgb8 are this rank's packed buffers
+        if (valid) {
+            const float4 a = blend(accum[p], v, f.weight, f.inv_weight);
+            accum[p] = a;
+            rgb8[p] = tonemap_pack(a);
+        } else {
+            accum[p] = make_float4(0.f, 0.f, 0.f, 0.f);
+            rgb8[p] = 0u;
+        }
     } else if (valid) {
         const uint64_t px = (uint64_t)y * f.width + x;
         if (f.flags & VPX_FLAG_NO_TONEMAP) {

@@ -11,6 +11,16 @@ Layout contract (shared with libvpx_hip.so's vpx_render_tiles / vpx_composite_ti
 There is one exchange per frame (the gather); the world is replicated per GPU.  Over
 RCCL (torch.distributed backend "nccl") the gather is R-1 point-to-point transfers into
 rank 0, each on its own xGMI link on an MI355X node.
+
+Two flows share that layout:
+  - ShardedFrame: ranks send raw float4 samples (16 B/pixel); rank 0 owns the whole
+    accumulator and composites (vpx_render_tiles + vpx_composite_tiles).
+  - ShardedAccumFrame (bench default): the accumulator is sharded with the tiles — each
+    rank keeps the running average of its own pixels and tonemaps them
+    (vpx_render_tiles_accum), so only packed RGB8 (4 B/pixel) travels, and rank 0 only
+    scatters it into the screen (vpx_composite_rgb8).  The gather of frame f is issued
+    asynchronously and overlaps the render of frame f+1 (double-buffered RGB8).  Screen and
+    accumulator values are bit-identical to the single-GPU frame.
 """
 import numpy as np
 
@@ -61,6 +71,27 @@ def unpack(gathered, width, height, n_ranks):
     return img
 
 
+def unpack_u32(gathered, width, height, n_ranks):
+    """Host reference of vpx_composite_rgb8: R packed uint32 buffers -> W*H screen."""
+    L = packed_len(width, height, n_ranks)
+    g = np.asarray(gathered).view(np.uint32).reshape(n_ranks, L)
+    img = np.zeros(width * height, np.uint32)
+    for r in range(n_ranks):
+        ids = rank_pixel_ids(width, height, r, n_ranks)
+        ok = ids >= 0
+        img[ids[ok]] = g[r][ok]
+    return img
+
+
+def gather_async(buf, rank, n_ranks, out_parts=None, group=None):
+    """Start the gather of every rank's packed buffer into rank 0's `out_parts` (list of
+    R tensors, rank 0 only).  Returns the torch.distributed work handle: RCCL runs it on
+    its own stream, so the caller's stream keeps rendering until work.wait()."""
+    import torch.distributed as dist
+
+    return dist.gather(buf, out_parts if rank == 0 else None, dst=0, group=group, async_op=True)
+
+
 def gather_tiles(packed, rank, n_ranks, out=None, group=None):
     """Gather every rank's packed tensor to rank 0 (torch.distributed; RCCL on GPUs,
     gloo on CPU).  Returns the concatenated [R*L*4] tensor on rank 0, None elsewhere."""
@@ -103,3 +134,60 @@ class ShardedFrame:
         if self.rank == 0:
             self.ctx.composite_tiles(p, self.n, g.data_ptr(), self.accum.data_ptr(), self.screen.data_ptr())
         self.frame += 1
+
+
+class ShardedAccumFrame:
+    """One rank's share with the accumulator sharded (see the module docstring).  GPU
+    path: libvpx_hip.so + RCCL; `host_gather=True` routes the gather through host memory
+    (gloo), for rehearsing N ranks on one GPU."""
+
+    def __init__(self, ctx, desc, rank, n_ranks, device, host_gather=False):
+        import torch
+
+        self.ctx, self.desc, self.rank, self.n = ctx, desc, rank, n_ranks
+        self.host = host_gather
+        w, h = desc.width, desc.height
+        self.L = ctx.packed_len(w, h, n_ranks)
+        assert self.L == packed_len(w, h, n_ranks)
+        self.accum = torch.zeros(self.L * 4, dtype=torch.float32, device=device)  # this rank's pixels
+        self.rgb = [torch.zeros(self.L, dtype=torch.int32, device=device) for _ in range(2)]
+        if rank == 0:
+            self.gathered = [torch.empty(n_ranks * self.L, dtype=torch.int32, device=device) for _ in range(2)]
+            self.parts = [list(g.view(n_ranks, self.L)) for g in self.gathered]  # gather straight into place
+            self.screen = torch.zeros(w * h, dtype=torch.int32, device=device)
+        self.pending = None  # (work, buffer, params) of the frame whose gather is in flight
+        self.frame = 0
+
+    def _finish(self):
+        work, b, p = self.pending
+        self.pending = None
+        if work is not None:
+            work.wait()  # the render stream waits for the RCCL stream (no host block)
+        if self.rank == 0:
+            self.ctx.composite_rgb8(p, self.n, self.gathered[b].data_ptr(), self.screen.data_ptr())
+
+    def step(self):
+        import torch
+        import torch.distributed as dist
+
+        p = self.desc.frame_params(frame_index=self.frame)
+        b = self.frame & 1
+        self.ctx.render_tiles_accum(p, self.rank, self.n, self.accum.data_ptr(), self.rgb[b].data_ptr())
+        if self.pending is not None:
+            self._finish()  # frame f-1: its gather overlapped this render
+        if self.host:
+            torch.cuda.current_stream().synchronize()
+            parts = [torch.empty(self.L, dtype=torch.int32) for _ in range(self.n)] if self.rank == 0 else None
+            dist.gather(self.rgb[b].cpu(), parts, dst=0)
+            if self.rank == 0:
+                self.gathered[b].copy_(torch.cat(parts))
+            self.pending = (None, b, p)
+        else:
+            self.pending = (gather_async(self.rgb[b], self.rank, self.n, self.parts[b] if self.rank == 0 else None),
+                            b, p)
+        self.frame += 1
+
+    def flush(self):
+        """Complete the last frame (its gather and rank 0's scatter)."""
+        if self.pending is not None:
+            self._finish()

@@ -48,6 +48,57 @@ def _worker(rank, world, port, w, h, q):
         dist.destroy_process_group()
 
 
+def _worker_rgb8(rank, world, port, w, h, q):
+    """Sharded-accumulator flow: each rank owns the accumulator of its tiles and sends only
+    packed RGB8; the gather is started asynchronously (double-buffered, one frame in flight)
+    exactly as dist.ShardedAccumFrame does."""
+    sys.path.insert(0, REPO)
+    import __graft_entry__ as entry
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        pkg, orc = entry.load_package(), entry.load_oracle()
+        desc = pkg.scene.model_scene("monu3", 64, w, h, 1, city_lights=True)
+        desc.flags = pkg.abi.VPX_FLAG_AA
+        o = orc.Oracle(pkg.abi, desc)
+        ids = pkg.dist.rank_pixel_ids(w, h, rank, world)
+        L = ids.size
+        bufs = [torch.zeros(L, dtype=torch.int32) for _ in range(2)]
+        outs = [torch.empty(world * L, dtype=torch.int32) for _ in range(2)]
+        acc = None
+        pending, ok = None, True
+        for f in range(3):
+            acc, rgb, _ = o.render(desc.frame_params(f), accum=acc, threads=2)  # stands in for render_tiles_accum
+            b = f & 1
+            mine = np.zeros(L, np.uint32)
+            mine[ids >= 0] = rgb[ids[ids >= 0]]
+            bufs[b].copy_(torch.from_numpy(mine.view(np.int32)))
+            if pending is not None:
+                work, pb, prgb = pending
+                work.wait()
+                if rank == 0:
+                    ok &= bool(np.array_equal(pkg.dist.unpack_u32(outs[pb].numpy(), w, h, world), prgb))
+            parts = list(outs[b].view(world, L)) if rank == 0 else None
+            pending = (pkg.dist.gather_async(bufs[b], rank, world, parts), b, rgb.copy())
+        work, pb, prgb = pending
+        work.wait()
+        if rank == 0:
+            ok &= bool(np.array_equal(pkg.dist.unpack_u32(outs[pb].numpy(), w, h, world), prgb))
+            q.put(ok)
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_accumulator_rgb8_gather_two_ranks_gloo():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    mp.start_processes(_worker_rgb8, args=(2, port, 40, 24, q), nprocs=2, join=True, start_method="spawn")
+    assert q.get(timeout=60) is True
+
+
 @pytest.mark.parametrize("wh", [(40, 24), (33, 17)])
 def test_gather_two_ranks_gloo(wh):
     ctx = mp.get_context("spawn")

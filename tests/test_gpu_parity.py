@@ -150,6 +150,32 @@ def test_tiles_composite_equals_monolithic(pkg, orc):
     ctx.close()
 
 
+def test_sharded_accumulator_equals_monolithic(pkg, orc):
+    """The bench's multi-GPU flow on one device: R ranks accumulate their own tiles
+    (vpx_render_tiles_accum) over 3 AA frames, rank 0 scatters the RGB8 (vpx_composite_rgb8);
+    screen and every rank's packed accumulator equal vpx_render's frames bit for bit."""
+    desc = pkg.scene.city_scene("monu3", 128, 100, 70, 1)
+    desc.flags = pkg.abi.VPX_FLAG_AA
+    acc_ref, rgb_ref, _ = render_gpu(pkg, desc, frames=3)
+    ctx = make_ctx(pkg, desc)
+    R = 3
+    W, H = desc.width, desc.height
+    L = ctx.packed_len(W, H, R)
+    accs = [torch.zeros(L * 4, dtype=torch.float32, device="cuda") for _ in range(R)]
+    gathered = torch.zeros(R * L, dtype=torch.int32, device="cuda")
+    rgb = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+    for f in range(3):
+        p = desc.frame_params(f)
+        for rank in range(R):
+            ctx.render_tiles_accum(p, rank, R, accs[rank].data_ptr(), gathered.data_ptr() + rank * L * 4)
+        ctx.composite_rgb8(p, R, gathered.data_ptr(), rgb.data_ptr())
+    ctx.synchronize()
+    assert np.array_equal(rgb.cpu().numpy().view(np.uint32), rgb_ref)
+    acc_img = pkg.dist.unpack(np.concatenate([a.cpu().numpy() for a in accs]), W, H, R)
+    assert np.array_equal(bits(acc_img), bits(acc_ref))
+    ctx.close()
+
+
 def test_tiled_world_generator_matches_oracle(pkg, orc):
     for model, n in (("monu3", 256), ("roomGlass", 320)):
         spec, _, _ = pkg.scene.tiled_grid(model, n)
