@@ -558,22 +558,24 @@ int launch_render(vpx_ctx* c, const SceneView& sv, const FrameArgs& f, uint32_t 
     const dim3 grid(tiles), block(kThreads);
     const size_t slds = sizeof(uint32_t) * S * kThreads * kGroupTiles;
     const dim3 ggrid((tiles + kGroupTiles - 1) / kGroupTiles);
+    // single volume, no analytic shapes: the DDA kernels' lean instances
+    const bool one = sv.num_volumes == 1 && !(sv.num_spheres | sv.num_triangles);
     prof_mark(c, VPX_STAGE_PRIMARY);
-    hipLaunchKernelGGL(k_primary, grid, block, 0, c->stream, sv, f, w, c->d_ctr);
+    hipLaunchKernelGGL(one ? k_primary<true> : k_primary<false>, grid, block, 0, c->stream, sv, f, w, c->d_ctr);
     prof_mark(c, -1);
     for (int level = 0; level <= f.max_bounces; ++level) {
         prof_mark(c, VPX_STAGE_SHADE);
         hipLaunchKernelGGL(k_shade, grid, block, 0, c->stream, sv, f, w, level, c->d_ctr);
         prof_mark(c, -1);
         prof_mark(c, VPX_STAGE_SHADOW);
-        hipLaunchKernelGGL(k_shadow_tile, ggrid, block, slds, c->stream, sv, w, c->d_ctr);
+        hipLaunchKernelGGL(one ? k_shadow_tile<true> : k_shadow_tile<false>, ggrid, block, slds, c->stream, sv, w, c->d_ctr);
         prof_mark(c, -1);
         prof_mark(c, VPX_STAGE_RESOLVE);
         hipLaunchKernelGGL(k_resolve, grid, block, 0, c->stream, sv, w);
         prof_mark(c, -1);
         if (level < f.max_bounces) {
             prof_mark(c, VPX_STAGE_BOUNCE);
-            hipLaunchKernelGGL(k_nearest_tile, ggrid, block, 0, c->stream, sv, w, c->d_ctr);
+            hipLaunchKernelGGL(one ? k_nearest_tile<true> : k_nearest_tile<false>, ggrid, block, 0, c->stream, sv, w, c->d_ctr);
             prof_mark(c, -1);
         }
     }
@@ -583,7 +585,7 @@ int launch_render(vpx_ctx* c, const SceneView& sv, const FrameArgs& f, uint32_t 
     } else {  // Renderer::Tick static branch, second pass (renderer.cpp:2024-2100)
         hipLaunchKernelGGL(k_finish_reproject, grid, block, 0, c->stream, f, w, rp->alb, rp->ill);
         hipLaunchKernelGGL(k_reproject_setup, grid, block, 0, c->stream, f, w, rp->prev);
-        hipLaunchKernelGGL(k_shadow_tile, ggrid, block, slds, c->stream, sv, w, c->d_ctr);
+        hipLaunchKernelGGL(one ? k_shadow_tile<true> : k_shadow_tile<false>, ggrid, block, slds, c->stream, sv, w, c->d_ctr);
         hipLaunchKernelGGL(k_reproject_resolve, grid, block, 0, c->stream, f, w, rp->alb, rp->ill, rp->hist, rp->temp,
                            rgb8);
         VPX_HIP(c, hipMemcpyAsync(rp->hist, rp->temp, sizeof(float4) * (size_t)f.width * f.height,

@@ -316,7 +316,6 @@ constexpr uint32_t kStepThreshold = VPX_STEP_THRESHOLD;
 #define VPX_MINC_SHADOW 1
 #endif
 constexpr int kStepUnroll = VPX_STEP_UNROLL;  // cell steps per step-phase iteration
-
 #ifdef VPX_ASM_MARKS  // analysis builds only: label the walk phases in the ISA listing
 #define VPX_MARK(s) asm volatile("; MARK " s)
 #else

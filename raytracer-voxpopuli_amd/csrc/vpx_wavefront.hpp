@@ -496,9 +496,53 @@ __device__ __forceinline__ void nearest_record(SceneView sv, const WaveBufs& w, 
     w.HM[p] = r.mat | ((uint32_t)(vox + 2) << 8) | (r.inside ? 0x80000000u : 0u);
 }
 
+// Object-space ray of path p in the single volume (FindNearest's SSE transforms).
+__device__ __forceinline__ ORay path_oray(const vpx_volume& vol, const WaveBufs& w, uint32_t p) {
+    const float4 o = w.O[p], d = w.D[p];
+    ORay r;
+    r.O = xform_pos_ssem(mk(o.x, o.y, o.z), vol.inv_matrix);
+    r.D = xform_vec_ssem(mk(d.x, d.y, d.z), vol.inv_matrix);
+    r.rD = mk(__fdiv_rn(1.0f, r.D.x), __fdiv_rn(1.0f, r.D.y), __fdiv_rn(1.0f, r.D.z));
+    return r;
+}
+
+// nearest_record for the single-volume, shape-free scene: the same result, but only the
+// walk state lives across the walk — the ray is read back from the path buffers and
+// transformed again for the normal (the same operations, so the same values), which
+// keeps the walker's registers from spilling.
+template <uint32_t SKIPW = VPX_SKIPW_NEAREST, uint32_t MINC = VPX_MINC_NEAREST>
+__device__ __forceinline__ void nearest_record_1v(const SceneView& sv, const WaveBufs& w, uint32_t p, Counters& k) {
+    const vpx_volume* vol = uni_ptr(&sv.volumes[0]);
+    const DevGrid g = sv.grids[vol->grid_id];
+    ++k.nearest;
+    bool hit = false;
+    skip::Walk wk;
+    {
+        const ORay o = path_oray(*vol, w, p);
+        Dda s;
+        if (dda_setup(*vol, g.n, o, s)) {
+            wk = to_walk(s);
+            hit = walk_wave<0, SKIPW, MINC>(grid_view(g), wk, kBig, k.cells);
+        }
+    }
+    asm volatile("" ::: "memory");  // re-read the ray below instead of keeping it live
+    const uint32_t inside = __float_as_uint(w.D[p].w) & kInside ? 0x80000000u : 0u;
+    if (!hit) {
+        w.H[p] = make_float4(kBig, 0.f, 0.f, 0.f);
+        w.HM[p] = kNone | inside;  // vox -2
+        return;
+    }
+    const ORay o = path_oray(*vol, w, p);
+    const f3 N = normal_voxel(o, wk.t, g.n, vol->matrix);
+    const uint32_t mat = g.cells[(uint64_t)wk.X + (uint64_t)wk.Y * g.n + (uint64_t)wk.Z * ((uint64_t)g.n * g.n)];
+    w.H[p] = make_float4(wk.t, N.x, N.y, N.z);
+    w.HM[p] = mat | (2u << 8) | inside;  // vox 0
+}
+
 // Primary rays + Renderer::FindNearest.  Every path's ray / RNG state is written; rays
 // that cannot hit a voxel or shape (one volume, no shapes, Setup3DDDA fails: the
 // reference returns before reading a cell) get their miss record directly.
+template <bool ONE>
 __global__ __launch_bounds__(256) VPX_WPE(VPX_WPE_NEAREST) void k_primary(SceneView sv, FrameArgs f, WaveBufs w,
                                                  unsigned long long* __restrict__ ctr) {
     __shared__ uint32_t sh[4];
@@ -531,7 +575,7 @@ __global__ __launch_bounds__(256) VPX_WPE(VPX_WPE_NEAREST) void k_primary(SceneV
         w.D[p] = make_float4(r.D.x, r.D.y, r.D.z, __uint_as_float(flags));
         if (go) {
             walk = true;
-            if (sv.num_volumes == 1 && !(sv.num_spheres | sv.num_triangles)) {
+            if (ONE) {
                 const vpx_volume& vol = sv.volumes[0];
                 ORay o;
                 o.O = xform_pos_ssem(r.O, vol.inv_matrix);
@@ -553,12 +597,16 @@ __global__ __launch_bounds__(256) VPX_WPE(VPX_WPE_NEAREST) void k_primary(SceneV
     __syncthreads();
     if (threadIdx.x < total) {
         const uint32_t q = lst[threadIdx.x];
-        const float4 o = w.O[q], d = w.D[q];
-        Ray r;
-        r.O = mk(o.x, o.y, o.z);
-        r.D = mk(d.x, d.y, d.z);
-        r.inside = false;
-        nearest_record(sv, w, q, r, k);
+        if (ONE) {
+            nearest_record_1v(sv, w, q, k);
+        } else {
+            const float4 o = w.O[q], d = w.D[q];
+            Ray r;
+            r.O = mk(o.x, o.y, o.z);
+            r.D = mk(d.x, d.y, d.z);
+            r.inside = false;
+            nearest_record(sv, w, q, r, k);
+        }
     }
     flush_counters(k, prim, ctr, VPX_STAGE_PRIMARY);
 }
@@ -583,6 +631,7 @@ __device__ __forceinline__ uint32_t group_scan(const uint32_t (&cnt)[G], uint32_
 }
 
 // Renderer::FindNearest for the active paths of G tiles (bounce levels).
+template <bool ONE>
 __global__ __launch_bounds__(256) VPX_WPE(VPX_WPE_NEAREST) void k_nearest_tile(SceneView sv, WaveBufs w, unsigned long long* __restrict__ ctr) {
     __shared__ uint32_t sh[4];
     __shared__ uint32_t lst[256 * kGroupTiles];
@@ -602,6 +651,10 @@ __global__ __launch_bounds__(256) VPX_WPE(VPX_WPE_NEAREST) void k_nearest_tile(S
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < total; i += 256u) {
         const uint32_t q = lst[i];
+        if (ONE) {
+            nearest_record_1v<VPX_SKIPW_BOUNCE, VPX_MINC_BOUNCE>(sv, w, q, k);
+            continue;
+        }
         const float4 o = w.O[q], d = w.D[q];
         Ray r;
         r.O = mk(o.x, o.y, o.z);
@@ -614,6 +667,7 @@ __global__ __launch_bounds__(256) VPX_WPE(VPX_WPE_NEAREST) void k_nearest_tile(S
 
 // Renderer::IsOccluded for the shadow slots of G tiles (entry = slot << 27 | path); sets
 // the slot's occluded flag.  The light sums are formed in slot order by k_resolve.
+template <bool ONE>
 __global__ __launch_bounds__(256) VPX_WPE(VPX_WPE_SHADOW) void k_shadow_tile(SceneView sv, WaveBufs w, unsigned long long* __restrict__ ctr) {
     __shared__ uint32_t sh[4];
     extern __shared__ uint32_t lst_dyn[];  // [S * 256 * G]
@@ -637,6 +691,29 @@ __global__ __launch_bounds__(256) VPX_WPE(VPX_WPE_SHADOW) void k_shadow_tile(Sce
     for (uint32_t i = threadIdx.x; i < total; i += 256u) {
         const uint32_t e = lst_dyn[i];
         const uint64_t slot = (uint64_t)(e >> 27) * w.P + (e & 0x07ffffffu);
+        if (ONE) {
+            // Renderer::IsOccluded in the single volume with only the walk state live
+            // across the walk (the slot flags are read back afterwards)
+            const vpx_volume* vol = uni_ptr(&sv.volumes[0]);
+            const DevGrid g = sv.grids[vol->grid_id];
+            ++k.shadow;
+            bool hit = false;
+            {
+                const float4 so = w.SO[slot], sd = w.SD[slot];
+                ORay o;
+                o.O = xform_pos(mk(so.x, so.y, so.z), vol->inv_matrix);
+                o.D = xform_vec(mk(sd.x, sd.y, sd.z), vol->inv_matrix);
+                o.rD = mk(__fdiv_rn(1.0f, o.D.x), __fdiv_rn(1.0f, o.D.y), __fdiv_rn(1.0f, o.D.z));
+                Dda s;
+                if (dda_setup(*vol, g.n, o, s)) {
+                    skip::Walk wk = to_walk(s);
+                    hit = walk_wave<16, VPX_SKIPW_SHADOW, VPX_MINC_SHADOW>(grid_view(g), wk, so.w, k.cells);
+                }
+            }
+            asm volatile("" ::: "memory");
+            if (hit) w.SD[slot].w = __uint_as_float(__float_as_uint(w.SD[slot].w) | 4u /* occluded */);
+            continue;
+        }
         const float4 so = w.SO[slot], sd = w.SD[slot];
         Ray r;
         r.O = mk(so.x, so.y, so.z);

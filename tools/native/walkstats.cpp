@@ -53,6 +53,8 @@ extern "C" void build_slabs(const uint8_t* bocc, uint32_t nb) {  // bocc[z][y][x
         }
 }
 static uint64_t g_slabskips;
+static uint64_t g_seg2[4];  // skips by the number of axes that need the second closed-form segment
+extern "C" void seg2_out(uint64_t* o) { for (int i = 0; i < 4; ++i) o[i] = g_seg2[i], g_seg2[i] = 0; }
 extern "C" uint64_t slab_out() { const uint64_t v = g_slabskips; g_slabskips = 0; return v; }
 
 // rays: st = (t, tx, ty, tz, dx, dy, dz), si = (X, Y, Z, sx, sy, sz) per ray; out[8] =
@@ -128,6 +130,18 @@ extern "C" void walk_sim(const uint8_t* cells, const uint64_t* l1, const uint64_
                 df_box(w, n, lo, hi);
                 if (slab) for (int q = 0; q < 3; ++q) lo[q] = slo[q], hi[q] = shi[q];
                 const uint32_t olo[3] = {lo[0], lo[1], lo[2]}, ohi[3] = {hi[0], hi[1], hi[2]};
+                {
+                    Axis ax[3];
+                    const float hh[3] = {w.tx, w.ty, w.tz}, dd[3] = {w.dx, w.dy, w.dz};
+                    const int32_t sg[3] = {w.sx, w.sy, w.sz};
+                    const uint32_t c3[3] = {w.X, w.Y, w.Z};
+                    int n2 = 0;
+                    for (int k = 0; k < 3; ++k) {
+                        axis_setup(hh[k], dd[k], sg[k] > 0 ? hi[k] - c3[k] : c3[k] - lo[k], ax[k]);
+                        n2 += ax[k].l > ax[k].m1;
+                    }
+                    g_seg2[n2]++;
+                }
                 Walk t = w;
                 uint32_t cc = 0;
                 const int sr = skip_box_lean(t, lo, hi, bound, cc);

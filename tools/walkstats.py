@@ -100,3 +100,5 @@ for name, (a, b, bnd), mode in [(nm_, v, md) for nm_, v in sets.items() for md i
     print(f"   steps in empty bricks with a cube below the skip minimum: {lib.small_out() / R:.1f} per ray")
     cr = np.zeros(16, np.uint64); lib.cross_out.argtypes = [V]; lib.cross_out(cr.ctypes.data)
     print("   clipped boxes by binade crossings of the full box (max over axes):", cr[:10])
+    s2 = np.zeros(4, np.uint64); lib.seg2_out.argtypes = [V]; lib.seg2_out(s2.ctypes.data)
+    print("   skips by #axes needing the 2nd segment:", s2, "frac any:", round(float(s2[1:].sum()) / max(1, float(s2.sum())), 4))
