@@ -4,8 +4,9 @@
 
 A step = one frame of the C1 workload (BASELINE.json configs[1]): 1920x1080, 1024^3 world
 (monu3.vox tiled), 1 spp, Trace depth 0 = primary ray + one light sample
-with its shadow ray(s), accumulate + tonemap + RGB8, all inside libvpx_hip.so's single
-render kernel.  Inputs (world, tables, accumulator) are resident in HBM before timing.
+with its shadow ray(s), accumulate + tonemap + RGB8: one vpx_render call (the wavefront
+kernels of DESIGN.md §4).  Inputs (world, tables, accumulator) are resident in HBM before
+timing.
 
 N > 1 (torchrun, one rank per GPU): weak scaling — the frame grows with N (N x 1920x1080
 pixels), its 16x16 tiles are dealt round-robin to ranks.  Default (--gather rgb8): each rank
@@ -16,9 +17,12 @@ samples and rank 0 composites (unpack + accumulate + tonemap) into its full accu
 Timed region: barrier + sync on both sides (the last frame's gather included), max over
 ranks.  value = all rays of all ranks / that time.
 
-roofline: algorithmic bytes of the render kernel per launch = DDA cells read x 1 B +
-W*H*36 B (accumulator float4 read+write + RGB8 write), SURVEY.md §8(d) / DESIGN.md §5,
-divided by the kernel's average duration measured with HIP events on its own stream.
+roofline: the dominant stage (largest device time in the last warmup frame, where every
+stage is timed): its algorithmic bytes per launch = DDA cells read x 1 B (the finish stage:
+W*H*36 B, accumulator float4 read+write + RGB8 write), SURVEY.md §8(d) / DESIGN.md §4,
+divided by its average launch duration measured with HIP events on the library's stream
+over the timed region (only that stage is timed there: each timed launch adds two event
+records to the stream).
 cpu_baseline: the CPU restatement (oracle/, C, -O2) on a bounded pixel sample of the same
 frame on this host's cores (rank 0, N = 1 only).
 """
@@ -147,27 +151,16 @@ def run(args):
         gathered = list(gbuf.view(n, L * 4)) if rank == 0 else None  # gather straight into gbuf
 
     frame = [0]
-    ev = []
 
-    def step(record=False):
+    def step():
         p = desc.frame_params(frame_index=frame[0])
-        e0 = e1 = None
-        if record:
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
         if n == 1:
             ctx.render(p, acc.data_ptr(), rgb.data_ptr())
-            if record:
-                e1.record(stream)
         elif sharded is not None:
             sharded.frame = frame[0]
             sharded.step()
-            if record:
-                e1.record(stream)
         else:
             ctx.render_tiles(p, rank, n, packed.data_ptr())
-            if record:
-                e1.record(stream)
             if shared:
                 stream.synchronize()
                 parts = [torch.empty(L * 4) for _ in range(n)] if rank == 0 else None
@@ -178,36 +171,46 @@ def run(args):
                 dist.gather(packed, gathered, dst=0)
             if rank == 0:
                 ctx.composite_tiles(p, n, gbuf.data_ptr(), acc.data_ptr(), rgb.data_ptr())
-        if record:
-            ev.append((e0, e1))
         frame[0] += 1
 
-    for _ in range(args.warmup):
+    launches = 4 * (desc.max_bounces + 1) + 4  # stage launches per frame, upper bound
+    # the last warmup frame times every stage (HIP events on the library's stream): the stage split
+    # and the dominant stage; the timed region then times only that stage, since every
+    # timed launch adds two event records to the stream (all five C1 stages: +4.3 %)
+    ctx.profile_select(None)
+    for i in range(args.warmup):
+        if i == args.warmup - 1:  # the last warmup frame (the first ones carry cold-start costs)
+            if sharded is not None:
+                sharded.flush()
+            torch.cuda.synchronize()
+            ctx.profile_enable(launches)
+            ctx.profile_read(reset=True)
         step()
     if sharded is not None:
         sharded.flush()
     torch.cuda.synchronize()
+    warm = ctx.profile_read(reset=True)
+    timed_stages = [max(warm, key=lambda k: warm[k][0])] if args.warmup > 0 else None
     ctx.counters(reset=True)
-    # per-stage HIP events on the library's stream (the same stream the kernels run on)
-    ctx.profile_enable(args.steps * (4 * (desc.max_bounces + 1) + 4))
+    ctx.profile_select(timed_stages)
+    ctx.profile_enable(args.steps * launches)
     ctx.profile_read(reset=True)
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step(record=True)
+        step()
     if sharded is not None:
         sharded.flush()  # the last frame's gather + scatter belong to the timed region
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    ks = [a.elapsed_time(b) for a, b in ev]
     st = ctx.counters()
     local_rays = float(st.primary_rays + st.shadow_rays)
-    vals = torch.tensor([elapsed, local_rays, float(st.primary_rays), float(st.shadow_rays), float(st.dda_cells),
-                         float(np.mean(ks))], dtype=torch.float64, device="cpu" if shared else "cuda")
+    vals = torch.tensor([elapsed, local_rays, float(st.primary_rays), float(st.shadow_rays), float(st.dda_cells)],
+                        dtype=torch.float64, device="cpu" if shared else "cuda")
     if dist:
         mx = vals.clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
@@ -215,10 +218,8 @@ def run(args):
         dist.all_reduce(sm, op=dist.ReduceOp.SUM)
         elapsed = mx[0].item()
         rays, prim, shad, cells = sm[1].item(), sm[2].item(), sm[3].item(), sm[4].item()
-        kernel_ms = mx[5].item()
     else:
         rays, prim, shad, cells = local_rays, float(st.primary_rays), float(st.shadow_rays), float(st.dda_cells)
-        kernel_ms = float(np.mean(ks))
     if rank == 0:
         K = args.steps
         ms_step = elapsed * 1000.0 / K
@@ -229,6 +230,7 @@ def run(args):
         prof = ctx.profile_read()
         dom = max(prof, key=lambda k: prof[k][0])
         dom_ms, dom_launches, dom_cells = prof[dom]
+        split = warm if timed_stages else prof
         kernel_ms = dom_ms / max(dom_launches, 1)
         if dom == "finish":
             alg_bytes = float(st.primary_rays) / K * 36.0
@@ -256,7 +258,8 @@ def run(args):
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                          "kernel": STAGE_KERNELS[dom], "kernel_ms": round(kernel_ms, 4),
                          "alg_bytes_per_launch": round(alg_bytes),
-                         "stages_ms": {k: round(v[0] / max(v[1], 1), 4) for k, v in prof.items() if v[1]},
+                         "stages_ms": {k: round(v[0] / max(v[1], 1), 4) for k, v in split.items() if v[1]},
+                         "stages_ms_from": "last warmup frame, every stage timed" if timed_stages else "timed region",
                          "frame_alg_bytes": round(frame_bytes),
                          "frame_achieved": round(frame_bytes / (ms_step * 1e-3) / 1e9, 2)},
             "cpu_baseline": None,

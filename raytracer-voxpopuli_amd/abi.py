@@ -151,6 +151,7 @@ SIGNATURES = {
     "vpx_prev_camera_look_at": (C.c_int, [C.POINTER(C.c_float), C.POINTER(C.c_float), C.c_uint32, C.c_uint32,
                                           C.POINTER(PrevCamera)]),
     "vpx_profile_enable": (C.c_int, [C.c_void_p, C.c_uint32]),
+    "vpx_profile_select": (C.c_int, [C.c_void_p, C.c_uint32]),
     "vpx_profile_read": (C.c_int, [C.c_void_p, C.POINTER(Profile), C.c_int]),
     "vpx_find_nearest": (C.c_int, [C.c_void_p, C.POINTER(Ray), C.c_uint32, C.POINTER(Hit)]),
     "vpx_is_occluded": (C.c_int, [C.c_void_p, C.POINTER(Ray), C.c_uint32, C.c_void_p]),

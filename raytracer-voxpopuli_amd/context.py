@@ -148,6 +148,11 @@ class Context:
     def profile_enable(self, max_launches):
         self._chk(self.lib.vpx_profile_enable(self.h, int(max_launches)), "vpx_profile_enable")
 
+    def profile_select(self, stages=None):
+        """Time only these stage names (abi.STAGES); None: all."""
+        mask = 0xFFFFFFFF if stages is None else sum(1 << abi.STAGES.index(s) for s in stages)
+        self._chk(self.lib.vpx_profile_select(self.h, mask), "vpx_profile_select")
+
     def profile_read(self, reset=True):
         """Per-stage device times / launches / DDA cells: {stage: (ms_total, launches, cells)}."""
         pr = abi.Profile()

@@ -347,6 +347,7 @@ struct vpx_ctx {
     std::vector<hipEvent_t> prof_ev;
     std::vector<int> prof_stage;
     uint32_t prof_cap = 0, prof_used = 0;
+    uint32_t prof_mask = 0xffffffffu;  // stages timed (vpx_profile_select)
     unsigned long long* d_sum = nullptr;
     void* d_scratch = nullptr;
     size_t scratch_bytes = 0;
@@ -531,6 +532,7 @@ int ensure_wave(vpx_ctx* c, uint32_t P, uint32_t L, uint32_t S) {
 // event pool lasts; a start without room for its end is not recorded.
 static void prof_mark(vpx_ctx* c, int stage) {
     if (!c->prof_cap) return;
+    if (stage >= 0 && !((c->prof_mask >> stage) & 1u)) return;  // not selected (its end is dropped too)
     if (stage >= 0 && c->prof_used + 2 > c->prof_cap) return;
     if (stage < 0 && (c->prof_used & 1u) == 0) return;  // its start was dropped
     if (hipEventRecord(c->prof_ev[c->prof_used], c->stream) != hipSuccess) return;
@@ -1186,6 +1188,12 @@ uint32_t vpx_pixel_seed(uint32_t base, uint32_t frame, uint32_t w, uint32_t h, u
 }
 
 }  // extern "C"
+
+extern "C" int vpx_profile_select(vpx_ctx* c, uint32_t stage_mask) {
+    if (!c) return VPX_E_INVALID;
+    c->prof_mask = stage_mask;
+    return VPX_OK;
+}
 
 extern "C" int vpx_profile_enable(vpx_ctx* c, uint32_t max_launches) {
     if (!c) return VPX_E_INVALID;
