@@ -327,6 +327,7 @@ struct vpx_ctx {
     uint32_t d_grids_cap = 0;
     std::vector<vpx_volume> volumes;
     vpx_volume* d_volumes = nullptr;
+    float4* d_vbounds = nullptr;  // per volume: world bounding sphere (centre, radius^2), see volume_bounds
     uint32_t d_volumes_cap = 0;
     vpx_material* d_materials = nullptr;
     vpx_point_light* d_points = nullptr;
@@ -430,6 +431,7 @@ SceneView view_of(const vpx_ctx* c, const float sky[3], int32_t area_samples, bo
     SceneView sv;
     sv.grids = c->d_grids;
     sv.volumes = c->d_volumes;
+    sv.vbounds = c->d_vbounds;
     sv.materials = c->d_materials;
     sv.points = c->d_points;
     sv.spots = c->d_spots;
@@ -656,7 +658,7 @@ int vpx_destroy(vpx_ctx* c) {
         if (g.l1) (void)hipFree(g.l1);
         if (g.l2) (void)hipFree(g.l2);
     }
-    void* ptrs[] = {c->d_grids, c->d_volumes, c->d_materials, c->d_points, c->d_spots, c->d_areas,
+    void* ptrs[] = {c->d_grids, c->d_volumes, c->d_vbounds, c->d_materials, c->d_points, c->d_spots, c->d_areas,
                     c->d_spheres, c->d_triangles, c->d_ctr, c->d_sum, c->d_scratch, c->d_wave, c->d_sky};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
@@ -848,18 +850,68 @@ int vpx_grid_checksum(vpx_ctx* c, uint32_t id, uint64_t* out) {
     return VPX_OK;
 }
 
+// World-space bounding sphere of a volume's cube, for the volume cull in find_nearest /
+// is_occluded: the cube [b0, b1] mapped by the inverse of inv_matrix (the matrix the walk
+// actually uses, inverted in double), inflated far beyond float rounding (0.1 % of the
+// radius + 1e-3 of the scale) so a ray that misses it also misses the cube in the
+// reference's float arithmetic.  A singular or non-affine inv_matrix disables the cull.
+static float4 volume_bounds(const vpx_volume& v) {
+    const float* m = v.inv_matrix;
+    const double a[3][3] = {{m[0], m[1], m[2]}, {m[4], m[5], m[6]}, {m[8], m[9], m[10]}};
+    const double det = a[0][0] * (a[1][1] * a[2][2] - a[1][2] * a[2][1]) -
+                       a[0][1] * (a[1][0] * a[2][2] - a[1][2] * a[2][0]) +
+                       a[0][2] * (a[1][0] * a[2][1] - a[1][1] * a[2][0]);
+    const float4 none = make_float4(0.f, 0.f, 0.f, INFINITY);
+    if (!(std::fabs(det) > 1e-30) || m[12] != 0.f || m[13] != 0.f || m[14] != 0.f || m[15] != 1.f) return none;
+    double r[3][3];  // inverse of the 3x3 part
+    r[0][0] = (a[1][1] * a[2][2] - a[1][2] * a[2][1]) / det;
+    r[0][1] = (a[0][2] * a[2][1] - a[0][1] * a[2][2]) / det;
+    r[0][2] = (a[0][1] * a[1][2] - a[0][2] * a[1][1]) / det;
+    r[1][0] = (a[1][2] * a[2][0] - a[1][0] * a[2][2]) / det;
+    r[1][1] = (a[0][0] * a[2][2] - a[0][2] * a[2][0]) / det;
+    r[1][2] = (a[0][2] * a[1][0] - a[0][0] * a[1][2]) / det;
+    r[2][0] = (a[1][0] * a[2][1] - a[1][1] * a[2][0]) / det;
+    r[2][1] = (a[0][1] * a[2][0] - a[0][0] * a[2][1]) / det;
+    r[2][2] = (a[0][0] * a[1][1] - a[0][1] * a[1][0]) / det;
+    const double t[3] = {m[3], m[7], m[11]};
+    double pts[8][3], cen[3] = {0, 0, 0};
+    for (int k = 0; k < 8; ++k) {
+        const double q[3] = {(k & 1) ? v.b1[0] : v.b0[0], (k & 2) ? v.b1[1] : v.b0[1], (k & 4) ? v.b1[2] : v.b0[2]};
+        for (int i = 0; i < 3; ++i) {
+            pts[k][i] = r[i][0] * (q[0] - t[0]) + r[i][1] * (q[1] - t[1]) + r[i][2] * (q[2] - t[2]);
+            cen[i] += pts[k][i] / 8.0;
+        }
+    }
+    double rad = 0.0;
+    for (int k = 0; k < 8; ++k)
+        rad = std::max(rad, std::sqrt((pts[k][0] - cen[0]) * (pts[k][0] - cen[0]) + (pts[k][1] - cen[1]) * (pts[k][1] - cen[1]) +
+                                      (pts[k][2] - cen[2]) * (pts[k][2] - cen[2])));
+    const double scale = 1.0 + std::fabs(cen[0]) + std::fabs(cen[1]) + std::fabs(cen[2]) + rad;
+    const double rr = rad * 1.001 + 1e-3 * scale;
+    if (!std::isfinite(rr)) return none;
+    return make_float4((float)cen[0], (float)cen[1], (float)cen[2], (float)(rr * rr));
+}
+
 int vpx_set_volumes(vpx_ctx* c, const vpx_volume* v, uint32_t count) {
     if (!c || (!v && count)) return fail(c, VPX_E_INVALID, "null argument");
     if (count > 65536) return fail(c, VPX_E_INVALID, "too many volumes");
     VPX_HIP(c, hipStreamSynchronize(c->stream));
     if (count > c->d_volumes_cap) {
         if (c->d_volumes) (void)hipFree(c->d_volumes);
+        if (c->d_vbounds) (void)hipFree(c->d_vbounds);
         c->d_volumes = nullptr;
+        c->d_vbounds = nullptr;
         VPX_HIP(c, hipMalloc(&c->d_volumes, sizeof(vpx_volume) * count));
+        VPX_HIP(c, hipMalloc(&c->d_vbounds, sizeof(float4) * count));
         c->d_volumes_cap = count;
     }
     c->volumes.assign(v, v + count);
-    if (count) VPX_HIP(c, hipMemcpy(c->d_volumes, v, sizeof(vpx_volume) * count, hipMemcpyHostToDevice));
+    std::vector<float4> bounds(count);
+    for (uint32_t i = 0; i < count; ++i) bounds[i] = volume_bounds(v[i]);
+    if (count) {
+        VPX_HIP(c, hipMemcpy(c->d_volumes, v, sizeof(vpx_volume) * count, hipMemcpyHostToDevice));
+        VPX_HIP(c, hipMemcpy(c->d_vbounds, bounds.data(), sizeof(float4) * count, hipMemcpyHostToDevice));
+    }
     return VPX_OK;
 }
 

@@ -48,6 +48,7 @@ struct DevGrid {
 struct SceneView {
     const DevGrid* grids;
     const vpx_volume* volumes;
+    const float4* vbounds;  // per volume: world bounding sphere (xyz centre, w radius^2), inflated
     const vpx_material* materials;
     const vpx_point_light* points;
     const vpx_spot_light* spots;
@@ -561,28 +562,60 @@ struct Counters {
     uint32_t nearest;
 };
 
+// Volume cull: true when the ray's line misses the volume's inflated world bounding sphere,
+// or the sphere lies wholly behind an origin outside it — then the object-space cube test
+// of Setup3DDDA (Cube::Contains / Cube::Intersect, scene.cpp:166-210) fails too, so the
+// reference reads no cell of that volume and skipping it changes nothing.  The margin
+// (vpx_kernels.hip volume_bounds) dwarfs the float rounding of both tests.
+#ifndef VPX_VOLUME_CULL
+#define VPX_VOLUME_CULL 1
+#endif
+__device__ __forceinline__ bool misses_volume(const float4 b, f3 o, f3 d) {
+    if (!VPX_VOLUME_CULL) return false;
+    const f3 oc = mk(b.x, b.y, b.z) - o;
+    const float oc2 = dot(oc, oc), bb = dot(oc, d), dd = dot(d, d);
+    const bool outside = oc2 > b.w;
+    return outside && (bb < 0.0f || bb * bb < (oc2 - b.w) * dd);
+}
+
 // Renderer::FindNearest, renderer.cpp:946-1018.  Linear loop over the volumes with the
 // SSE transforms; a later volume wins only with a strictly smaller t (ties -> lowest index).
+// The winner's normal and material are formed once after the loop (the reference forms
+// them at every improving hit; the last one is the winner's, from the same object-space
+// ray and t), so only t and the hit cell are carried through the walks.
 template <uint32_t SKIPW = VPX_SKIPW_NEAREST, uint32_t MINC = VPX_MINC_NEAREST>
 __device__ __forceinline__ int32_t find_nearest(const SceneView& sv, Ray& r, Counters& k) {
     int32_t vox = -2;
     ++k.nearest;
+    uint32_t hx = 0, hy = 0, hz = 0;  // hit cell in volume `vox`
     for (uint32_t i = 0; i < sv.num_volumes; ++i) {
+        if (misses_volume(sv.vbounds[i], r.O, r.D)) continue;  // Setup3DDDA would fail
         const vpx_volume& vol = sv.volumes[i];
+        const DevGrid g = sv.grids[vol.grid_id];
+        skip::Walk w;
+        {
+            ORay o;
+            o.O = xform_pos_ssem(r.O, vol.inv_matrix);
+            o.D = xform_vec_ssem(r.D, vol.inv_matrix);
+            o.rD = mk(__fdiv_rn(1.0f, o.D.x), __fdiv_rn(1.0f, o.D.y), __fdiv_rn(1.0f, o.D.z));
+            Dda s;
+            if (!dda_setup(vol, g.n, o, s)) continue;
+            w = to_walk(s);
+        }
+        if (walk_wave<0, SKIPW, MINC>(grid_view(g), w, r.t, k.cells)) {
+            r.t = w.t;
+            hx = w.X, hy = w.Y, hz = w.Z;
+            vox = (int32_t)i;
+        }
+    }
+    if (vox >= 0) {
+        const vpx_volume& vol = sv.volumes[vox];
+        const DevGrid g = sv.grids[vol.grid_id];
         ORay o;
         o.O = xform_pos_ssem(r.O, vol.inv_matrix);
         o.D = xform_vec_ssem(r.D, vol.inv_matrix);
-        o.rD = mk(__fdiv_rn(1.0f, o.D.x), __fdiv_rn(1.0f, o.D.y), __fdiv_rn(1.0f, o.D.z));
-        const DevGrid g = sv.grids[vol.grid_id];
-        Dda s;
-        if (!dda_setup(vol, g.n, o, s)) continue;
-        skip::Walk w = to_walk(s);
-        if (walk_wave<0, SKIPW, MINC>(grid_view(g), w, r.t, k.cells)) {
-            r.t = w.t;
-            r.N = normal_voxel(o, w.t, g.n, vol.matrix);
-            r.mat = g.cells[(uint64_t)w.X + (uint64_t)w.Y * g.n + (uint64_t)w.Z * ((uint64_t)g.n * g.n)];
-            vox = (int32_t)i;
-        }
+        r.N = normal_voxel(o, r.t, g.n, vol.matrix);
+        r.mat = g.cells[(uint64_t)hx + (uint64_t)hy * g.n + (uint64_t)hz * ((uint64_t)g.n * g.n)];
     }
     if (sv.num_spheres | sv.num_triangles) {
         Ray sh = make_ray(r.O, r.D);
@@ -602,6 +635,7 @@ __device__ __forceinline__ int32_t find_nearest(const SceneView& sv, Ray& r, Cou
 // Renderer::IsOccluded, renderer.cpp:209-243 (scalar transforms, exact 1/D).
 __device__ __forceinline__ bool is_occluded(const SceneView& sv, const Ray& r, Counters& k) {
     for (uint32_t i = 0; i < sv.num_volumes; ++i) {
+        if (misses_volume(sv.vbounds[i], r.O, r.D)) continue;  // Setup3DDDA would fail
         const vpx_volume& vol = sv.volumes[i];
         ORay o;
         o.O = xform_pos(r.O, vol.inv_matrix);

@@ -460,6 +460,15 @@ __global__ __launch_bounds__(256) void k_resolve(SceneView sv, WaveBufs w) {
 #ifndef VPX_WPE_SHADOW
 #define VPX_WPE_SHADOW 6
 #endif
+// The multi-volume / shape instances (C4) carry the volume loop's state across the walks:
+// at 6 waves/SIMD they spilled 45-53 VGPRs.  Measured C4 (ms, FindNearest / IsOccluded
+// stages): 6 -> 2.98 / 2.50, 5 -> 2.13 / 2.40, 4 (no spills) -> 1.72 / 2.59.
+#ifndef VPX_WPE_MULTI_NEAREST
+#define VPX_WPE_MULTI_NEAREST 4
+#endif
+#ifndef VPX_WPE_MULTI_SHADOW
+#define VPX_WPE_MULTI_SHADOW 5
+#endif
 
 #define VPX_WPE(n) __attribute__((amdgpu_waves_per_eu(n)))
 
@@ -543,7 +552,7 @@ __device__ __forceinline__ void nearest_record_1v(const SceneView& sv, const Wav
 // that cannot hit a voxel or shape (one volume, no shapes, Setup3DDDA fails: the
 // reference returns before reading a cell) get their miss record directly.
 template <bool ONE>
-__global__ __launch_bounds__(256) VPX_WPE(VPX_WPE_NEAREST) void k_primary(SceneView sv, FrameArgs f, WaveBufs w,
+__global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_NEAREST : VPX_WPE_MULTI_NEAREST) void k_primary(SceneView sv, FrameArgs f, WaveBufs w,
                                                  unsigned long long* __restrict__ ctr) {
     __shared__ uint32_t sh[4];
     __shared__ uint32_t lst[256];
@@ -632,7 +641,7 @@ __device__ __forceinline__ uint32_t group_scan(const uint32_t (&cnt)[G], uint32_
 
 // Renderer::FindNearest for the active paths of G tiles (bounce levels).
 template <bool ONE>
-__global__ __launch_bounds__(256) VPX_WPE(VPX_WPE_NEAREST) void k_nearest_tile(SceneView sv, WaveBufs w, unsigned long long* __restrict__ ctr) {
+__global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_NEAREST : VPX_WPE_MULTI_NEAREST) void k_nearest_tile(SceneView sv, WaveBufs w, unsigned long long* __restrict__ ctr) {
     __shared__ uint32_t sh[4];
     __shared__ uint32_t lst[256 * kGroupTiles];
     const uint32_t base = blockIdx.x * 256u * kGroupTiles;
@@ -668,7 +677,7 @@ __global__ __launch_bounds__(256) VPX_WPE(VPX_WPE_NEAREST) void k_nearest_tile(S
 // Renderer::IsOccluded for the shadow slots of G tiles (entry = slot << 27 | path); sets
 // the slot's occluded flag.  The light sums are formed in slot order by k_resolve.
 template <bool ONE>
-__global__ __launch_bounds__(256) VPX_WPE(VPX_WPE_SHADOW) void k_shadow_tile(SceneView sv, WaveBufs w, unsigned long long* __restrict__ ctr) {
+__global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_SHADOW : VPX_WPE_MULTI_SHADOW) void k_shadow_tile(SceneView sv, WaveBufs w, unsigned long long* __restrict__ ctr) {
     __shared__ uint32_t sh[4];
     extern __shared__ uint32_t lst_dyn[];  // [S * 256 * G]
     const uint32_t base = blockIdx.x * 256u * kGroupTiles;
