@@ -217,6 +217,45 @@ def test_multi_volume_transforms_shapes(pkg, orc):
     assert np.array_equal(bits(acc_g), bits(acc_o)) and np.array_equal(rgb_g, rgb_o)
 
 
+def test_volume_cull_grazing_rays(pkg, orc):
+    """The device culls volumes whose inflated world bounding sphere a ray misses
+    (vpx_trace.hpp misses_volume); rays aimed at the corners and edges of rotated, scaled
+    instances, from outside and inside them, must still match the oracle's full loop."""
+    sc, abi = pkg.scene, pkg.abi
+    desc = sc.model_scene("monu3", 64, 32, 24, 0, city_lights=True)
+    vols = [sc.volume((0.1, 0.1, 0.1), (0.1, 0.1, 0.1), (0.3, 1.1, 0.2))]
+    rng = np.random.default_rng(11)
+    for _ in range(12):
+        pos = tuple(rng.uniform(-1.0, 1.0, 3))
+        scl = tuple(rng.uniform(0.05, 0.4, 3))
+        rot = tuple(rng.uniform(-3.1, 3.1, 3))
+        vols.append(sc.volume(pos, scl, rot, grid_id=0))
+    desc.volumes = (abi.Volume * len(vols))(*vols)
+    targets = []
+    for v in vols:
+        m = np.array(v.matrix, np.float64).reshape(4, 4)
+        b0, b1 = np.array(v.b0, np.float64), np.array(v.b1, np.float64)
+        for _ in range(96):
+            u = rng.integers(0, 2, 3).astype(np.float64)
+            u[rng.integers(0, 3)] = rng.uniform(0, 1)  # a point on an edge (or a corner)
+            p = b0 + (b1 - b0) * u + rng.normal(0, 1e-5, 3) * (b1 - b0)
+            targets.append((m @ np.append(p, 1.0))[:3])
+    targets = np.array(targets)
+    org = targets + rng.normal(0, 1, targets.shape) * rng.choice([0.02, 0.5, 2.0], (len(targets), 1))
+    org = np.concatenate([org, targets[::-1] + rng.normal(0, 1e-3, targets.shape)])
+    tgt = np.concatenate([targets, targets])
+    rays = pkg.context.make_rays(org.astype(np.float32), (tgt - org).astype(np.float32))
+    ctx = make_ctx(pkg, desc)
+    o = orc.Oracle(pkg.abi, desc)
+    g = cmp_hits(pkg, ctx.find_nearest(rays), o.find_nearest(rays), len(rays))
+    assert (g["vox_index"] >= 1).sum() > 50  # instances are hit, not only the main grid
+    srays = pkg.context.make_rays(org.astype(np.float32), (tgt - org).astype(np.float32),
+                                  tmax=rng.uniform(0.05, 5.0, len(org)))
+    occ_o, _ = o.is_occluded(srays)
+    assert np.array_equal(ctx.is_occluded(srays), occ_o)
+    ctx.close()
+
+
 def test_smoke_material_exits(pkg, orc):
     """Smoke and glass volumes exercise FindSmokeExit / FindMaterialExit."""
     sc = pkg.scene
