@@ -49,6 +49,15 @@ per = np.zeros((len(st), 2), np.uint32)
 out = np.zeros(8, np.uint64)
 lib.walk_sim.argtypes = [V, V, V, C.c_uint32, V, V, V, C.c_uint32, V, V, V]
 bnd = np.full(len(st), 1e34, np.float32)
+MODE = int(os.environ.get("MODE", "0"))  # walkstats box experiments (1: anisotropic slabs)
+if MODE:
+    nbk = nb[0]
+    bocc = np.ascontiguousarray((np.pad(cells.reshape(n, n, n), [(0, nbk * 4 - n)] * 3, constant_values=255)
+                                .reshape(nbk, 4, nbk, 4, nbk, 4) != 255).any(axis=(1, 3, 5)).astype(np.uint8))
+    lib.build_slabs.argtypes = [V, C.c_uint32]
+    lib.build_slabs(bocc.ctypes.data, nbk)
+    lib.set_mode.argtypes = [C.c_int]
+    lib.set_mode(MODE)
 lib.walk_sim(cells.ctypes.data, l1.ctypes.data, l2.ctypes.data, n, st.ctypes.data, si.ctypes.data, bnd.ctypes.data,
              len(st), out.ctypes.data, None, per.ctypes.data)
 SKIP = float(os.environ.get("SKIPCOST", "5.8"))
