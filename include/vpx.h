@@ -31,10 +31,14 @@
  *   vpx_set_shapes        Renderer::spheres/triangles renderer.h:207-208
  *   vpx_set_camera        Renderer::camera            renderer.h:181, template/camera.h:14-192
  *   vpx_set_sky           Renderer::skyPixels (+ SampleSky) renderer.cpp:691, 2308-2326
+ *   vpx_bvh_set           Renderer::bvh (BasicBVH)    renderer.h:220, src/BVH/BasicBVH.cpp:72-136
+ *   vpx_bvh_intersect     BasicBVH::IntersectBVH      src/BVH/BasicBVH.cpp:19-70
  * Host-side helpers that restate reference host code (no GPU needed):
  *   vpx_camera_look_at       Camera::HandleInput basis   template/camera.h:113-181
  *   vpx_volume_set_transform Scene::SetTransform         template/scene.cpp:373-405
  *   vpx_default_materials    Renderer::MaterialSetUp     renderer.cpp:357-443
+ *   vpx_bvh_build_host       BasicBVH::BuildBVH          src/BVH/BasicBVH.cpp:72-136
+ *   vpx_bvh_random_tris      BasicBVH::BasicBVH()        src/BVH/BasicBVH.cpp:4-16
  */
 #ifndef VPX_H_
 #define VPX_H_
@@ -330,6 +334,27 @@ int vpx_trace(vpx_ctx* ctx, const vpx_ray* rays, const uint32_t* seeds, uint32_t
 /* Focus ray of Renderer::Tick (world-space ray against every Scene::FindNearest). */
 int vpx_focus_distance(vpx_ctx* ctx, uint32_t width, uint32_t height, float* focal_distance);
 
+/* ---- BasicBVH (src/BVH/BasicBVH.{h,cpp}) ----------------------- */
+/* The reference's triangle BVH: midpoint split on the longest axis, leaves of <= 2
+   triangles, recursive left-then-right traversal that only shortens Ray::t.  A Renderer
+   member (renderer.h:220) that Renderer::Trace does not call; offered as the reference
+   offers it.  The device traversal stages the whole BVH (nodes, triangles, indices) in
+   LDS per workgroup, one ray per lane. */
+#define VPX_BVH_MAX_TRIS 512
+typedef struct vpx_bvh_tri {       /* Tri (BasicBVH.h:3-7) without the centroid */
+    float v0[3], v1[3], v2[3];
+} vpx_bvh_tri;                     /* 36 bytes */
+typedef struct vpx_bvh_node {      /* BVHNode (BasicBVH.h:11-20) */
+    float aabb_min[3], aabb_max[3];
+    uint32_t left_first, tri_count;
+} vpx_bvh_node;                    /* 32 bytes */
+/* Build (vpx_bvh_build_host) and upload the BVH of n triangles (1..VPX_BVH_MAX_TRIS;
+   n = 0 removes it). */
+int vpx_bvh_set(vpx_ctx* ctx, const vpx_bvh_tri* tris, uint32_t n);
+/* IntersectBVH(ray, 0) per ray: rays built as in vpx_find_nearest (Ray(O, D) normalises D,
+   t = tmax); t_out[i] = ray.t afterwards (tmax when nothing closer is hit). */
+int vpx_bvh_intersect(vpx_ctx* ctx, const vpx_ray* rays, uint32_t n, float* t_out);
+
 /* ---- host-side helpers restating reference host code (no device work) -------------- */
 /* Camera basis exactly as Camera::HandleInput(0) leaves it (camera.h:121-178). */
 int vpx_camera_look_at(const float pos[3], const float target[3], uint32_t width,
@@ -347,6 +372,15 @@ int vpx_default_materials(vpx_material* out256);
    k = seed_base + frame_index*W*H + y*W + x  (InitSeed, template/tmpl8math.cpp:35-38). */
 uint32_t vpx_pixel_seed(uint32_t seed_base, uint32_t frame_index, uint32_t width,
                         uint32_t height, uint32_t x, uint32_t y);
+/* BasicBVH::BuildBVH (BasicBVH.cpp:72-136): nodes needs 2n-1 entries, tri_idx n; the
+   number of nodes used is stored in *nodes_used. */
+int vpx_bvh_build_host(const vpx_bvh_tri* tris, uint32_t n, vpx_bvh_node* nodes, uint32_t* tri_idx,
+                       uint32_t* nodes_used);
+/* BasicBVH::BasicBVH() triangle set (BasicBVH.cpp:4-16): 64 triangles, vertex0 = r0*9-5,
+   vertex1 = vertex0+r1, vertex2 = vertex0+r2, each r a float3 of RandomFloat() from the
+   xorshift32 state *seed (advanced; the three draws of a float3 taken left to right —
+   C++ leaves that order unspecified). */
+int vpx_bvh_random_tris(uint32_t* seed, vpx_bvh_tri out[64]);
 
 #ifdef __cplusplus
 }

@@ -62,7 +62,41 @@ def _lib(abi):
     lib.oracle_offset_ray.restype = None
     lib.oracle_cube_intersect.argtypes = [P(C.c_float)] * 5
     lib.oracle_cube_intersect.restype = C.c_float
+    lib.oracle_bvh_random_tris.argtypes = [C.c_uint32, P(abi.BvhTri)]
+    lib.oracle_bvh_random_tris.restype = C.c_uint32
+    lib.oracle_bvh_build.argtypes = [P(abi.BvhTri), C.c_uint32, P(abi.BvhNode), P(C.c_uint32)]
+    lib.oracle_bvh_build.restype = C.c_uint32
+    lib.oracle_bvh_intersect.argtypes = [P(abi.BvhNode), P(abi.BvhTri), P(C.c_uint32), P(abi.Ray), C.c_uint32,
+                                         P(C.c_float)]
+    lib.oracle_bvh_intersect.restype = C.c_int
     return lib
+
+
+class BasicBVH:
+    """src/BVH/BasicBVH.{h,cpp} restated (oracle_bvh_*): build once, intersect rays."""
+
+    def __init__(self, abi, tris):
+        self.lib = _lib(abi)
+        self.abi = abi
+        n = len(tris)
+        self.tris = tris
+        self.nodes = (abi.BvhNode * max(1, 2 * n - 1))()
+        self.idx = (C.c_uint32 * max(1, n))()
+        self.used = self.lib.oracle_bvh_build(tris, n, self.nodes, self.idx)
+
+    @staticmethod
+    def random_tris(abi, seed=0x12345678):
+        """BasicBVH::BasicBVH()'s 64 triangles from xorshift32 state `seed`; (tris, state after)."""
+        tris = (abi.BvhTri * 64)()
+        after = _lib(abi).oracle_bvh_random_tris(seed, tris)
+        return tris, after
+
+    def intersect(self, rays):
+        out = np.zeros(len(rays), np.float32)
+        rc = self.lib.oracle_bvh_intersect(self.nodes, self.tris, self.idx, rays, len(rays),
+                                           out.ctypes.data_as(C.POINTER(C.c_float)))
+        assert rc == 0
+        return out
 
 
 class OracleGrid(C.Structure):

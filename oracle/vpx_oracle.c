@@ -1590,3 +1590,171 @@ uint64_t oracle_grid_checksum(const uint8_t* cells, uint64_t count)
     for (uint64_t i = 0; i < count; i++) s += (uint64_t)(cells[i] + 1u) * splitmix64(i);
     return s;
 }
+
+/* ------------------------------------------------------------------ BasicBVH -- */
+/* src/BVH/BasicBVH.{h,cpp}: the reference's triangle BVH (jacco.ompf2.com tutorial, part
+   1).  A Renderer member (renderer.h:220) that Trace never calls;
+   restated for the vpx_bvh_* entry points. */
+
+/* BasicBVH::BasicBVH() (BasicBVH.cpp:4-16): 64 triangles from RandomFloat.  The three
+   RandomFloat() arguments of each float3 constructor are drawn left to right (C++ leaves
+   the order unspecified — the same hazard as Update's RNG). */
+uint32_t oracle_bvh_random_tris(uint32_t seed, vpx_bvh_tri* out)
+{
+    for (int i = 0; i < 64; ++i) {
+        float r[9];
+        for (int k = 0; k < 9; ++k) r[k] = oracle_random_float(&seed);
+        const v3 r0 = V3(r[0], r[1], r[2]), r1 = V3(r[3], r[4], r[5]), r2 = V3(r[6], r[7], r[8]);
+        const v3 a = vsub(vmuls(r0, 9.0f), V3(5.0f, 5.0f, 5.0f)); /* r0 * 9 - float3(5) */
+        const v3 b = vadd(a, r1), c = vadd(a, r2);
+        out[i].v0[0] = a.x, out[i].v0[1] = a.y, out[i].v0[2] = a.z;
+        out[i].v1[0] = b.x, out[i].v1[1] = b.y, out[i].v1[2] = b.z;
+        out[i].v2[0] = c.x, out[i].v2[1] = c.y, out[i].v2[2] = c.z;
+    }
+    return seed;
+}
+
+typedef struct {
+    const vpx_bvh_tri* tri;
+    v3* centroid;
+    uint32_t* idx;
+    vpx_bvh_node* node;
+    uint32_t used;
+} bvh_build_t;
+
+static inline float fminf_t(float a, float b) { return a < b ? a : b; } /* tmpl8math.h:401-404 */
+static inline float fmaxf_t(float a, float b) { return a > b ? a : b; } /* :406-409 */
+
+/* BasicBVH::UpdateNodeBounds, BasicBVH.cpp:87-103 */
+static void bvh_update_bounds(bvh_build_t* b, uint32_t ni)
+{
+    vpx_bvh_node* nd = &b->node[ni];
+    float mn[3] = {1e30f, 1e30f, 1e30f}, mx[3] = {-1e30f, -1e30f, -1e30f};
+    for (uint32_t i = 0; i < nd->tri_count; ++i) {
+        const vpx_bvh_tri* t = &b->tri[b->idx[nd->left_first + i]];
+        for (int k = 0; k < 3; ++k) {
+            mn[k] = fminf_t(mn[k], t->v0[k]), mn[k] = fminf_t(mn[k], t->v1[k]), mn[k] = fminf_t(mn[k], t->v2[k]);
+            mx[k] = fmaxf_t(mx[k], t->v0[k]), mx[k] = fmaxf_t(mx[k], t->v1[k]), mx[k] = fmaxf_t(mx[k], t->v2[k]);
+        }
+    }
+    for (int k = 0; k < 3; ++k) nd->aabb_min[k] = mn[k], nd->aabb_max[k] = mx[k];
+}
+
+/* BasicBVH::Subdivide, BasicBVH.cpp:105-136 */
+static void bvh_subdivide(bvh_build_t* b, uint32_t ni)
+{
+    vpx_bvh_node* nd = &b->node[ni];
+    if (nd->tri_count <= 2) return;
+    const float ext[3] = {nd->aabb_max[0] - nd->aabb_min[0], nd->aabb_max[1] - nd->aabb_min[1],
+                          nd->aabb_max[2] - nd->aabb_min[2]};
+    int axis = 0;
+    if (ext[1] > ext[0]) axis = 1;
+    if (ext[2] > ext[axis]) axis = 2;
+    const float split = nd->aabb_min[axis] + ext[axis] * 0.5f;
+    int i = (int)nd->left_first;
+    int j = i + (int)nd->tri_count - 1;
+    while (i <= j) {
+        const v3 c = b->centroid[b->idx[i]];
+        const float ca = axis == 0 ? c.x : (axis == 1 ? c.y : c.z);
+        if (ca < split) {
+            i++;
+        } else {
+            const uint32_t tmp = b->idx[i];
+            b->idx[i] = b->idx[j];
+            b->idx[j--] = tmp;
+        }
+    }
+    const int left = i - (int)nd->left_first;
+    if (left == 0 || (uint32_t)left == nd->tri_count) return;
+    const uint32_t li = b->used++, ri = b->used++;
+    b->node[li].left_first = nd->left_first;
+    b->node[li].tri_count = (uint32_t)left;
+    b->node[ri].left_first = (uint32_t)i;
+    b->node[ri].tri_count = nd->tri_count - (uint32_t)left;
+    nd->left_first = li;
+    nd->tri_count = 0;
+    bvh_update_bounds(b, li);
+    bvh_update_bounds(b, ri);
+    bvh_subdivide(b, li);
+    bvh_subdivide(b, ri);
+}
+
+/* BasicBVH::BuildBVH, BasicBVH.cpp:72-85 (centroid = (v0 + v1 + v2) * 0.3333f). */
+uint32_t oracle_bvh_build(const vpx_bvh_tri* tris, uint32_t n, vpx_bvh_node* nodes, uint32_t* tri_idx)
+{
+    if (!n) return 0;
+    bvh_build_t b;
+    b.tri = tris;
+    b.idx = tri_idx;
+    b.node = nodes;
+    b.used = 1;
+    b.centroid = (v3*)malloc(sizeof(v3) * n);
+    for (uint32_t i = 0; i < n; ++i) tri_idx[i] = i;
+    for (uint32_t i = 0; i < n; ++i)
+        b.centroid[i] = vmuls(vadd(vadd(v3f(tris[i].v0), v3f(tris[i].v1)), v3f(tris[i].v2)), 0.3333f);
+    memset(nodes, 0, sizeof(vpx_bvh_node) * (2 * (size_t)n - 1));
+    nodes[0].left_first = 0, nodes[0].tri_count = n;
+    bvh_update_bounds(&b, 0);
+    bvh_subdivide(&b, 0);
+    free(b.centroid);
+    return b.used;
+}
+
+/* BasicBVH::IntersectTri, BasicBVH.cpp:19-36 */
+static void bvh_tri(ray_t* r, const vpx_bvh_tri* t)
+{
+    const v3 v0 = v3f(t->v0);
+    const v3 e1 = vsub(v3f(t->v1), v0), e2 = vsub(v3f(t->v2), v0);
+    const v3 h = vcross(r->D, e2);
+    const float a = vdot(e1, h);
+    if (a > -0.0001f && a < 0.0001f) return;
+    const float f = 1 / a;
+    const v3 s = vsub(r->O, v0);
+    const float u = f * vdot(s, h);
+    if (u < 0 || u > 1) return;
+    const v3 q = vcross(s, e1);
+    const float v = f * vdot(r->D, q);
+    if (v < 0 || u + v > 1) return;
+    const float tt = f * vdot(e2, q);
+    if (tt > 0.0001f) r->t = smin(r->t, tt);
+}
+
+/* BasicBVH::IntersectAABB, BasicBVH.cpp:38-48 */
+static int bvh_aabb(const ray_t* r, const float* bmin, const float* bmax)
+{
+    const float tx1 = (bmin[0] - r->O.x) / r->D.x, tx2 = (bmax[0] - r->O.x) / r->D.x;
+    float tmin = smin(tx1, tx2), tmax = smax(tx1, tx2);
+    const float ty1 = (bmin[1] - r->O.y) / r->D.y, ty2 = (bmax[1] - r->O.y) / r->D.y;
+    tmin = smax(tmin, smin(ty1, ty2)), tmax = smin(tmax, smax(ty1, ty2));
+    const float tz1 = (bmin[2] - r->O.z) / r->D.z, tz2 = (bmax[2] - r->O.z) / r->D.z;
+    tmin = smax(tmin, smin(tz1, tz2)), tmax = smin(tmax, smax(tz1, tz2));
+    return tmax >= tmin && tmin < r->t && tmax > 0;
+}
+
+/* BasicBVH::IntersectBVH, BasicBVH.cpp:50-70 (recursive: left subtree, then right). */
+static void bvh_node_visit(ray_t* r, const vpx_bvh_node* nodes, const vpx_bvh_tri* tris, const uint32_t* idx,
+                           uint32_t ni)
+{
+    const vpx_bvh_node* nd = &nodes[ni];
+    if (!bvh_aabb(r, nd->aabb_min, nd->aabb_max)) return;
+    if (nd->tri_count > 0) {
+        for (uint32_t i = 0; i < nd->tri_count; ++i) bvh_tri(r, &tris[idx[nd->left_first + i]]);
+    } else {
+        bvh_node_visit(r, nodes, tris, idx, nd->left_first);
+        bvh_node_visit(r, nodes, tris, idx, nd->left_first + 1);
+    }
+}
+
+int oracle_bvh_intersect(const vpx_bvh_node* nodes, const vpx_bvh_tri* tris, const uint32_t* tri_idx,
+                         const vpx_ray* rays, uint32_t n, float* t_out)
+{
+    if ((!rays || !t_out) && n) return VPX_E_INVALID;
+    const fpstate fs = fp_enter();
+    for (uint32_t i = 0; i < n; ++i) {
+        ray_t r = ray_from_api(&rays[i]);
+        if (nodes) bvh_node_visit(&r, nodes, tris, tri_idx, 0);
+        t_out[i] = r.t;
+    }
+    fp_leave(fs);
+    return VPX_OK;
+}

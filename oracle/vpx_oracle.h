@@ -114,6 +114,15 @@ void oracle_load_model_partial(const uint8_t* vox, uint32_t sx, uint32_t sy, uin
                                const float scale_model[3], uint32_t columns, uint32_t thickness, uint8_t* out);
 void oracle_emissive_sphere(uint8_t* grid, uint32_t n, uint8_t mat, float radius);
 
+/* BasicBVH (src/BVH/BasicBVH.{h,cpp}): the constructor's random triangle
+   set (returns the RNG state after), BuildBVH (returns nodes used; nodes: 2n-1 entries,
+   tri_idx: n) and IntersectBVH(ray, 0) per ray (t_out = ray.t afterwards; rays built as
+   oracle_find_nearest builds them).  nodes == NULL: no BVH, t_out = tmax. */
+uint32_t oracle_bvh_random_tris(uint32_t seed, vpx_bvh_tri* out);
+uint32_t oracle_bvh_build(const vpx_bvh_tri* tris, uint32_t n, vpx_bvh_node* nodes, uint32_t* tri_idx);
+int oracle_bvh_intersect(const vpx_bvh_node* nodes, const vpx_bvh_tri* tris, const uint32_t* tri_idx,
+                         const vpx_ray* rays, uint32_t n, float* t_out);
+
 #ifdef __cplusplus
 }
 #endif

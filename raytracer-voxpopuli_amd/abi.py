@@ -95,10 +95,22 @@ class Profile(C.Structure):
     _fields_ = [("stage_ms", C.c_float * 8), ("stage_launches", C.c_uint32 * 8), ("stage_cells", C.c_uint64 * 8)]
 
 
+class BvhTri(C.Structure):  # vpx_bvh_tri: BasicBVH Tri (BasicBVH.h:3-7) without the centroid
+    _fields_ = [("v0", C.c_float * 3), ("v1", C.c_float * 3), ("v2", C.c_float * 3)]
+
+
+class BvhNode(C.Structure):  # vpx_bvh_node: BVHNode (BasicBVH.h:11-20)
+    _fields_ = [("aabb_min", C.c_float * 3), ("aabb_max", C.c_float * 3), ("left_first", C.c_uint32),
+                ("tri_count", C.c_uint32)]
+
+
+BVH_MAX_TRIS = 512
+
 STAGES = ("primary", "shade", "shadow", "resolve", "bounce", "finish")
 
 STRUCT_SIZES = {PrevCamera: 64, Profile: 128, Volume: 160, Material: 32, PointLight: 24, SpotLight: 40, AreaLight: 32, DirLight: 24,
-                Sphere: 32, Triangle: 64, Camera: 80, FrameParams: 48, Ray: 32, Hit: 32, Stats: 40}
+                Sphere: 32, Triangle: 64, Camera: 80, FrameParams: 48, Ray: 32, Hit: 32, Stats: 40,
+                BvhTri: 36, BvhNode: 32}
 
 
 def np_dtype(struct):
@@ -163,6 +175,11 @@ SIGNATURES = {
     "vpx_volume_set_transform": (C.c_int, [C.POINTER(C.c_float)] * 3 + [C.POINTER(Volume)]),
     "vpx_default_materials": (C.c_int, [C.POINTER(Material)]),
     "vpx_pixel_seed": (C.c_uint32, [C.c_uint32] * 6),
+    "vpx_bvh_set": (C.c_int, [C.c_void_p, C.POINTER(BvhTri), C.c_uint32]),
+    "vpx_bvh_intersect": (C.c_int, [C.c_void_p, C.POINTER(Ray), C.c_uint32, C.POINTER(C.c_float)]),
+    "vpx_bvh_build_host": (C.c_int, [C.POINTER(BvhTri), C.c_uint32, C.POINTER(BvhNode), C.POINTER(C.c_uint32),
+                                     C.POINTER(C.c_uint32)]),
+    "vpx_bvh_random_tris": (C.c_int, [C.POINTER(C.c_uint32), C.POINTER(BvhTri)]),
 }
 
 _LIB = None

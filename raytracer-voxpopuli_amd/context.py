@@ -148,6 +148,17 @@ class Context:
     def profile_enable(self, max_launches):
         self._chk(self.lib.vpx_profile_enable(self.h, int(max_launches)), "vpx_profile_enable")
 
+    def bvh_set(self, tris):
+        """BasicBVH of `tris` (ctypes array of abi.BvhTri) built and uploaded (vpx_bvh_set)."""
+        self._chk(self.lib.vpx_bvh_set(self.h, tris, len(tris)), "vpx_bvh_set")
+
+    def bvh_intersect(self, rays):
+        """BasicBVH::IntersectBVH per ray: float32 t after the traversal."""
+        out = np.zeros(len(rays), np.float32)
+        self._chk(self.lib.vpx_bvh_intersect(self.h, rays, len(rays), out.ctypes.data_as(C.POINTER(C.c_float))),
+                  "vpx_bvh_intersect")
+        return out
+
     def profile_select(self, stages=None):
         """Time only these stage names (abi.STAGES); None: all."""
         mask = 0xFFFFFFFF if stages is None else sum(1 << abi.STAGES.index(s) for s in stages)

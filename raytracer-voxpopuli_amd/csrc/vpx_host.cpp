@@ -7,6 +7,8 @@
 // sinf/cosf are the correctly rounded values (f64 evaluation), as on the device.
 #include <cmath>
 #include <cstring>
+#include <utility>
+#include <vector>
 
 #include "../../include/vpx.h"
 
@@ -253,3 +255,110 @@ static_assert(sizeof(vpx_area_light) == 32 && sizeof(vpx_dir_light) == 24, "ligh
 static_assert(sizeof(vpx_sphere) == 32 && sizeof(vpx_triangle) == 64, "shape layout");
 static_assert(sizeof(vpx_camera) == 80 && sizeof(vpx_frame_params) == 48, "camera/frame layout");
 static_assert(sizeof(vpx_ray) == 32 && sizeof(vpx_hit) == 32 && sizeof(vpx_stats) == 40, "ray/hit/stats layout");
+static_assert(sizeof(vpx_bvh_tri) == 36 && sizeof(vpx_bvh_node) == 32, "bvh layout");
+
+// ---------------------------------------------------------------------- BasicBVH
+// src/BVH/BasicBVH.cpp, host side: the constructor's triangle set and BuildBVH.  The
+// device traversal is vpx_bvh_intersect (vpx_kernels.hip).
+namespace {
+
+struct BvhBuilder {
+    const vpx_bvh_tri* tri;
+    vpx_bvh_node* node;
+    uint32_t* idx;
+    std::vector<v3> centroid;
+    uint32_t used = 1;
+
+    static float lo(float a, float b) { return a < b ? a : b; }  // fminf, tmpl8math.h:401-404
+    static float hi(float a, float b) { return a > b ? a : b; }  // fmaxf, tmpl8math.h:406-409
+
+    // UpdateNodeBounds (BasicBVH.cpp:87-103): vertex0, vertex1, vertex2 folded in that order
+    void bounds(uint32_t ni) {
+        vpx_bvh_node& nd = node[ni];
+        float mn[3] = {1e30f, 1e30f, 1e30f}, mx[3] = {-1e30f, -1e30f, -1e30f};
+        for (uint32_t i = 0; i < nd.tri_count; ++i) {
+            const vpx_bvh_tri& t = tri[idx[nd.left_first + i]];
+            for (const float* v : {t.v0, t.v1, t.v2})
+                for (int k = 0; k < 3; ++k) mn[k] = lo(mn[k], v[k]), mx[k] = hi(mx[k], v[k]);
+        }
+        std::memcpy(nd.aabb_min, mn, sizeof mn);
+        std::memcpy(nd.aabb_max, mx, sizeof mx);
+    }
+
+    // Subdivide (BasicBVH.cpp:105-136): midpoint of the longest axis, in-place partition
+    void split(uint32_t ni) {
+        vpx_bvh_node& nd = node[ni];
+        if (nd.tri_count <= 2) return;
+        const float ext[3] = {nd.aabb_max[0] - nd.aabb_min[0], nd.aabb_max[1] - nd.aabb_min[1],
+                              nd.aabb_max[2] - nd.aabb_min[2]};
+        int axis = ext[1] > ext[0] ? 1 : 0;
+        if (ext[2] > ext[axis]) axis = 2;
+        const float pos = nd.aabb_min[axis] + ext[axis] * 0.5f;
+        int i = (int)nd.left_first, j = i + (int)nd.tri_count - 1;
+        while (i <= j) {
+            const v3& c = centroid[idx[i]];
+            if ((axis == 0 ? c.x : axis == 1 ? c.y : c.z) < pos)
+                ++i;
+            else
+                std::swap(idx[i], idx[j--]);
+        }
+        const uint32_t left = (uint32_t)(i - (int)nd.left_first);
+        if (left == 0 || left == nd.tri_count) return;
+        const uint32_t l = used++, r = used++;
+        node[l].left_first = nd.left_first, node[l].tri_count = left;
+        node[r].left_first = (uint32_t)i, node[r].tri_count = nd.tri_count - left;
+        nd.left_first = l, nd.tri_count = 0;
+        bounds(l);
+        bounds(r);
+        split(l);
+        split(r);
+    }
+};
+
+float bvh_random_float(uint32_t& s) {  // RandomFloat (tmpl8math.cpp:119-133)
+    s ^= s << 13;
+    s ^= s >> 17;
+    s ^= s << 5;
+    return (float)s * 2.3283064365387e-10f;
+}
+
+}  // namespace
+
+extern "C" {
+
+int vpx_bvh_build_host(const vpx_bvh_tri* tris, uint32_t n, vpx_bvh_node* nodes, uint32_t* tri_idx,
+                       uint32_t* nodes_used) {
+    if ((n && (!tris || !nodes || !tri_idx)) || !nodes_used) return VPX_E_INVALID;
+    *nodes_used = 0;
+    if (!n) return VPX_OK;
+    BvhBuilder b;
+    b.tri = tris, b.node = nodes, b.idx = tri_idx;
+    b.centroid.resize(n);
+    for (uint32_t i = 0; i < n; ++i) {  // BuildBVH (BasicBVH.cpp:72-85)
+        tri_idx[i] = i;
+        const v3 v0{tris[i].v0[0], tris[i].v0[1], tris[i].v0[2]}, v1{tris[i].v1[0], tris[i].v1[1], tris[i].v1[2]},
+            v2{tris[i].v2[0], tris[i].v2[1], tris[i].v2[2]};
+        b.centroid[i] = mul(add(add(v0, v1), v2), 0.3333f);
+    }
+    std::memset(nodes, 0, sizeof(vpx_bvh_node) * (2 * (size_t)n - 1));
+    nodes[0].left_first = 0, nodes[0].tri_count = n;
+    b.bounds(0);
+    b.split(0);
+    *nodes_used = b.used;
+    return VPX_OK;
+}
+
+int vpx_bvh_random_tris(uint32_t* seed, vpx_bvh_tri out[64]) {
+    if (!seed || !out) return VPX_E_INVALID;
+    for (int i = 0; i < 64; ++i) {  // BasicBVH::BasicBVH (BasicBVH.cpp:4-16)
+        float r[9];
+        for (float& x : r) x = bvh_random_float(*seed);
+        const v3 a = sub(mul(v3{r[0], r[1], r[2]}, 9.0f), v3{5.0f, 5.0f, 5.0f});
+        put(out[i].v0, a);
+        put(out[i].v1, add(a, v3{r[3], r[4], r[5]}));
+        put(out[i].v2, add(a, v3{r[6], r[7], r[8]}));
+    }
+    return VPX_OK;
+}
+
+}  // extern "C"

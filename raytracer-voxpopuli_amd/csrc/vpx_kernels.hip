@@ -86,6 +86,63 @@ __global__ void is_occluded_k(SceneView sv, const vpx_ray* rays, uint32_t n, uin
     occ[i] = is_occluded(sv, r, k) ? 1 : 0;
 }
 
+// BasicBVH::IntersectBVH (src/BVH/BasicBVH.cpp:19-70), one ray per lane.  The workgroup
+// stages the whole BVH in LDS (nodes, then the triangles already permuted into tri_idx
+// order, so a leaf's triangles are contiguous); the recursion (node test, then left
+// subtree, then right) becomes an explicit stack that pops the left child first.  Float
+// expressions keep the reference's operand order: IEEE divisions, std::min / std::max.
+constexpr int kBvhStack = 64;
+__global__ __launch_bounds__(256) void bvh_intersect_k(const uint32_t* __restrict__ bvh, uint32_t n_nodes,
+                                                       uint32_t n_tris, const vpx_ray* rays, uint32_t n,
+                                                       float* t_out) {
+    extern __shared__ uint32_t lds_bvh[];
+    const uint32_t words = n_nodes * 8u + n_tris * 9u;
+    for (uint32_t i = threadIdx.x; i < words; i += blockDim.x) lds_bvh[i] = bvh[i];
+    __syncthreads();
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const vpx_bvh_node* nodes = (const vpx_bvh_node*)lds_bvh;
+    const vpx_bvh_tri* tris = (const vpx_bvh_tri*)(lds_bvh + n_nodes * 8u);
+    Ray r = ray_from(rays[i]);
+    uint32_t stack[kBvhStack];
+    int sp = 0;
+    stack[sp++] = 0;
+    while (sp > 0) {
+        const vpx_bvh_node& nd = nodes[stack[--sp]];
+        // IntersectAABB (BasicBVH.cpp:38-48)
+        const float tx1 = (nd.aabb_min[0] - r.O.x) / r.D.x, tx2 = (nd.aabb_max[0] - r.O.x) / r.D.x;
+        float tmin = smin(tx1, tx2), tmax = smax(tx1, tx2);
+        const float ty1 = (nd.aabb_min[1] - r.O.y) / r.D.y, ty2 = (nd.aabb_max[1] - r.O.y) / r.D.y;
+        tmin = smax(tmin, smin(ty1, ty2)), tmax = smin(tmax, smax(ty1, ty2));
+        const float tz1 = (nd.aabb_min[2] - r.O.z) / r.D.z, tz2 = (nd.aabb_max[2] - r.O.z) / r.D.z;
+        tmin = smax(tmin, smin(tz1, tz2)), tmax = smin(tmax, smax(tz1, tz2));
+        if (!(tmax >= tmin && tmin < r.t && tmax > 0)) continue;
+        if (nd.tri_count == 0) {  // interior: left subtree first
+            stack[sp++] = nd.left_first + 1u;
+            stack[sp++] = nd.left_first;
+            continue;
+        }
+        for (uint32_t k = 0; k < nd.tri_count; ++k) {  // IntersectTri (BasicBVH.cpp:19-36)
+            const vpx_bvh_tri& t = tris[nd.left_first + k];
+            const f3 v0 = ld3(t.v0);
+            const f3 e1 = ld3(t.v1) - v0, e2 = ld3(t.v2) - v0;
+            const f3 h = cross(r.D, e2);
+            const float a = dot(e1, h);
+            if (a > -0.0001f && a < 0.0001f) continue;
+            const float f = __fdiv_rn(1.0f, a);
+            const f3 sv = r.O - v0;
+            const float u = f * dot(sv, h);
+            if (u < 0 || u > 1) continue;
+            const f3 q = cross(sv, e1);
+            const float v = f * dot(r.D, q);
+            if (v < 0 || u + v > 1) continue;
+            const float tt = f * dot(e2, q);
+            if (tt > 0.0001f) r.t = smin(r.t, tt);
+        }
+    }
+    t_out[i] = r.t;
+}
+
 template <int LEVELS>
 __global__ void trace_k(SceneView sv, const vpx_ray* rays, const uint32_t* seeds, uint32_t n, int32_t depth,
                         float* out) {
@@ -328,6 +385,8 @@ struct vpx_ctx {
     std::vector<vpx_volume> volumes;
     vpx_volume* d_volumes = nullptr;
     float4* d_vbounds = nullptr;  // per volume: world bounding sphere (centre, radius^2), see volume_bounds
+    void* d_bvh = nullptr;        // BasicBVH: nodes, then the triangles in tri_idx order (vpx_bvh_set)
+    uint32_t bvh_nodes = 0, bvh_tris = 0;
     uint32_t d_volumes_cap = 0;
     vpx_material* d_materials = nullptr;
     vpx_point_light* d_points = nullptr;
@@ -658,7 +717,7 @@ int vpx_destroy(vpx_ctx* c) {
         if (g.l1) (void)hipFree(g.l1);
         if (g.l2) (void)hipFree(g.l2);
     }
-    void* ptrs[] = {c->d_grids, c->d_volumes, c->d_vbounds, c->d_materials, c->d_points, c->d_spots, c->d_areas,
+    void* ptrs[] = {c->d_grids, c->d_volumes, c->d_vbounds, c->d_bvh, c->d_materials, c->d_points, c->d_spots, c->d_areas,
                     c->d_spheres, c->d_triangles, c->d_ctr, c->d_sum, c->d_scratch, c->d_wave, c->d_sky};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
@@ -1214,6 +1273,56 @@ int vpx_trace(vpx_ctx* c, const vpx_ray* rays, const uint32_t* seeds, uint32_t n
         hipLaunchKernelGGL(trace_k<kMaxLevels>, g, b, 0, c->stream, sv, dr, ds, n, depth, dout);
     VPX_HIP(c, hipGetLastError());
     VPX_HIP(c, hipMemcpyAsync(radiance, dout, ob, hipMemcpyDeviceToHost, c->stream));
+    VPX_HIP(c, hipStreamSynchronize(c->stream));
+    return VPX_OK;
+}
+
+// Depth of a built BasicBVH (root = 1); the traversal stack needs one entry per level.
+static uint32_t bvh_depth(const vpx_bvh_node* nodes, uint32_t ni) {
+    if (nodes[ni].tri_count) return 1;
+    const uint32_t l = bvh_depth(nodes, nodes[ni].left_first), r = bvh_depth(nodes, nodes[ni].left_first + 1);
+    return 1 + (l > r ? l : r);
+}
+
+int vpx_bvh_set(vpx_ctx* c, const vpx_bvh_tri* tris, uint32_t n) {
+    if (!c || (n && !tris)) return fail(c, VPX_E_INVALID, "null argument");
+    if (n > VPX_BVH_MAX_TRIS) return fail(c, VPX_E_INVALID, "more triangles than VPX_BVH_MAX_TRIS");
+    VPX_HIP(c, hipStreamSynchronize(c->stream));
+    if (c->d_bvh) (void)hipFree(c->d_bvh);
+    c->d_bvh = nullptr;
+    c->bvh_nodes = c->bvh_tris = 0;
+    if (!n) return VPX_OK;
+    std::vector<vpx_bvh_node> nodes(2 * (size_t)n - 1);
+    std::vector<uint32_t> idx(n);
+    uint32_t used = 0;
+    int rc = vpx_bvh_build_host(tris, n, nodes.data(), idx.data(), &used);
+    if (rc) return fail(c, rc, "vpx_bvh_build_host failed");
+    // the traversal pushes both children of every interior node it enters
+    if (bvh_depth(nodes.data(), 0) + 1 > (uint32_t)kBvhStack) return fail(c, VPX_E_INVALID, "BVH deeper than the traversal stack");
+    std::vector<uint32_t> img(used * 8u + n * 9u);
+    std::memcpy(img.data(), nodes.data(), sizeof(vpx_bvh_node) * used);
+    for (uint32_t k = 0; k < n; ++k) std::memcpy(&img[used * 8u + k * 9u], &tris[idx[k]], sizeof(vpx_bvh_tri));
+    VPX_HIP(c, hipMalloc(&c->d_bvh, sizeof(uint32_t) * img.size()));
+    VPX_HIP(c, hipMemcpy(c->d_bvh, img.data(), sizeof(uint32_t) * img.size(), hipMemcpyHostToDevice));
+    c->bvh_nodes = used, c->bvh_tris = n;
+    return VPX_OK;
+}
+
+int vpx_bvh_intersect(vpx_ctx* c, const vpx_ray* rays, uint32_t n, float* t_out) {
+    if (!c || (n && (!rays || !t_out))) return fail(c, VPX_E_INVALID, "null argument");
+    if (!c->d_bvh) return fail(c, VPX_E_STATE, "no BVH set (vpx_bvh_set)");
+    if (n == 0) return VPX_OK;
+    const size_t rb = sizeof(vpx_ray) * n, tb = sizeof(float) * n;
+    int rc = ensure_scratch(c, rb + tb);
+    if (rc) return rc;
+    vpx_ray* dr = (vpx_ray*)c->d_scratch;
+    float* dt = (float*)((char*)c->d_scratch + rb);
+    VPX_HIP(c, hipMemcpyAsync(dr, rays, rb, hipMemcpyHostToDevice, c->stream));
+    const size_t lds = sizeof(uint32_t) * (c->bvh_nodes * 8u + c->bvh_tris * 9u);  // <= 51 KiB (512 triangles)
+    hipLaunchKernelGGL(bvh_intersect_k, dim3((n + 255) / 256), dim3(256), lds, c->stream, (const uint32_t*)c->d_bvh,
+                       c->bvh_nodes, c->bvh_tris, dr, n, dt);
+    VPX_HIP(c, hipGetLastError());
+    VPX_HIP(c, hipMemcpyAsync(t_out, dt, tb, hipMemcpyDeviceToHost, c->stream));
     VPX_HIP(c, hipStreamSynchronize(c->stream));
     return VPX_OK;
 }

@@ -256,6 +256,37 @@ def test_volume_cull_grazing_rays(pkg, orc):
     ctx.close()
 
 
+@pytest.mark.parametrize("n", [64, 1, 7, 512])
+def test_bvh_intersect(pkg, orc, n):
+    """BasicBVH::IntersectBVH on the device (LDS-staged tree, explicit stack) equals the
+    oracle's recursive restatement bit for bit; n = 64 is the reference constructor's set."""
+    abi = pkg.abi
+    rng = np.random.default_rng(n)
+    if n == 64:
+        tris, _ = orc.BasicBVH.random_tris(abi)
+    else:
+        a = rng.uniform(-5, 4, (n, 3))
+        v = np.concatenate([a, a + rng.uniform(0, 1, (n, 3)), a + rng.uniform(0, 1, (n, 3))], 1).astype(np.float32)
+        tris = (abi.BvhTri * n)()
+        np.frombuffer(tris, np.float32).reshape(-1, 9)[:] = v
+    o = orc.BasicBVH(abi, tris)
+    cen = np.frombuffer(tris, np.float32).reshape(n, 3, 3).mean(1)
+    m = 8192
+    org = np.concatenate([rng.uniform(-8, 8, (m // 2, 3)), cen[rng.integers(0, n, m // 2)] + rng.normal(0, 0.3, (m // 2, 3))])
+    tgt = cen[rng.integers(0, n, m)] + rng.normal(0, 0.05, (m, 3))
+    tmax = np.where(rng.random(m) < 0.3, rng.uniform(0.1, 10, m), 1e34)
+    rays = pkg.context.make_rays(org.astype(np.float32), (tgt - org).astype(np.float32), tmax=tmax)
+    ctx = pkg.context.Context(0)
+    ctx.bvh_set(tris)
+    t_g = ctx.bvh_intersect(rays)
+    t_o = o.intersect(rays)
+    assert np.array_equal(bits(t_g), bits(t_o))
+    assert (t_o < 1e33).mean() > 0.1
+    with pytest.raises(pkg.abi.VpxError):
+        ctx.bvh_set((abi.BvhTri * (abi.BVH_MAX_TRIS + 1))())
+    ctx.close()
+
+
 def test_smoke_material_exits(pkg, orc):
     """Smoke and glass volumes exercise FindSmokeExit / FindMaterialExit."""
     sc = pkg.scene
