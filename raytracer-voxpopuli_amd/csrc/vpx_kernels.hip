@@ -626,10 +626,19 @@ int launch_render(vpx_ctx* c, const SceneView& sv, const FrameArgs& f, uint32_t 
     prof_mark(c, VPX_STAGE_PRIMARY);
     hipLaunchKernelGGL(one ? k_primary<true> : k_primary<false>, grid, block, 0, c->stream, sv, f, w, c->d_ctr);
     prof_mark(c, -1);
+    // the last level's shadow -> resolve -> finish as one launch (k_shadow_finish)
+    const bool fuse_tail = kFuseTail && !rp && kGroupTiles == 1;
     for (int level = 0; level <= f.max_bounces; ++level) {
         prof_mark(c, VPX_STAGE_SHADE);
         hipLaunchKernelGGL(k_shade, grid, block, 0, c->stream, sv, f, w, level, c->d_ctr);
         prof_mark(c, -1);
+        if (fuse_tail && level == f.max_bounces) {
+            prof_mark(c, VPX_STAGE_SHADOW);
+            hipLaunchKernelGGL((one ? k_shadow_finish<true, MODE> : k_shadow_finish<false, MODE>), grid, block, slds,
+                               c->stream, sv, f, w, c->d_ctr, accum, rgb8, packed);
+            prof_mark(c, -1);
+            break;
+        }
         prof_mark(c, VPX_STAGE_SHADOW);
         hipLaunchKernelGGL(one ? k_shadow_tile<true> : k_shadow_tile<false>, ggrid, block, slds, c->stream, sv, w, c->d_ctr);
         prof_mark(c, -1);
@@ -642,9 +651,12 @@ int launch_render(vpx_ctx* c, const SceneView& sv, const FrameArgs& f, uint32_t 
             prof_mark(c, -1);
         }
     }
-    prof_mark(c, VPX_STAGE_FINISH);
+    // (fused tail: k_shadow_finish already finished the frame; max_bounces = -1 runs no
+    // level, so the finish folds the zero leaf here)
+    const bool finished = fuse_tail && f.max_bounces >= 0;
+    if (!finished) prof_mark(c, VPX_STAGE_FINISH);
     if (!rp) {
-        hipLaunchKernelGGL((k_finish<MODE>), grid, block, 0, c->stream, f, w, accum, rgb8, packed);
+        if (!finished) hipLaunchKernelGGL((k_finish<MODE>), grid, block, 0, c->stream, f, w, accum, rgb8, packed);
     } else {  // Renderer::Tick static branch, second pass (renderer.cpp:2024-2100)
         hipLaunchKernelGGL(k_finish_reproject, grid, block, 0, c->stream, f, w, rp->alb, rp->ill);
         hipLaunchKernelGGL(k_reproject_setup, grid, block, 0, c->stream, f, w, rp->prev);
@@ -654,7 +666,7 @@ int launch_render(vpx_ctx* c, const SceneView& sv, const FrameArgs& f, uint32_t 
         VPX_HIP(c, hipMemcpyAsync(rp->hist, rp->temp, sizeof(float4) * (size_t)f.width * f.height,
                                   hipMemcpyDeviceToDevice, c->stream));  // history = temp
     }
-    prof_mark(c, -1);
+    if (!finished) prof_mark(c, -1);
     VPX_HIP(c, hipGetLastError());
     return VPX_OK;
 }

@@ -392,27 +392,30 @@ __global__ __launch_bounds__(256) void k_shade(SceneView sv, FrameArgs f, WaveBu
                     a = albedo(sv, m);
                     form = kFormAddMul;
                 }
+                // LB is read by k_finish only for the MulAdd / AddMul forms, and those
+                // levels always carry a pending light whose k_resolve writes LB: no zero fill
                 const uint64_t li = (uint64_t)nl * w.P + p;
                 w.LA[li] = make_float4(a.x, a.y, a.z, 0.f);
-                w.LB[li] = make_float4(0.f, 0.f, 0.f, 0.f);
                 forms = (forms & 0x07ffffffu) | (form << (2 * nl)) | ((nl + 1u) << 27);
                 if (pending) {
                     pending |= (nl << 8);
                     w.SM[p] = make_float4(kd.x, kd.y, kd.z, __uint_as_float(pending));
                 }
                 --depth;
-                if (depth < 0) done = true;  // the child Trace(depth < 0) returns 0
-                flags = (next.inside ? kInside : 0u) | (done ? 0u : kActive);
-                w.O[p] = make_float4(next.O.x, next.O.y, next.O.z, __uint_as_float(g.s));
-                w.D[p] = make_float4(next.D.x, next.D.y, next.D.z, __uint_as_float(flags));
-                w.depth[p] = depth;
+                if (depth >= 0) {
+                    flags = (next.inside ? kInside : 0u) | kActive;
+                    w.O[p] = make_float4(next.O.x, next.O.y, next.O.z, __uint_as_float(g.s));
+                    w.D[p] = make_float4(next.D.x, next.D.y, next.D.z, __uint_as_float(flags));
+                    w.depth[p] = depth;
+                }
+                // else: the child Trace(depth < 0) returns 0 (the leaf k_primary zeroed).
+                // Only the last level gets here (depth starts at max_bounces) and no kernel
+                // after it reads the path's ray, flags or depth, so they are not written.
                 w.forms[p] = forms;
             }
-            if (done) {
+            if (done) {  // sky / emissive leaf; the path stops
                 w.leaf[p] = make_float4(leaf.x, leaf.y, leaf.z, 0.f);
-                if (ray.mat == kNone || ray.mat == VPX_MAT_EMISSIVE) {
-                    w.D[p] = make_float4(od.x, od.y, od.z, __uint_as_float(0u));
-                }
+                w.D[p] = make_float4(od.x, od.y, od.z, __uint_as_float(0u));
             }
         }
         if (!pending) w.SM[p] = make_float4(0.f, 0.f, 0.f, __uint_as_float(0u));
@@ -423,8 +426,7 @@ __global__ __launch_bounds__(256) void k_shade(SceneView sv, FrameArgs f, WaveBu
 
 // Light sum of a level once its shadow rays are resolved (kSlotOcc set by k_shadow1):
 // the evaluators' accumulation (renderer.cpp:102-207) and Illumination's *lightCount.
-__global__ __launch_bounds__(256) void k_resolve(SceneView sv, WaveBufs w) {
-    const uint32_t p = blockIdx.x * 256u + threadIdx.x;
+__device__ __forceinline__ void resolve_path(const SceneView& sv, const WaveBufs& w, uint32_t p) {
     if (p >= w.P) return;
     const float4 sm = w.SM[p];
     const uint32_t pend = __float_as_uint(sm.w);
@@ -448,6 +450,10 @@ __global__ __launch_bounds__(256) void k_resolve(SceneView sv, WaveBufs w) {
     inc = inc * (float)lc;
     if (pend & kPendZeroAdd) inc = mk(0.f, 0.f, 0.f) + inc;
     w.LB[(uint64_t)lvl * w.P + p] = make_float4(inc.x, inc.y, inc.z, 0.f);
+}
+
+__global__ __launch_bounds__(256) void k_resolve(SceneView sv, WaveBufs w) {
+    resolve_path(sv, w, blockIdx.x * 256u + threadIdx.x);
 }
 
 // ------------------------------------------------------------ tile kernels
@@ -630,6 +636,13 @@ __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_NEAREST : VPX_WPE_MULTI_
 #endif
 constexpr uint32_t kGroupTiles = VPX_GROUP_TILES;
 
+// Run the last level's IsOccluded, light resolve and finish as one launch (k_shadow_finish;
+// needs one tile per workgroup).  -DVPX_FUSE_TAIL=0 restores the three launches.
+#ifndef VPX_FUSE_TAIL
+#define VPX_FUSE_TAIL 1
+#endif
+constexpr bool kFuseTail = VPX_FUSE_TAIL != 0;
+
 // Prefix scan over the G*256 paths of a workgroup (each thread scans G paths).
 template <uint32_t G>
 __device__ __forceinline__ uint32_t group_scan(const uint32_t (&cnt)[G], uint32_t& total, uint32_t* sh) {
@@ -677,7 +690,7 @@ __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_NEAREST : VPX_WPE_MULTI_
 // Renderer::IsOccluded for the shadow slots of G tiles (entry = slot << 27 | path); sets
 // the slot's occluded flag.  The light sums are formed in slot order by k_resolve.
 template <bool ONE>
-__global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_SHADOW : VPX_WPE_MULTI_SHADOW) void k_shadow_tile(SceneView sv, WaveBufs w, unsigned long long* __restrict__ ctr) {
+__device__ __forceinline__ void shadow_tile(const SceneView& sv, const WaveBufs& w, unsigned long long* __restrict__ ctr) {
     __shared__ uint32_t sh[4];
     extern __shared__ uint32_t lst_dyn[];  // [S * 256 * G]
     const uint32_t base = blockIdx.x * 256u * kGroupTiles;
@@ -733,6 +746,11 @@ __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_SHADOW : VPX_WPE_MULTI_S
     flush_counters(k, 0u, ctr, VPX_STAGE_SHADOW);
 }
 
+template <bool ONE>
+__global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_SHADOW : VPX_WPE_MULTI_SHADOW) void k_shadow_tile(SceneView sv, WaveBufs w, unsigned long long* __restrict__ ctr) {
+    shadow_tile<ONE>(sv, w, ctr);
+}
+
 // ------------------------------------------------------------------- stage 4
 // GetLuminance / ApplyReinhardJodie / RGBF32_to_RGB8 (renderer.cpp:2222-2240,
 // template/precomp.h:372-388).
@@ -763,9 +781,8 @@ enum FinishMode : int { kFinishImage = 0, kFinishPackedSample = 1, kFinishPacked
 
 // Fold the level records bottom-up (the recursion's rounding order), then write per MODE.
 template <int MODE>
-__global__ __launch_bounds__(256) void k_finish(FrameArgs f, WaveBufs w, float4* __restrict__ accum,
-                                                uint32_t* __restrict__ rgb8, float4* __restrict__ packed) {
-    const uint32_t p = blockIdx.x * 256u + threadIdx.x;
+__device__ __forceinline__ void finish_path(const FrameArgs& f, const WaveBufs& w, uint32_t p, float4* __restrict__ accum,
+                                            uint32_t* __restrict__ rgb8, float4* __restrict__ packed) {
     if (p >= w.P) return;
     uint32_t x, y;
     const bool valid = path_pixel(f, p, x, y);
@@ -811,6 +828,29 @@ __global__ __launch_bounds__(256) void k_finish(FrameArgs f, WaveBufs w, float4*
             if (rgb8) rgb8[px] = tonemap_pack(a);
         }
     }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) void k_finish(FrameArgs f, WaveBufs w, float4* __restrict__ accum,
+                                                uint32_t* __restrict__ rgb8, float4* __restrict__ packed) {
+    finish_path<MODE>(f, w, blockIdx.x * 256u + threadIdx.x, accum, rgb8, packed);
+}
+
+// The last level's tail in one launch: IsOccluded for the tile's shadow slots, then (after
+// the workgroup barrier, which makes the slots' occluded flags visible to the whole tile)
+// each thread resolves and finishes its own path.  The same per-path operations as
+// k_shadow_tile -> k_resolve -> k_finish, so the same values; the light/accumulate work of
+// a finished tile overlaps the walks of the others instead of running as two more
+// bandwidth-bound launches after the slowest walk.
+template <bool ONE, int MODE>
+__global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_SHADOW : VPX_WPE_MULTI_SHADOW) void k_shadow_finish(
+    SceneView sv, FrameArgs f, WaveBufs w, unsigned long long* __restrict__ ctr, float4* __restrict__ accum,
+    uint32_t* __restrict__ rgb8, float4* __restrict__ packed) {
+    shadow_tile<ONE>(sv, w, ctr);
+    __syncthreads();
+    const uint32_t p = blockIdx.x * 256u + threadIdx.x;
+    resolve_path(sv, w, p);
+    finish_path<MODE>(f, w, p, accum, rgb8, packed);
 }
 
 // ------------------------------------------------------ static-camera reprojection
