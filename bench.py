@@ -232,13 +232,22 @@ def run(args):
         dom_ms, dom_launches, dom_cells = prof[dom]
         split = warm if timed_stages else prof
         kernel_ms = dom_ms / max(dom_launches, 1)
+        # the library runs the last level's shadow -> resolve -> finish as one launch
+        # (k_shadow_finish) unless built with VPX_FUSE_TAIL=0: then there is
+        # no separate finish stage, and the shadow stage carries the 36 B per pixel
+        fused = "finish" not in split
+        kernels = dict(STAGE_KERNELS)
+        if fused:
+            kernels["shadow"] = "k_shadow_finish" if desc.max_bounces == 0 else "k_shadow_tile+k_shadow_finish"
         if dom == "finish":
             alg_bytes = float(st.primary_rays) / K * 36.0
         else:
             alg_bytes = float(dom_cells) / max(dom_launches, 1)
+            if dom == "shadow" and fused:
+                alg_bytes += float(st.primary_rays) * 36.0 / max(dom_launches, 1)
         achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
         frame_bytes = float(st.dda_cells) / K + float(st.primary_rays) / K * 36.0
-        traffic = pmc_traffic(STAGE_KERNELS[dom], args.config, W, H)
+        traffic = pmc_traffic(kernels[dom], args.config, W, H)
         out = {
             "metric": METRIC, "value": round(value, 3), "unit": "Mray/s", "n_gpus": n, "steps": K,
             "warmup": args.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True,
@@ -256,7 +265,7 @@ def run(args):
             "mpix_per_s": round(prim / elapsed / 1e6, 3),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                         "kernel": STAGE_KERNELS[dom], "kernel_ms": round(kernel_ms, 4),
+                         "kernel": kernels[dom], "kernel_ms": round(kernel_ms, 4),
                          "alg_bytes_per_launch": round(alg_bytes),
                          "stages_ms": {k: round(v[0] / max(v[1], 1), 4) for k, v in split.items() if v[1]},
                          "stages_ms_from": "last warmup frame, every stage timed" if timed_stages else "timed region",
