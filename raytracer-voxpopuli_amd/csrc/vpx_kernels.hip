@@ -624,14 +624,22 @@ int launch_render(vpx_ctx* c, const SceneView& sv, const FrameArgs& f, uint32_t 
     // single volume, no analytic shapes: the DDA kernels' lean instances
     const bool one = sv.num_volumes == 1 && !(sv.num_spheres | sv.num_triangles);
     prof_mark(c, VPX_STAGE_PRIMARY);
-    hipLaunchKernelGGL(one ? k_primary<true> : k_primary<false>, grid, block, 0, c->stream, sv, f, w, c->d_ctr);
+    const bool fuse_head = kFuseHead && f.max_bounces >= 0;
+    if (fuse_head)
+        hipLaunchKernelGGL((one ? k_primary<true, true> : k_primary<false, true>), grid, block, 0, c->stream, sv, f, w,
+                           c->d_ctr);
+    else
+        hipLaunchKernelGGL((one ? k_primary<true, false> : k_primary<false, false>), grid, block, 0, c->stream, sv, f,
+                           w, c->d_ctr);
     prof_mark(c, -1);
     // the last level's shadow -> resolve -> finish as one launch (k_shadow_finish)
     const bool fuse_tail = kFuseTail && !rp && kGroupTiles == 1;
     for (int level = 0; level <= f.max_bounces; ++level) {
-        prof_mark(c, VPX_STAGE_SHADE);
-        hipLaunchKernelGGL(k_shade, grid, block, 0, c->stream, sv, f, w, level, c->d_ctr);
-        prof_mark(c, -1);
+        if (!(fuse_head && level == 0)) {
+            prof_mark(c, VPX_STAGE_SHADE);
+            hipLaunchKernelGGL(k_shade, grid, block, 0, c->stream, sv, f, w, level, c->d_ctr);
+            prof_mark(c, -1);
+        }
         if (fuse_tail && level == f.max_bounces) {
             prof_mark(c, VPX_STAGE_SHADOW);
             hipLaunchKernelGGL((one ? k_shadow_finish<true, MODE> : k_shadow_finish<false, MODE>), grid, block, slds,

@@ -249,10 +249,8 @@ __device__ __forceinline__ uint32_t wave_prefix(uint32_t v, uint32_t& total) {
     return x - v;
 }
 
-__global__ __launch_bounds__(256) void k_shade(SceneView sv, FrameArgs f, WaveBufs w, int level,
-                                               unsigned long long* ctr) {
-    const uint32_t p = blockIdx.x * 256u + threadIdx.x;
-    Counters k{0u, 0u, 0u};
+__device__ __forceinline__ void shade_path(const SceneView& sv, const FrameArgs& f, const WaveBufs& w, uint32_t p,
+                                           int level, Counters& k) {
     uint32_t slots = 0;
     if (p < w.P) {
         float4 od = w.D[p];
@@ -421,6 +419,12 @@ __global__ __launch_bounds__(256) void k_shade(SceneView sv, FrameArgs f, WaveBu
         if (!pending) w.SM[p] = make_float4(0.f, 0.f, 0.f, __uint_as_float(0u));
     }
     if (p < w.P) w.smask[p] = slots;
+}
+
+__global__ __launch_bounds__(256) void k_shade(SceneView sv, FrameArgs f, WaveBufs w, int level,
+                                               unsigned long long* ctr) {
+    Counters k{0u, 0u, 0u};
+    shade_path(sv, f, w, blockIdx.x * 256u + threadIdx.x, level, k);
     flush_counters(k, 0u, ctr, VPX_STAGE_SHADE);
 }
 
@@ -557,7 +561,7 @@ __device__ __forceinline__ void nearest_record_1v(const SceneView& sv, const Wav
 // Primary rays + Renderer::FindNearest.  Every path's ray / RNG state is written; rays
 // that cannot hit a voxel or shape (one volume, no shapes, Setup3DDDA fails: the
 // reference returns before reading a cell) get their miss record directly.
-template <bool ONE>
+template <bool ONE, bool SHADE = false>
 __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_NEAREST : VPX_WPE_MULTI_NEAREST) void k_primary(SceneView sv, FrameArgs f, WaveBufs w,
                                                  unsigned long long* __restrict__ ctr) {
     __shared__ uint32_t sh[4];
@@ -624,6 +628,12 @@ __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_NEAREST : VPX_WPE_MULTI_
         }
     }
     flush_counters(k, prim, ctr, VPX_STAGE_PRIMARY);
+    if (SHADE) {  // level 0's material switch for this thread's own path (k_primary_shade)
+        __syncthreads();  // the tile's hit records, written by the compacted walkers
+        Counters ks{0u, 0u, 0u};
+        shade_path(sv, f, w, p, 0, ks);
+        flush_counters(ks, 0u, ctr, VPX_STAGE_SHADE);
+    }
 }
 
 // Sparse stages (bounce FindNearest, IsOccluded) can gather the work of G tiles per
@@ -642,6 +652,11 @@ constexpr uint32_t kGroupTiles = VPX_GROUP_TILES;
 #define VPX_FUSE_TAIL 1
 #endif
 constexpr bool kFuseTail = VPX_FUSE_TAIL != 0;
+// Run level 0's material switch at the end of the primary-ray kernel (k_primary<.., true>).
+#ifndef VPX_FUSE_HEAD
+#define VPX_FUSE_HEAD 1
+#endif
+constexpr bool kFuseHead = VPX_FUSE_HEAD != 0;
 
 // Prefix scan over the G*256 paths of a workgroup (each thread scans G paths).
 template <uint32_t G>
