@@ -1134,7 +1134,8 @@ static int run_jobs(const oracle_scene* sc, const vpx_frame_params* p, const uin
             stats->bounce_rays += jobs[t].nearest;
             stats->dda_cells += jobs[t].cells;
         }
-        stats->bounce_rays -= n;
+        /* Trace(ray, -1) makes no FindNearest call: no bounce rays (not a negative count) */
+        stats->bounce_rays = stats->bounce_rays > n ? stats->bounce_rays - n : 0;
     }
     return VPX_OK;
 }

@@ -693,7 +693,8 @@ int snapshot_counters(vpx_ctx* c, unsigned long long out[kCtrWords]) {
 void fill_stats(vpx_stats* s, const unsigned long long a[kCtrWords], const unsigned long long b[kCtrWords]) {
     s->shadow_rays = b[0] - a[0];
     s->primary_rays = b[3] - a[3];
-    s->bounce_rays = (b[1] - a[1]) - s->primary_rays;
+    const unsigned long long nearest = b[1] - a[1];  // 0 for Trace(ray, -1): no bounce rays
+    s->bounce_rays = nearest > s->primary_rays ? nearest - s->primary_rays : 0;
     s->dda_cells = b[2] - a[2];
 }
 

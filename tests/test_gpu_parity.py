@@ -94,6 +94,34 @@ def test_render_frame_bit_exact(pkg, orc, name):
         ost.primary_rays, ost.shadow_rays, ost.bounce_rays, ost.dda_cells)
 
 
+@pytest.mark.parametrize("depth", [-1, 0, 1, 3])
+@pytest.mark.parametrize("lights", ["points", "areas"])
+def test_depth_sweep_fused_head_tail(pkg, orc, depth, lights):
+    """The fused kernels' edges: level 0 shaded inside k_primary, the last level's IsOccluded
+    + light resolve + finish in k_shadow_finish (several area-light slots per path), and
+    Trace(ray, -1) (no level runs: the plain finish folds the zero leaf).  Two frames, so the
+    running average goes through the fused finish twice."""
+    sc = pkg.scene
+    areas = sc.C3_AREAS[:2] if lights == "areas" else None
+    desc = sc.city_scene("roomGlass", 128, 48, 40, depth, areas=areas)
+    desc.area_samples = 3
+    acc_g, rgb_g, st = render_gpu(pkg, desc, frames=2)
+    o = orc.Oracle(pkg.abi, desc)
+    acc = None
+    ost = None
+    for f in range(2):
+        acc, rgb, ost = o.render(desc.frame_params(f), accum=acc)
+    assert np.array_equal(bits(acc_g), bits(acc))
+    assert np.array_equal(rgb_g, rgb)
+    s = st[-1]
+    assert (s.primary_rays, s.shadow_rays, s.bounce_rays, s.dda_cells) == (
+        ost.primary_rays, ost.shadow_rays, ost.bounce_rays, ost.dda_cells)
+    if depth >= 0:
+        assert s.shadow_rays > 0
+    else:
+        assert s.bounce_rays == 0 and s.dda_cells == 0
+
+
 def test_progressive_accumulation_aa(pkg, orc):
     """4 frames with AA jitter: running average w = 1/(n+1), seeds advance per frame."""
     desc = pkg.scene.model_scene("monu3", 128, 80, 48, 1, city_lights=True)
