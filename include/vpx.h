@@ -39,6 +39,7 @@
  *   vpx_default_materials    Renderer::MaterialSetUp     renderer.cpp:357-443
  *   vpx_bvh_build_host       BasicBVH::BuildBVH          src/BVH/BasicBVH.cpp:72-136
  *   vpx_bvh_random_tris      BasicBVH::BasicBVH()        src/BVH/BasicBVH.cpp:4-16
+ *   vpx_bvh_depth            (recursion depth of IntersectBVH, src/BVH/BasicBVH.cpp:47-61)
  */
 #ifndef VPX_H_
 #define VPX_H_
@@ -341,6 +342,7 @@ int vpx_focus_distance(vpx_ctx* ctx, uint32_t width, uint32_t height, float* foc
    offers it.  The device traversal stages the whole BVH (nodes, triangles, indices) in
    LDS per workgroup, one ray per lane. */
 #define VPX_BVH_MAX_TRIS 512
+#define VPX_BVH_MAX_DEPTH 63   /* deepest tree the device traversal stack holds (root = 1) */
 typedef struct vpx_bvh_tri {       /* Tri (BasicBVH.h:3-7) without the centroid */
     float v0[3], v1[3], v2[3];
 } vpx_bvh_tri;                     /* 36 bytes */
@@ -349,7 +351,8 @@ typedef struct vpx_bvh_node {      /* BVHNode (BasicBVH.h:11-20) */
     uint32_t left_first, tri_count;
 } vpx_bvh_node;                    /* 32 bytes */
 /* Build (vpx_bvh_build_host) and upload the BVH of n triangles (1..VPX_BVH_MAX_TRIS;
-   n = 0 removes it). */
+   n = 0 removes it).  The midpoint split has no depth cap (as the reference's recursion):
+   a tree deeper than VPX_BVH_MAX_DEPTH (vpx_bvh_depth) is refused with VPX_E_INVALID. */
 int vpx_bvh_set(vpx_ctx* ctx, const vpx_bvh_tri* tris, uint32_t n);
 /* IntersectBVH(ray, 0) per ray: rays built as in vpx_find_nearest (Ray(O, D) normalises D,
    t = tmax); t_out[i] = ray.t afterwards (tmax when nothing closer is hit). */
@@ -376,6 +379,8 @@ uint32_t vpx_pixel_seed(uint32_t seed_base, uint32_t frame_index, uint32_t width
    number of nodes used is stored in *nodes_used. */
 int vpx_bvh_build_host(const vpx_bvh_tri* tris, uint32_t n, vpx_bvh_node* nodes, uint32_t* tri_idx,
                        uint32_t* nodes_used);
+/* Depth of a tree built by vpx_bvh_build_host (a leaf root = 1; 0 when nodes_used == 0). */
+uint32_t vpx_bvh_depth(const vpx_bvh_node* nodes, uint32_t nodes_used);
 /* BasicBVH::BasicBVH() triangle set (BasicBVH.cpp:4-16): 64 triangles, vertex0 = r0*9-5,
    vertex1 = vertex0+r1, vertex2 = vertex0+r2, each r a float3 of RandomFloat() from the
    xorshift32 state *seed (advanced; the three draws of a float3 taken left to right —

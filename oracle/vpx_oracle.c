@@ -71,11 +71,75 @@ static inline int f2i_trunc(float f)
     return (int)f;
 }
 
-/* Correctly rounded float transcendentals (see header comment). */
-static inline float cr_sinf(float x) { return (float)sin((double)x); }
-static inline float cr_cosf(float x) { return (float)cos((double)x); }
-static inline float cr_expf(float x) { return (float)exp((double)x); }
-static inline float cr_powf(float x, float y) { return (float)pow((double)x, (double)y); }
+/* sinf / cosf / expf / powf(x, 5) (tmpl8math.h:2506-2508, renderer.cpp:1593, 1607, 1615):
+ * the float result of one fixed double-precision evaluation (Cody-Waite reduction, fdlibm
+ * kernel polynomials), within 1 ulp (double) of the true value, hence the correctly rounded
+ * float except at double-rounding midpoints.  tests/test_cpu_oracle.py checks these against
+ * (float)libm(double) on 4M arguments each.  The device evaluates the same operations in the
+ * same order (csrc/vpx_trace.hpp namespace dm), so the two agree bit for bit by construction
+ * -- the MSVC powf/sinf the reference links are unknowable here (parity hazard 4). */
+static const double dm_S1 = -1.66666666666666324348e-01, dm_S2 = 8.33333333332248946124e-03,
+                    dm_S3 = -1.98412698298579493134e-04, dm_S4 = 2.75573137070700676789e-06,
+                    dm_S5 = -2.50507602534068634195e-08, dm_S6 = 1.58969099521155010221e-10;
+static const double dm_C1 = 4.16666666666666019037e-02, dm_C2 = -1.38888888888741095749e-03,
+                    dm_C3 = 2.48015872894767294178e-05, dm_C4 = -2.75573143513906633035e-07,
+                    dm_C5 = 2.08757232129817482790e-09, dm_C6 = -1.13596475577881948265e-11;
+static const double dm_invpio2 = 6.36619772367581382433e-01, dm_pio2_1 = 1.57079632673412561417e+00,
+                    dm_pio2_1t = 6.07710050650619224932e-11;
+static const double dm_ln2hi = 6.93147180369123816490e-01, dm_ln2lo = 1.90821492927058770002e-10,
+                    dm_invln2 = 1.44269504088896338700e+00;
+static const double dm_P1 = 1.66666666666666019037e-01, dm_P2 = -2.77777777770155933842e-03,
+                    dm_P3 = 6.61375632143793436117e-05, dm_P4 = -1.65339022054652515390e-06,
+                    dm_P5 = 4.13813679705723846039e-08;
+static inline double dm_ksin(double x)
+{
+    const double z = x * x, v = z * x;
+    const double r = dm_S2 + z * (dm_S3 + z * (dm_S4 + z * (dm_S5 + z * dm_S6)));
+    return x + v * (dm_S1 + z * r);
+}
+static inline double dm_kcos(double x)
+{
+    const double z = x * x;
+    const double r = z * (dm_C1 + z * (dm_C2 + z * (dm_C3 + z * (dm_C4 + z * (dm_C5 + z * dm_C6)))));
+    const double hz = 0.5 * z, w = 1.0 - hz;
+    return w + (((1.0 - w) - hz) + z * r);
+}
+/* |x| < 2^20: k * dm_pio2_1 is exact (33-bit constant) */
+static inline void dm_sincosf(float xf, float* sf, float* cf)
+{
+    const double x = (double)xf;
+    const double k = rint(x * dm_invpio2);
+    const double r = (x - k * dm_pio2_1) - k * dm_pio2_1t;
+    const int n = (int)k & 3;
+    const double s = dm_ksin(r), c = dm_kcos(r);
+    *sf = (float)(n == 0 ? s : n == 1 ? c : n == 2 ? -s : -c);
+    *cf = (float)(n == 0 ? c : n == 1 ? -s : n == 2 ? -c : s);
+}
+static inline float cr_sinf(float x) { float s, c; dm_sincosf(x, &s, &c); return s; }
+static inline float cr_cosf(float x) { float s, c; dm_sincosf(x, &s, &c); return c; }
+static inline float cr_expf(float xf)
+{
+    if (xf != xf) return xf;
+    double x = (double)xf;
+    x = x < -800.0 ? -800.0 : (x > 800.0 ? 800.0 : x);
+    const double k = rint(x * dm_invln2);
+    const double hi = x - k * dm_ln2hi, lo = k * dm_ln2lo;
+    const double r = hi - lo, t = r * r;
+    const double c = r - t * (dm_P1 + t * (dm_P2 + t * (dm_P3 + t * (dm_P4 + t * dm_P5))));
+    const double y = 1.0 - ((lo - (r * c) / (2.0 - c)) - hi);
+    return (float)ldexp(y, (int)k);
+}
+static inline float cr_pow5f(float xf)
+{
+    const double x = (double)xf, x2 = x * x, x4 = x2 * x2;
+    return (float)(x4 * x);
+}
+/* for the CPU pin test: fn 0 sin, 1 cos, 2 exp, 3 pow5 over n arguments */
+void oracle_dm_eval(int fn, const float* x, float* out, uint32_t n)
+{
+    for (uint32_t i = 0; i < n; ++i)
+        out[i] = fn == 0 ? cr_sinf(x[i]) : fn == 1 ? cr_cosf(x[i]) : fn == 2 ? cr_expf(x[i]) : cr_pow5f(x[i]);
+}
 
 /* ----------------------------------------------------------------------- RNG -- */
 /* WangHash, template/tmpl8math.cpp:20-27 */
@@ -650,12 +714,12 @@ static inline float schlick(float cosine, float ior)
 {
     float r0 = (1 - ior) / (1 + ior);
     r0 = r0 * r0;
-    return r0 + (1 - r0) * cr_powf((1 - cosine), 5);
+    return r0 + (1 - r0) * cr_pow5f(1 - cosine);
 }
 static inline float schlick_nonmetal(float cosine)
 {
     const float r0 = 0.04f;
-    return r0 + (1 - r0) * cr_powf((1 - cosine), 5);
+    return r0 + (1 - r0) * cr_pow5f(1 - cosine);
 }
 
 /* Renderer::Absorption, renderer.cpp:1596-1608 */

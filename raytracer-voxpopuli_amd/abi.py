@@ -105,6 +105,7 @@ class BvhNode(C.Structure):  # vpx_bvh_node: BVHNode (BasicBVH.h:11-20)
 
 
 BVH_MAX_TRIS = 512
+BVH_MAX_DEPTH = 63
 
 STAGES = ("primary", "shade", "shadow", "resolve", "bounce", "finish")
 
@@ -180,6 +181,7 @@ SIGNATURES = {
     "vpx_bvh_build_host": (C.c_int, [C.POINTER(BvhTri), C.c_uint32, C.POINTER(BvhNode), C.POINTER(C.c_uint32),
                                      C.POINTER(C.c_uint32)]),
     "vpx_bvh_random_tris": (C.c_int, [C.POINTER(C.c_uint32), C.POINTER(BvhTri)]),
+    "vpx_bvh_depth": (C.c_uint32, [C.POINTER(BvhNode), C.c_uint32]),
 }
 
 _LIB = None

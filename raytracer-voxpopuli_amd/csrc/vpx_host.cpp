@@ -348,6 +348,24 @@ int vpx_bvh_build_host(const vpx_bvh_tri* tris, uint32_t n, vpx_bvh_node* nodes,
     return VPX_OK;
 }
 
+uint32_t vpx_bvh_depth(const vpx_bvh_node* nodes, uint32_t nodes_used) {
+    if (!nodes || !nodes_used) return 0;
+    // iterative (a degenerate chain of VPX_BVH_MAX_TRIS triangles is 511 deep)
+    std::vector<std::pair<uint32_t, uint32_t>> st{{0u, 1u}};
+    uint32_t best = 0;
+    while (!st.empty()) {
+        const auto [ni, d] = st.back();
+        st.pop_back();
+        if (ni >= nodes_used) return 0;  // not a tree built by vpx_bvh_build_host
+        best = d > best ? d : best;
+        if (!nodes[ni].tri_count) {
+            st.push_back({nodes[ni].left_first, d + 1});
+            st.push_back({nodes[ni].left_first + 1, d + 1});
+        }
+    }
+    return best;
+}
+
 int vpx_bvh_random_tris(uint32_t* seed, vpx_bvh_tri out[64]) {
     if (!seed || !out) return VPX_E_INVALID;
     for (int i = 0; i < 64; ++i) {  // BasicBVH::BasicBVH (BasicBVH.cpp:4-16)

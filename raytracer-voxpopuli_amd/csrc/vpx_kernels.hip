@@ -1298,13 +1298,6 @@ int vpx_trace(vpx_ctx* c, const vpx_ray* rays, const uint32_t* seeds, uint32_t n
     return VPX_OK;
 }
 
-// Depth of a built BasicBVH (root = 1); the traversal stack needs one entry per level.
-static uint32_t bvh_depth(const vpx_bvh_node* nodes, uint32_t ni) {
-    if (nodes[ni].tri_count) return 1;
-    const uint32_t l = bvh_depth(nodes, nodes[ni].left_first), r = bvh_depth(nodes, nodes[ni].left_first + 1);
-    return 1 + (l > r ? l : r);
-}
-
 int vpx_bvh_set(vpx_ctx* c, const vpx_bvh_tri* tris, uint32_t n) {
     if (!c || (n && !tris)) return fail(c, VPX_E_INVALID, "null argument");
     if (n > VPX_BVH_MAX_TRIS) return fail(c, VPX_E_INVALID, "more triangles than VPX_BVH_MAX_TRIS");
@@ -1319,7 +1312,9 @@ int vpx_bvh_set(vpx_ctx* c, const vpx_bvh_tri* tris, uint32_t n) {
     int rc = vpx_bvh_build_host(tris, n, nodes.data(), idx.data(), &used);
     if (rc) return fail(c, rc, "vpx_bvh_build_host failed");
     // the traversal pushes both children of every interior node it enters
-    if (bvh_depth(nodes.data(), 0) + 1 > (uint32_t)kBvhStack) return fail(c, VPX_E_INVALID, "BVH deeper than the traversal stack");
+    static_assert(VPX_BVH_MAX_DEPTH + 1 <= kBvhStack, "traversal stack: one pending sibling per level + the root");
+    if (vpx_bvh_depth(nodes.data(), used) > VPX_BVH_MAX_DEPTH)
+        return fail(c, VPX_E_INVALID, "BVH deeper than VPX_BVH_MAX_DEPTH (the traversal stack)");
     std::vector<uint32_t> img(used * 8u + n * 9u);
     std::memcpy(img.data(), nodes.data(), sizeof(vpx_bvh_node) * used);
     for (uint32_t k = 0; k < n; ++k) std::memcpy(&img[used * 8u + k * 9u], &tris[idx[k]], sizeof(vpx_bvh_tri));

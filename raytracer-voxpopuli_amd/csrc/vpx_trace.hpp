@@ -101,10 +101,69 @@ __device__ __forceinline__ int trunc_i32(float f) {
 __device__ __forceinline__ float sign_of(float d) { return (float)(__float_as_uint(d) >> 31); }
 __device__ __forceinline__ f3 dsign(f3 d) { return mk(sign_of(d.x), sign_of(d.y), sign_of(d.z)); }
 
-__device__ __forceinline__ float cr_sin(float x) { return (float)sin((double)x); }
-__device__ __forceinline__ float cr_cos(float x) { return (float)cos((double)x); }
-__device__ __forceinline__ float cr_exp(float x) { return (float)exp((double)x); }
-__device__ __forceinline__ float cr_pow5(float x) { return (float)pow((double)x, 5.0); }
+// sinf / cosf / expf / powf(x, 5) of the reference (tmpl8math.h:2506-2508, renderer.cpp:
+// 1593, 1607, 1615) as float results of one fixed double-precision evaluation that the
+// oracle repeats operation for operation (vpx_oracle.c dm_*): Cody-Waite reduction and the
+// fdlibm kernel polynomials, within 1 ulp (double) of the true value, so the float result
+// is the correctly rounded one except at double-rounding midpoints (none in 4M samples per
+// function, tests/test_cpu_oracle.py).  ocml's sin/cos/exp/pow carry a large-argument
+// reduction path whose registers spilled the fused level-0 shade; the callers' arguments
+// are bounded (sin/cos: [0, 2pi), exp: <= 0, pow5: [0, 2]).
+namespace dm {
+constexpr double kS1 = -1.66666666666666324348e-01, kS2 = 8.33333333332248946124e-03,
+                 kS3 = -1.98412698298579493134e-04, kS4 = 2.75573137070700676789e-06,
+                 kS5 = -2.50507602534068634195e-08, kS6 = 1.58969099521155010221e-10;
+constexpr double kC1 = 4.16666666666666019037e-02, kC2 = -1.38888888888741095749e-03,
+                 kC3 = 2.48015872894767294178e-05, kC4 = -2.75573143513906633035e-07,
+                 kC5 = 2.08757232129817482790e-09, kC6 = -1.13596475577881948265e-11;
+constexpr double kInvPio2 = 6.36619772367581382433e-01, kPio2_1 = 1.57079632673412561417e+00,
+                 kPio2_1t = 6.07710050650619224932e-11;
+constexpr double kLn2Hi = 6.93147180369123816490e-01, kLn2Lo = 1.90821492927058770002e-10,
+                 kInvLn2 = 1.44269504088896338700e+00;
+constexpr double kP1 = 1.66666666666666019037e-01, kP2 = -2.77777777770155933842e-03,
+                 kP3 = 6.61375632143793436117e-05, kP4 = -1.65339022054652515390e-06,
+                 kP5 = 4.13813679705723846039e-08;
+__device__ __forceinline__ double ksin(double x) {  // |x| <= pi/4
+    const double z = x * x, v = z * x;
+    const double r = kS2 + z * (kS3 + z * (kS4 + z * (kS5 + z * kS6)));
+    return x + v * (kS1 + z * r);
+}
+__device__ __forceinline__ double kcos(double x) {  // |x| <= pi/4
+    const double z = x * x;
+    const double r = z * (kC1 + z * (kC2 + z * (kC3 + z * (kC4 + z * (kC5 + z * kC6)))));
+    const double hz = 0.5 * z, w = 1.0 - hz;
+    return w + (((1.0 - w) - hz) + z * r);
+}
+// sin and cos of one argument, |x| < 2^20 (k * kPio2_1 exact: kPio2_1 has 33 bits)
+__device__ __forceinline__ void sincos(float xf, float& sf, float& cf) {
+    const double x = (double)xf;
+    const double k = __builtin_rint(x * kInvPio2);
+    const double r = (x - k * kPio2_1) - k * kPio2_1t;
+    const int n = (int)k & 3;
+    const double s = ksin(r), c = kcos(r);
+    sf = (float)(n == 0 ? s : n == 1 ? c : n == 2 ? -s : -c);
+    cf = (float)(n == 0 ? c : n == 1 ? -s : n == 2 ? -c : s);
+}
+__device__ __forceinline__ float exp(float xf) {
+    if (xf != xf) return xf;
+    double x = (double)xf;
+    x = x < -800.0 ? -800.0 : (x > 800.0 ? 800.0 : x);
+    const double k = __builtin_rint(x * kInvLn2);
+    const double hi = x - k * kLn2Hi, lo = k * kLn2Lo;
+    const double r = hi - lo, t = r * r;
+    const double c = r - t * (kP1 + t * (kP2 + t * (kP3 + t * (kP4 + t * kP5))));
+    const double y = 1.0 - ((lo - (r * c) / (2.0 - c)) - hi);
+    return (float)__builtin_ldexp(y, (int)k);
+}
+__device__ __forceinline__ float pow5(float xf) {
+    const double x = (double)xf, x2 = x * x, x4 = x2 * x2;
+    return (float)(x4 * x);
+}
+}  // namespace dm
+__device__ __forceinline__ float cr_sin(float x) { float s, c; dm::sincos(x, s, c); return s; }
+__device__ __forceinline__ float cr_cos(float x) { float s, c; dm::sincos(x, s, c); return c; }
+__device__ __forceinline__ float cr_exp(float x) { return dm::exp(x); }
+__device__ __forceinline__ float cr_pow5(float x) { return dm::pow5(x); }
 
 // ---------------------------------------------------------------------------- RNG
 // WangHash / xorshift32 / RandomFloat: template/tmpl8math.cpp:20-27, 119-133.
@@ -726,8 +785,10 @@ __device__ __forceinline__ f3 random_sphere_sample(Rng& g) {
     const float theta = g.next() * 2.0f * kPi;
     const float phi = g.next() * kPi;
     const float r = g.next();
-    const float sp = cr_sin(phi);
-    return mk(r * sp * cr_cos(theta), r * sp * cr_sin(theta), r * cr_cos(phi));
+    float sp, cp, st, ct;
+    dm::sincos(phi, sp, cp);
+    dm::sincos(theta, st, ct);
+    return mk(r * sp * ct, r * sp * st, r * cp);
 }
 __device__ __forceinline__ f3 diffuse_reflection(Rng& g, f3 n) {
     f3 r;

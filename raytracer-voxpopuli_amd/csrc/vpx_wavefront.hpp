@@ -54,13 +54,19 @@ struct FrameArgs {
     uint32_t tiles_per_rank;
 };
 
+// Per-path level forms: level l's 2-bit form at bits 2l..2l+1 and a sentinel 1 just above
+// the last recorded level, so a count of up to kMaxLevels - 1 = 15 levels (max_bounces 14)
+// takes bits 0..30 (a separate count field would not fit beside 30 form bits).
+static_assert(2 * (kMaxLevels - 1) < 32, "forms word: 2 bits per level + sentinel must fit 32 bits");
+__device__ __forceinline__ uint32_t forms_count(uint32_t forms) { return (31u - (uint32_t)__clz(forms)) >> 1; }
+
 struct WaveBufs {
     float4* O;     // [P] ray origin, w = rng state bits
     float4* D;     // [P] ray direction, w = flags bits (kActive | kInside)
     float4* H;     // [P] hit: t, normal
     uint32_t* HM;  // [P] hit: material | (vox + 2) << 8
     int32_t* depth;  // [P] remaining Trace depth
-    uint32_t* forms; // [P] 2 bits per level + level count in bits 27..31
+    uint32_t* forms; // [P] form of level l in bits 2l..2l+1, sentinel 1 at bit 2*count (forms_count)
     float4* LA;    // [L][P] level multiplier a (xyz)
     float4* LB;    // [L][P] level addend b (xyz)
     float4* leaf;  // [P] leaf radiance (sky / emissive / 0)
@@ -92,7 +98,9 @@ __device__ __forceinline__ Ray primary_ray(const FrameArgs& f, uint32_t x, uint3
     if (f.flags & VPX_FLAG_DOF) {
         const float rr = sqrtf(g.next());
         const float theta = g.next() * (2.0f * kPi);
-        const float cx = cr_cos(theta) * rr, cy = cr_sin(theta) * rr;
+        float st, ct;
+        dm::sincos(theta, st, ct);
+        const float cx = ct * rr, cy = st * rr;
         const float jx = (cx * f.cam.defocus_jitter) / (float)f.width;
         const float jy = (cy * f.cam.defocus_jitter) / (float)f.width;
         const f3 focal = cp + normalize(P - cp) * f.cam.focal_distance;
@@ -249,6 +257,10 @@ __device__ __forceinline__ uint32_t wave_prefix(uint32_t v, uint32_t& total) {
     return x - v;
 }
 
+// L0: the call shades level 0 (the fused head in k_primary).  Level 0 rays are primary
+// rays, which never start inside glass or smoke, so the interior exit marches (a whole DDA
+// walker each) drop out of that instance; the forms word is known (no levels yet).
+template <bool L0 = false>
 __device__ __forceinline__ void shade_path(const SceneView& sv, const FrameArgs& f, const WaveBufs& w, uint32_t p,
                                            int level, Counters& k) {
     uint32_t slots = 0;
@@ -266,7 +278,7 @@ __device__ __forceinline__ void shade_path(const SceneView& sv, const FrameArgs&
             ray.t = hh.x;
             ray.N = mk(hh.y, hh.z, hh.w);
             ray.mat = hm & 0xffu;
-            ray.inside = (hm & 0x80000000u) != 0u;
+            ray.inside = L0 ? false : (hm & 0x80000000u) != 0u;
             if ((f.flags & kFlagReproject) && level == 0) {  // RayDataReproject::GetRayInfo (renderer.h:31-34)
                 uint32_t x, y;
                 if (path_pixel(f, p, x, y)) {
@@ -277,8 +289,9 @@ __device__ __forceinline__ void shade_path(const SceneView& sv, const FrameArgs&
             const int32_t vox = (int32_t)((hm >> 8) & 0xffffu) - 2;
             Rng g{__float_as_uint(oo.w)};
             int depth = w.depth[p];
-            uint32_t forms = w.forms[p];
-            const uint32_t nl = forms >> 27;
+            // a path being shaded at `level` has recorded exactly `level` forms
+            uint32_t forms = (L0 || level == 0) ? 1u : w.forms[p];
+            const uint32_t nl = forms_count(forms);
             bool done = false;
             f3 leaf = mk(0.f, 0.f, 0.f);
             if (ray.mat == kNone) {  // SampleSky, :1092-1095
@@ -394,7 +407,7 @@ __device__ __forceinline__ void shade_path(const SceneView& sv, const FrameArgs&
                 // levels always carry a pending light whose k_resolve writes LB: no zero fill
                 const uint64_t li = (uint64_t)nl * w.P + p;
                 w.LA[li] = make_float4(a.x, a.y, a.z, 0.f);
-                forms = (forms & 0x07ffffffu) | (form << (2 * nl)) | ((nl + 1u) << 27);
+                forms = (forms ^ (1u << (2 * nl))) | (form << (2 * nl)) | (1u << (2 * nl + 2));
                 if (pending) {
                     pending |= (nl << 8);
                     w.SM[p] = make_float4(kd.x, kd.y, kd.z, __uint_as_float(pending));
@@ -574,7 +587,7 @@ __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_NEAREST : VPX_WPE_MULTI_
         uint32_t x, y;
         bool go = path_pixel(f, p, x, y);
         w.depth[p] = f.max_bounces;
-        w.forms[p] = 0u;
+        w.forms[p] = 1u;  // no levels recorded
         w.leaf[p] = make_float4(0.f, 0.f, 0.f, 0.f);
         Ray r;
         r.O = r.D = mk(0.f, 0.f, 0.f);
@@ -631,7 +644,7 @@ __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_NEAREST : VPX_WPE_MULTI_
     if (SHADE) {  // level 0's material switch for this thread's own path (k_primary_shade)
         __syncthreads();  // the tile's hit records, written by the compacted walkers
         Counters ks{0u, 0u, 0u};
-        shade_path(sv, f, w, p, 0, ks);
+        shade_path<true>(sv, f, w, p, 0, ks);
         flush_counters(ks, 0u, ctr, VPX_STAGE_SHADE);
     }
 }
@@ -806,7 +819,7 @@ __device__ __forceinline__ void finish_path(const FrameArgs& f, const WaveBufs& 
         const float4 lf = w.leaf[p];
         v = mk(lf.x, lf.y, lf.z);
         const uint32_t forms = w.forms[p];
-        for (int i = (int)(forms >> 27) - 1; i >= 0; --i) {
+        for (int i = (int)forms_count(forms) - 1; i >= 0; --i) {
             const uint32_t form = (forms >> (2 * i)) & 3u;
             const uint64_t li = (uint64_t)i * w.P + p;
             const float4 a4 = w.LA[li];
@@ -897,7 +910,7 @@ __global__ __launch_bounds__(256) void k_finish_reproject(FrameArgs f, WaveBufs 
         const float4 lf = w.leaf[p];
         f3 v = mk(lf.x, lf.y, lf.z);
         const uint32_t forms = w.forms[p];
-        const int nl = (int)(forms >> 27);
+        const int nl = (int)forms_count(forms);
         if (nl == 0) {  // sky / emissive at the top: {colour, 1} (renderer.cpp:1333, 2330-2333)
             A = v;
             I = mk(1.f, 1.f, 1.f);

@@ -83,6 +83,24 @@ def test_host_build_matches_oracle_and_is_a_valid_tree(pkg, orc):
             assert used == 1  # the split of identical centroids aborts (BasicBVH.cpp:123-124)
 
 
+def test_depth_of_degenerate_chain(pkg, orc):
+    """vpx_bvh_depth (what vpx_bvh_set checks against VPX_BVH_MAX_DEPTH): centroids at
+    x = 2^i make every midpoint split peel off one triangle, a chain as deep as the set."""
+    abi, lib = pkg.abi, pkg.load_library()
+    for n, want in ((80, 79), (40, 39), (2, 1), (1, 1)):  # leaves hold <= 2 triangles
+        v = np.zeros((n, 9), np.float32)
+        x = np.float32(2.0) ** np.arange(n, dtype=np.float32)
+        v[:, 0], v[:, 3], v[:, 6] = x, x, x
+        v[:, 4], v[:, 8] = 1.0, 1.0
+        nodes, idx, used = lib_build(pkg, tri_array(abi, v))
+        o = orc.BasicBVH(abi, tri_array(abi, v))
+        assert used == o.used and bytes(nodes)[: 32 * used] == bytes(o.nodes)[: 32 * used]
+        assert lib.vpx_bvh_depth(nodes, used) == want, n
+    assert lib.vpx_bvh_depth(nodes, 0) == 0
+    nodes, idx, used = lib_build(pkg, orc.BasicBVH.random_tris(abi)[0])
+    assert 1 < lib.vpx_bvh_depth(nodes, used) <= abi.BVH_MAX_DEPTH  # the reference's own set fits
+
+
 def test_oracle_traversal_equals_a_linear_loop(pkg, orc):
     """Sanity of the restatement: the BVH's nearest t is the nearest over all triangles
     (up to rays whose hit lies on a box face within float rounding)."""

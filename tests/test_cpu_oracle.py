@@ -300,3 +300,34 @@ def test_emissive_sphere_restatement(orc, pkg, n, radius):
     d = np.sqrt(((vx * vx) + (vy * vy)) + (vz * vz)).astype(np.float32)
     want = np.where(d < np.float32(radius), 15, 255).astype(np.uint8).reshape(-1)
     assert np.array_equal(g, want)
+
+
+@pytest.mark.parametrize("fn,name", [(0, "sin"), (1, "cos"), (2, "exp"), (3, "pow5")])
+def test_transcendentals_are_correctly_rounded_floats(orc, abi, fn, name):
+    """Parity hazard 4: sinf/cosf/expf/powf(x, 5) are the float results of one
+    fixed double-precision evaluation (the device runs the same operations).  Pinned here
+    against libm in double rounded to float, on the arguments the path feeds them:
+    RandomSphereSample / the DOF disc (RandomFloat * 2 * PI, RandomFloat * PI), Absorption
+    (-dist * intensity * (1 - albedo) <= 0), Schlick (1 - cos in [0, 2])."""
+    lib = orc._lib(abi)
+    lib.oracle_dm_eval.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_uint32]
+    lib.oracle_dm_eval.restype = None
+    rng = np.random.default_rng(40 + fn)
+    m = 1 << 22
+    u = (rng.integers(0, 1 << 32, m, dtype=np.uint64).astype(np.float32) * np.float32(2.3283064365387e-10))
+    if fn < 2:
+        x = np.concatenate([u * np.float32(2) * np.float32(np.pi), u * np.float32(np.pi)])
+        ref = (np.sin if fn == 0 else np.cos)(x.astype(np.float64))
+    elif fn == 2:
+        x = np.concatenate([-(u * np.float32(120)), -(u * np.float32(1e-3)), np.float32([0, -0.0, -104, -1e30])])
+        ref = np.exp(x.astype(np.float64))
+    else:
+        x = np.concatenate([u * np.float32(2), u * np.float32(1e-6), np.float32([0, 1, 2])])
+        ref = np.power(x.astype(np.float64), 5.0)
+    x = np.ascontiguousarray(x, np.float32)
+    out = np.empty_like(x)
+    lib.oracle_dm_eval(fn, x.ctypes.data, out.ctypes.data, len(x))
+    ref32 = ref.astype(np.float32)
+    for a in (ref32, out):  # FTZ (template/template.cpp:130; the path runs with it set)
+        a[np.abs(a) < np.float32(2.0 ** -126)] = 0.0
+    assert np.array_equal(bits(np.abs(out)), bits(np.abs(ref32))), f"{name}: {(bits(out) != bits(ref32)).sum()} mismatches"

@@ -122,6 +122,29 @@ def test_depth_sweep_fused_head_tail(pkg, orc, depth, lights):
         assert s.bounce_rays == 0 and s.dda_cells == 0
 
 
+@pytest.mark.parametrize("depth", [13, 14])
+def test_deepest_levels(pkg, orc, depth):
+    """Renderer::maxBounces = 14 (renderer.h:175), the API's maximum: 15 levels of records
+    in the per-path forms word (2 bits a level + the sentinel that marks the count).  The
+    tiled glass rooms keep paths alive to the last level (checked: depth d casts more bounce
+    rays than depth d - 1); two frames, every float and byte equal to the oracle."""
+    sc = pkg.scene
+    desc = sc.city_scene("roomGlass", 128, 64, 48, depth)
+    acc_g, rgb_g, st = render_gpu(pkg, desc, frames=2)
+    o = orc.Oracle(pkg.abi, desc)
+    acc = None
+    for f in range(2):
+        acc, rgb, ost = o.render(desc.frame_params(f), accum=acc)
+    assert np.array_equal(bits(acc_g), bits(acc))
+    assert np.array_equal(rgb_g, rgb)
+    s = st[-1]
+    assert (s.primary_rays, s.shadow_rays, s.bounce_rays, s.dda_cells) == (
+        ost.primary_rays, ost.shadow_rays, ost.bounce_rays, ost.dda_cells)
+    desc.max_bounces = depth - 1
+    _, _, shallower = o.render(desc.frame_params(1))
+    assert ost.bounce_rays > shallower.bounce_rays  # some paths reach level `depth`
+
+
 def test_progressive_accumulation_aa(pkg, orc):
     """4 frames with AA jitter: running average w = 1/(n+1), seeds advance per frame."""
     desc = pkg.scene.model_scene("monu3", 128, 80, 48, 1, city_lights=True)
@@ -312,7 +335,22 @@ def test_bvh_intersect(pkg, orc, n):
     assert (t_o < 1e33).mean() > 0.1
     with pytest.raises(pkg.abi.VpxError):
         ctx.bvh_set((abi.BvhTri * (abi.BVH_MAX_TRIS + 1))())
+    # a degenerate chain deeper than the device traversal stack is refused, not traversed
+    with pytest.raises(pkg.abi.VpxError, match="VPX_BVH_MAX_DEPTH"):
+        ctx.bvh_set(chain_tris(abi, 80))
     ctx.close()
+
+
+def chain_tris(abi, n):
+    """Triangles with centroids at x = 2^i: every midpoint split peels off the last one, so
+    the tree is a chain n deep (the reference's recursion has no depth cap)."""
+    v = np.zeros((n, 9), np.float32)
+    x = np.float32(2.0) ** np.arange(n, dtype=np.float32)
+    v[:, 0], v[:, 3], v[:, 6] = x, x, x
+    v[:, 4], v[:, 8] = 1.0, 1.0
+    tris = (abi.BvhTri * n)()
+    np.frombuffer(tris, np.float32).reshape(-1, 9)[:] = v
+    return tris
 
 
 def test_smoke_material_exits(pkg, orc):
@@ -460,7 +498,8 @@ def test_world_edits_random_boxes_odd_size(pkg, orc):
     r.ctx.close()
 
 
-@pytest.mark.parametrize("name,depth", [("monu3", 2), ("roomGlass", 4), ("teapot", 3)])
+@pytest.mark.parametrize("name,depth", [("monu3", 2), ("roomGlass", 4), ("teapot", 3), ("roomGlass", 13),
+                                        ("roomGlass", 14)])
 def test_static_camera_reprojection(pkg, orc, name, depth):
     """SURVEY §8(f) rank 1: Renderer::Tick's static branch — TraceReproject, reprojection
     into the previous camera, history clamp/blend — 3 frames with the camera nudged after
