@@ -1,32 +1,41 @@
 """bench.py — Mray/s (primary+shadow) of the MI355X voxel ray-trace path.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config C1] [--no-cpu]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config C1] [--no-cpu] [--no-extra]
 
-A step = one frame of the C1 workload (BASELINE.json configs[1]): 1920x1080, 1024^3 world
-(monu3.vox tiled), 1 spp, Trace depth 0 = primary ray + one light sample
-with its shadow ray(s), accumulate + tonemap + RGB8: one vpx_render call (the wavefront
-kernels of DESIGN.md §4).  Inputs (world, tables, accumulator) are resident in HBM before
-timing.
+A step = one image of the workload: spp accumulated frames (C1-C3: 1, C4: 16), each one
+vpx_render call (primary rays, Trace(ray, max_bounces) flattened, the light samples with
+their shadow rays, running-average accumulate, tonemap, RGB8; the wavefront kernels of
+DESIGN.md §4).  The headline line is C1 (BASELINE.json configs[1]): 1920x1080, 1024^3 world
+(monu3.vox tiled), 1 spp, depth 0.  Inputs (world, tables, accumulator)
+are resident in HBM before timing.
 
-N > 1 (torchrun, one rank per GPU): weak scaling — the frame grows with N (N x 1920x1080
-pixels), its 16x16 tiles are dealt round-robin to ranks.  Default (--gather rgb8): each rank
-accumulates and tonemaps its own tiles (the accumulator is sharded with them) and an RCCL
-gather (torch.distributed, backend nccl) brings the packed RGB8 to rank 0's screen; the
-gather of frame f overlaps the render of frame f+1.  --gather samples: ranks send float4
-samples and rank 0 composites (unpack + accumulate + tonemap) into its full accumulator.
-Timed region: barrier + sync on both sides (the last frame's gather included), max over
-ranks.  value = all rays of all ranks / that time.
+N > 1 (torchrun, one rank per GPU): STRONG scaling — the configured frame (C1: 1920x1080
+at every N; C3/C4: 3840x2160) is cut into 16x16 tiles dealt round-robin to the ranks; each
+rank accumulates and tonemaps its own tiles (the accumulator is sharded with them) and an
+RCCL gather (torch.distributed, backend nccl) brings the packed RGB8 of the step's last
+frame to rank 0's screen, overlapped with the next step's renders.  Timed region: barrier
++ sync on both sides (the last gather included), max over ranks; value = all ranks' rays /
+that time.  Weak scaling (N x 1920x1080 pixels) is reported as the extra key
+`weak_scaling`.
 
-roofline: the dominant stage (largest device time in the last warmup frame, where every
-stage is timed): its algorithmic bytes per launch = DDA cells read x 1 B (the finish stage:
-W*H*36 B, accumulator float4 read+write + RGB8 write), SURVEY.md §8(d) / DESIGN.md §4,
-divided by its average launch duration measured with HIP events on the library's stream
-over the timed region (only that stage is timed there: each timed launch adds two event
-records to the stream).
-cpu_baseline: the CPU restatement (oracle/, C, -O2) on a bounded pixel sample of the same
-frame on this host's cores (rank 0, N = 1 only).
+Extra keys: `extra_configs` C2 / C3 / C4 (same N, their stated sizes, fewer steps), each
+with ms/step, Mray/s (primary+shadow), total Mray/s (incl. bounce rays) and its own
+dominant-stage roofline.
+
+roofline: the dominant stage (largest device time in the last warmup step, where every
+stage is timed): its algorithmic bytes per launch = DDA cells read x 1 B (+ W*H*36 B for
+the accumulate/tonemap work when the stage's kernel carries it), SURVEY.md §8(d) /
+DESIGN.md §4, divided by its average launch duration measured with HIP events on the
+library's stream over the timed region (only that stage is timed there).  traffic: HBM
+bytes per launch from the rocprofv3 PMC summary committed for THIS library build
+(profiles/*_pmc_traffic.json, matched by the library's sha256), else null.
+cpu_baseline (rank 0, N = 1): the CPU restatement (oracle/liboracle_perf.so, -O3
+x86-64-v3, bit-identical to the checker) on a bounded row sample of the C1 frame with every
+thread of the box's CPU share, plus BASELINE.md §3's C0 / C0' frames (640x360, 1 thread and
+all threads, median of 20 after 3 warm-ups).
 """
 import argparse
+import hashlib
 import json
 import math
 import os
@@ -42,6 +51,9 @@ import __graft_entry__ as entry  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 METRIC = "Mray/s (primary+shadow) at 1920×1080, 1024³ world; 1/2/4/8-GPU"
+EXTRA_CONFIGS = ("C2", "C3", "C4")
+STAGE_KERNELS = {"primary": "k_primary", "shade": "k_shade", "shadow": "k_shadow_tile", "resolve": "k_resolve",
+                 "bounce": "k_nearest_tile", "finish": "k_finish"}
 
 
 def weak_size(n, base=(1920, 1080)):
@@ -54,132 +66,99 @@ def weak_size(n, base=(1920, 1080)):
     return base[0] * a, base[1] * b
 
 
-def build_scene(pkg, cfg, width=None, height=None):
-    desc = pkg.scene.CONFIGS[cfg]()
-    if width and (width, height) != (desc.width, desc.height):
-        desc = desc.with_size(width, height)
-    return desc
+def lib_sha256(pkg):
+    path = os.environ.get("VPX_LIB") or pkg.abi.LIB_PATH
+    with open(path, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
 
 
-def cpu_baseline(pkg, desc, budget_s=12.0):
-    """Oracle timed on a bounded sample (whole rows, evenly spaced) of the same frame."""
-    orc = entry.load_oracle()
-    t0 = time.time()
-    o = orc.Oracle(pkg.abi, desc)
-    gen_s = time.time() - t0
-    threads = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
-    p = desc.frame_params(0)
-    W, H = desc.width, desc.height
-    # calibrate on 2 rows, then size the sample to ~budget_s
-    rows = np.array([H // 2, H // 3], np.int64)
-    ids = (rows[:, None] * W + np.arange(W)[None, :]).reshape(-1)
-    t = time.time()
-    _, st = o.render_pixels(p, ids, threads)
-    dt = max(time.time() - t, 1e-3)
-    per_row = dt / len(rows)
-    nrows = int(max(4, min(H, budget_s / per_row)))
-    rows = np.linspace(0, H - 1, nrows).astype(np.int64)
-    ids = (rows[:, None] * W + np.arange(W)[None, :]).reshape(-1)
-    t = time.time()
-    _, st = o.render_pixels(p, ids, threads)
-    dt = time.time() - t
-    rays = st.primary_rays + st.shadow_rays
-    return {"value": round(rays / dt / 1e6, 4), "unit": "Mray/s", "cores": threads, "kind": "port",
-            "sample": f"{nrows} evenly spaced rows of the {W}x{H} frame ({len(ids)} pixels, {rays} primary+shadow "
-                      f"rays, {dt:.1f} s); world generated on host in {gen_s:.1f} s"}
-
-
-STAGE_KERNELS = {"primary": "k_primary", "shade": "k_shade", "shadow": "k_shadow_tile", "resolve": "k_resolve",
-                 "bounce": "k_nearest_tile", "finish": "k_finish"}
-
-
-def pmc_traffic(kernel, config, W, H):
+def pmc_traffic(kernel, config, W, H, sha):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of this
-    workload (profiles/*_pmc_traffic.json, FETCH_SIZE x2 + WRITE_SIZE per the gfx950
-    correction); None when no summary for this exact workload exists."""
+    workload AND this library build (FETCH_SIZE x2 + WRITE_SIZE per the gfx950
+    correction); None when no summary for this exact build / workload exists."""
     import glob
     best = None
-    for f in sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "*_pmc_traffic.json"))):
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_traffic.json"))):
         try:
             d = json.load(open(f))
         except (OSError, ValueError):
             continue
-        if d.get("config") == config and d.get("width") == W and d.get("height") == H and kernel in d.get("kernels", {}):
+        if (d.get("config") == config and d.get("width") == W and d.get("height") == H
+                and d.get("lib_sha256") == sha and kernel in d.get("kernels", {})):
             best = d["kernels"][kernel]["hbm_bytes_per_launch"]
     return best
 
 
-def run(args):
-    pkg = entry.load_package()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    n = args.gpus
-    if world != n:
-        raise SystemExit(f"--gpus {n} but WORLD_SIZE={world}")
-    # VPX_BENCH_SHARED_DEVICE=1 rehearses the N-rank flow on ONE GPU (every rank on device 0,
-    # gloo collectives through host copies) — for checking the sharded path on a 1-GPU box;
-    # real multi-GPU runs use one GPU per rank and RCCL ("nccl").
-    shared = os.environ.get("VPX_BENCH_SHARED_DEVICE") == "1"
-    dev = 0 if shared else local
-    torch.cuda.set_device(dev)
-    dist = None
-    if n > 1:
-        import torch.distributed as dist
-        if shared:
-            dist.init_process_group("gloo")
-        else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
-    desc = pkg.scene.CONFIGS[args.config]()
-    W, H = weak_size(n, (desc.width, desc.height))
-    desc = build_scene(pkg, args.config, W, H)
-    stream = torch.cuda.Stream()  # a real stream: the kernel and its HIP events share it
-    torch.cuda.set_stream(stream)
-    ctx = pkg.context.Context(dev)
-    ctx.set_stream(stream.cuda_stream)
+class Env:
+    """Rank / device / process-group state of this bench process."""
+
+    def __init__(self, n):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.n = n
+        if self.world != n:
+            raise SystemExit(f"--gpus {n} but WORLD_SIZE={self.world}")
+        # VPX_BENCH_SHARED_DEVICE=1 rehearses the N-rank flow on ONE GPU (every rank on device 0,
+        # gloo collectives through host copies) — for checking the sharded path on a 1-GPU box;
+        # real multi-GPU runs use one GPU per rank and RCCL ("nccl").
+        self.shared = os.environ.get("VPX_BENCH_SHARED_DEVICE") == "1"
+        self.dev = 0 if self.shared else self.local
+        torch.cuda.set_device(self.dev)
+        self.dist = None
+        if n > 1:
+            import torch.distributed as dist
+            if self.shared:
+                dist.init_process_group("gloo")
+            else:
+                dist.init_process_group("nccl", device_id=torch.device("cuda", self.dev))
+            self.dist = dist
+        self.stream = torch.cuda.Stream()  # a real stream: the kernels and their HIP events share it
+        torch.cuda.set_stream(self.stream)
+
+    def parallelism(self):
+        if self.n == 1:
+            return "single GPU"
+        if self.shared:
+            return f"REHEARSAL: {self.n} ranks sharing one GPU, gloo gather via host"
+        return f"tile-shard x{self.n}, accumulator sharded, RCCL gather of RGB8 to rank 0 (overlapped)"
+
+
+def run_config(pkg, env, cfg, steps, warmup, weak=False, sha=None):
+    """Load `cfg` on this rank, run warmup + `steps` timed steps, return the result dict
+    (rank 0; None elsewhere).  Frees the world before returning."""
+    desc = pkg.scene.CONFIGS[cfg]()
+    if weak:
+        desc = desc.with_size(*weak_size(env.n, (desc.width, desc.height)))
+    W, H, spp = desc.width, desc.height, max(1, int(desc.spp))
+    ctx = pkg.context.Context(env.dev)
+    ctx.set_stream(env.stream.cuda_stream)
     ctx.load_scene(desc)
     torch.cuda.synchronize()
-    acc = torch.zeros(W * H * 4, dtype=torch.float32, device="cuda") if rank == 0 else None
-    rgb = torch.zeros(W * H, dtype=torch.int32, device="cuda") if rank == 0 else None
-    sharded = None
-    if n > 1 and args.gather == "rgb8":
-        sharded = pkg.dist.ShardedAccumFrame(ctx, desc, rank, n, torch.device("cuda", dev), host_gather=shared)
-    elif n > 1:
-        L = ctx.packed_len(W, H, n)
-        packed = torch.zeros(L * 4, dtype=torch.float32, device="cuda")
-        gbuf = torch.empty(n * L * 4, dtype=torch.float32, device="cuda") if rank == 0 else None
-        gathered = list(gbuf.view(n, L * 4)) if rank == 0 else None  # gather straight into gbuf
-
-    frame = [0]
+    acc = rgb = sharded = None
+    if env.n == 1:
+        acc = torch.zeros(W * H * 4, dtype=torch.float32, device="cuda")
+        rgb = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+    else:
+        sharded = pkg.dist.ShardedAccumFrame(ctx, desc, env.rank, env.n, torch.device("cuda", env.dev),
+                                             host_gather=env.shared)
 
     def step():
-        p = desc.frame_params(frame_index=frame[0])
-        if n == 1:
-            ctx.render(p, acc.data_ptr(), rgb.data_ptr())
-        elif sharded is not None:
-            sharded.frame = frame[0]
-            sharded.step()
-        else:
-            ctx.render_tiles(p, rank, n, packed.data_ptr())
-            if shared:
-                stream.synchronize()
-                parts = [torch.empty(L * 4) for _ in range(n)] if rank == 0 else None
-                dist.gather(packed.cpu(), parts, dst=0)
-                if rank == 0:
-                    gbuf.copy_(torch.cat(parts))
+        for f in range(spp):  # accumulation window: w = 1/(f+1), per-frame seeds (renderer.cpp:1791-1828)
+            if sharded is None:
+                ctx.render(desc.frame_params(frame_index=f), acc.data_ptr(), rgb.data_ptr())
             else:
-                dist.gather(packed, gathered, dst=0)
-            if rank == 0:
-                ctx.composite_tiles(p, n, gbuf.data_ptr(), acc.data_ptr(), rgb.data_ptr())
-        frame[0] += 1
+                sharded.render(f)
+        if sharded is not None:
+            sharded.publish()
 
-    launches = 4 * (desc.max_bounces + 1) + 4  # stage launches per frame, upper bound
-    # the last warmup frame times every stage (HIP events on the library's stream): the stage split
-    # and the dominant stage; the timed region then times only that stage, since every
+    launches = spp * (4 * (desc.max_bounces + 1) + 4)  # stage launches per step, upper bound
+    # the last warmup step times every stage (HIP events on the library's stream): the stage
+    # split and the dominant stage; the timed region then times only that stage, since every
     # timed launch adds two event records to the stream (all five C1 stages: +4.3 %)
     ctx.profile_select(None)
-    for i in range(args.warmup):
-        if i == args.warmup - 1:  # the last warmup frame (the first ones carry cold-start costs)
+    for i in range(warmup):
+        if i == warmup - 1:  # the last warmup step (the first ones carry cold-start costs)
             if sharded is not None:
                 sharded.flush()
             torch.cuda.synchronize()
@@ -190,95 +169,166 @@ def run(args):
         sharded.flush()
     torch.cuda.synchronize()
     warm = ctx.profile_read(reset=True)
-    timed_stages = [max(warm, key=lambda k: warm[k][0])] if args.warmup > 0 else None
+    timed_stages = [max(warm, key=lambda k: warm[k][0])] if warmup > 0 else None
     ctx.counters(reset=True)
     ctx.profile_select(timed_stages)
-    ctx.profile_enable(args.steps * launches)
+    ctx.profile_enable(steps * launches)
     ctx.profile_read(reset=True)
-    if dist:
-        dist.barrier()
+    if env.dist:
+        env.dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         step()
     if sharded is not None:
-        sharded.flush()  # the last frame's gather + scatter belong to the timed region
+        sharded.flush()  # the last step's gather + scatter belong to the timed region
     torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
+    if env.dist:
+        env.dist.barrier()
     elapsed = time.perf_counter() - t0
     st = ctx.counters()
-    local_rays = float(st.primary_rays + st.shadow_rays)
-    vals = torch.tensor([elapsed, local_rays, float(st.primary_rays), float(st.shadow_rays), float(st.dda_cells)],
-                        dtype=torch.float64, device="cpu" if shared else "cuda")
-    if dist:
-        mx = vals.clone()
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        sm = vals.clone()
-        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+    vals = torch.tensor([elapsed, float(st.primary_rays), float(st.shadow_rays), float(st.bounce_rays),
+                         float(st.dda_cells)], dtype=torch.float64, device="cpu" if env.shared else "cuda")
+    if env.dist:
+        mx, sm = vals.clone(), vals.clone()
+        env.dist.all_reduce(mx, op=env.dist.ReduceOp.MAX)
+        env.dist.all_reduce(sm, op=env.dist.ReduceOp.SUM)
         elapsed = mx[0].item()
-        rays, prim, shad, cells = sm[1].item(), sm[2].item(), sm[3].item(), sm[4].item()
+        prim, shad, bounce, cells = (sm[i].item() for i in range(1, 5))
     else:
-        rays, prim, shad, cells = local_rays, float(st.primary_rays), float(st.shadow_rays), float(st.dda_cells)
-    if rank == 0:
-        K = args.steps
+        prim, shad, bounce, cells = float(st.primary_rays), float(st.shadow_rays), float(st.bounce_rays), \
+            float(st.dda_cells)
+    out = None
+    if env.rank == 0:
+        K = steps
         ms_step = elapsed * 1000.0 / K
-        value = rays / elapsed / 1e6
-        # roofline of the dominant kernel: the stage with the largest device time in the
-        # timed region, its algorithmic bytes per launch (1 B per DDA cell
-        # read; 36 B per pixel for the accumulate/tonemap stage) over its average launch time
         prof = ctx.profile_read()
         dom = max(prof, key=lambda k: prof[k][0])
         dom_ms, dom_launches, dom_cells = prof[dom]
         split = warm if timed_stages else prof
         kernel_ms = dom_ms / max(dom_launches, 1)
         # the library runs the last level's shadow -> resolve -> finish as one launch
-        # (k_shadow_finish) unless built with VPX_FUSE_TAIL=0: then there is
-        # no separate finish stage, and the shadow stage carries the 36 B per pixel
+        # (k_shadow_finish) unless built with VPX_FUSE_TAIL=0: then there is no
+        # separate finish stage, and the shadow stage carries the 36 B per pixel
         fused = "finish" not in split
         kernels = dict(STAGE_KERNELS)
         if fused:
             kernels["shadow"] = "k_shadow_finish" if desc.max_bounces == 0 else "k_shadow_tile+k_shadow_finish"
+        # rank 0's own work (its launches, cells and pixels)
+        local_pix = float(st.primary_rays)
         if dom == "finish":
-            alg_bytes = float(st.primary_rays) / K * 36.0
+            alg_bytes = local_pix / K / spp * 36.0
         else:
             alg_bytes = float(dom_cells) / max(dom_launches, 1)
             if dom == "shadow" and fused:
-                alg_bytes += float(st.primary_rays) * 36.0 / max(dom_launches, 1)
+                alg_bytes += local_pix * 36.0 / max(dom_launches, 1)
         achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
-        frame_bytes = float(st.dda_cells) / K + float(st.primary_rays) / K * 36.0
-        traffic = pmc_traffic(kernels[dom], args.config, W, H)
+        frame_bytes = (cells + prim * 36.0) / K
+        traffic = pmc_traffic(kernels[dom], cfg, W, H, sha) if env.n == 1 else None
         out = {
-            "metric": METRIC, "value": round(value, 3), "unit": "Mray/s", "n_gpus": n, "steps": K,
-            "warmup": args.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-            "data": f"synthetic world '{desc.name}': the reference's .vox asset decoded like ogt_vox, placed in a "
-                    f"{desc.grids[0].n}^3 u8 grid on device; fixed lights/camera (SURVEY.md §8(d))",
-            "config": {"workload": f"{args.config}: {W}x{H}, {desc.grids[0].n}^3 {desc.name}, 1 spp, "
-                                   f"Trace depth {desc.max_bounces} (primary+shadow)",
-                       "width": W, "height": H, "world_n": desc.grids[0].n, "max_bounces": desc.max_bounces,
-                       "spp": 1, "parallelism": "single GPU" if n == 1 else (
-                           (f"tile-shard x{n}, accumulator sharded, RCCL gather of RGB8 to rank 0 (overlapped)"
-                            if args.gather == "rgb8" else f"tile-shard x{n} + RCCL gather of samples to rank 0")
-                           if not shared else f"REHEARSAL: {n} ranks sharing one GPU, gloo gather via host")},
-            "rays_per_step": {"primary": prim / K, "shadow": shad / K, "dda_cells": cells / K},
+            "config": cfg, "value": round((prim + shad) / elapsed / 1e6, 3), "ms_per_step": round(ms_step, 4),
+            "total_mray_s": round((prim + shad + bounce) / elapsed / 1e6, 3),
+            "workload": f"{cfg}: {W}x{H}, {desc.grids[0].n}^3 {desc.name}, {spp} spp, Trace depth {desc.max_bounces}"
+                        + (f", {len(desc.volumes)} volumes" if len(desc.volumes) > 1 else "")
+                        + (f", {len(desc.areas)} area lights x {desc.area_samples} samples" if desc.areas else ""),
+            "width": W, "height": H, "world_n": desc.grids[0].n, "max_bounces": desc.max_bounces, "spp": spp,
+            "rays_per_step": {"primary": prim / K, "shadow": shad / K, "bounce": bounce / K, "dda_cells": cells / K},
             "mpix_per_s": round(prim / elapsed / 1e6, 3),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                         "traffic_source": ("profiles/*_pmc_traffic.json for this library build (sha256 match)"
+                                            if traffic is not None else
+                                            "null: no PMC pass committed for this library build / workload"),
                          "kernel": kernels[dom], "kernel_ms": round(kernel_ms, 4),
                          "alg_bytes_per_launch": round(alg_bytes),
                          "stages_ms": {k: round(v[0] / max(v[1], 1), 4) for k, v in split.items() if v[1]},
-                         "stages_ms_from": "last warmup frame, every stage timed" if timed_stages else "timed region",
+                         "stages_ms_from": "last warmup step, every stage timed" if timed_stages else "timed region",
                          "frame_alg_bytes": round(frame_bytes),
                          "frame_achieved": round(frame_bytes / (ms_step * 1e-3) / 1e9, 2)},
-            "cpu_baseline": None,
         }
-        if n == 1 and not args.no_cpu:
-            out["cpu_baseline"] = cpu_baseline(pkg, desc, args.cpu_budget)
-        print(json.dumps(out), flush=True)
+    del acc, rgb, sharded
     ctx.close()
-    if dist:
-        dist.destroy_process_group()
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return out
+
+
+# ------------------------------------------------------------------ CPU baseline
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_threads():
+    """Threads the box gives this job: OMP_NUM_THREADS (16 per GPU on the pool), else the
+    affinity mask."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return int(env)
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
+def time_frames(o, desc, threads, warm=3, frames=20):
+    """Median over `frames` whole-frame oracle renders after `warm` warm-ups."""
+    p = desc.frame_params(0)
+    acc = np.zeros((desc.width * desc.height, 4), np.float32)
+    ts, st = [], None
+    for i in range(warm + frames):
+        t = time.perf_counter()
+        _, _, st = o.render(p, accum=acc, threads=threads)
+        if i >= warm:
+            ts.append(time.perf_counter() - t)
+    med = float(np.median(ts))
+    rays = st.primary_rays + st.shadow_rays
+    return {"ms_median": round(med * 1e3, 3), "ms_min": round(min(ts) * 1e3, 3), "ms_max": round(max(ts) * 1e3, 3),
+            "mray_s": round(rays / med / 1e6, 4), "mpix_s": round(st.primary_rays / med / 1e6, 4),
+            "rays_per_frame": {"primary": st.primary_rays, "shadow": st.shadow_rays}}
+
+
+def cpu_baseline(pkg, desc, budget_s=12.0):
+    """The oracle (perf build) on the host: C1 row sample (value) + C0 / C0' frames."""
+    orc = entry.load_oracle()
+    threads = cpu_threads()
+    t0 = time.time()
+    o = orc.Oracle(pkg.abi, desc, perf=True)
+    gen_s = time.time() - t0
+    p = desc.frame_params(0)
+    W, H = desc.width, desc.height
+    rows = np.array([H // 2, H // 3], np.int64)  # calibrate on 2 rows, then size the sample to ~budget_s
+    ids = (rows[:, None] * W + np.arange(W)[None, :]).reshape(-1)
+    t = time.time()
+    o.render_pixels(p, ids, threads)
+    per_row = max(time.time() - t, 1e-3) / len(rows)
+    nrows = int(max(4, min(H, budget_s / 3 / per_row)))
+    rows = np.linspace(0, H - 1, nrows).astype(np.int64)
+    ids = (rows[:, None] * W + np.arange(W)[None, :]).reshape(-1)
+    runs = []
+    for _ in range(3):  # three passes over the same sample: median and spread
+        t = time.time()
+        _, st = o.render_pixels(p, ids, threads)
+        runs.append((st.primary_rays + st.shadow_rays) / (time.time() - t) / 1e6)
+    del o
+    out = {"value": round(float(np.median(runs)), 4), "unit": "Mray/s", "cores": threads, "kind": "port",
+           "sample": f"{nrows} evenly spaced rows of the {W}x{H} C1 frame ({len(ids)} pixels, "
+                     f"{st.primary_rays + st.shadow_rays} primary+shadow rays per pass), median of 3 passes "
+                     f"(min {min(runs):.3f}, max {max(runs):.3f} Mray/s); world generated on host in {gen_s:.1f} s",
+           "cpu_model": cpu_model(), "machine_logical_cpus": os.cpu_count(),
+           "threads_note": "cores = threads used = the box's CPU share (OMP_NUM_THREADS); std::thread pixel pool",
+           "build": "oracle/liboracle_perf.so: gcc -O3 -march=x86-64-v3 -ffp-contract=off, FTZ/DAZ"}
+    for key, cfg in (("c0", "C0"), ("c0_prime", "C0m")):  # BASELINE.md §3: 640x360, 1 spp, depth 0
+        d = pkg.scene.CONFIGS[cfg]()
+        oc = orc.Oracle(pkg.abi, d, perf=True)
+        out[key] = {"workload": f"{d.width}x{d.height}, {d.grids[0].n}^3 {d.name}, 1 spp, depth 0",
+                    "threads_1": time_frames(oc, d, 1), f"threads_{threads}": time_frames(oc, d, threads)}
+    return out
 
 
 def main():
@@ -288,10 +338,43 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="C1")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-extra", action="store_true", help="skip extra_configs / weak_scaling")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
-    ap.add_argument("--gather", choices=("rgb8", "samples"), default="rgb8",
-                    help="N>1: sharded accumulator + RGB8 gather (default) or float4 samples to rank 0")
-    run(ap.parse_args())
+    args = ap.parse_args()
+    pkg = entry.load_package()
+    env = Env(args.gpus)
+    sha = lib_sha256(pkg)
+    head = run_config(pkg, env, args.config, args.steps, args.warmup, sha=sha)
+    extra, weak = {}, None
+    if not args.no_extra:
+        xs = max(3, args.steps // 4)
+        for cfg in EXTRA_CONFIGS:
+            if cfg != args.config:
+                r = run_config(pkg, env, cfg, xs, min(args.warmup, 2), sha=sha)
+                if r is not None:
+                    extra[cfg] = r
+        if env.n > 1:
+            weak = run_config(pkg, env, args.config, xs, min(args.warmup, 2), weak=True, sha=sha)
+    if env.rank == 0:
+        out = {"metric": METRIC, "value": head["value"], "unit": "Mray/s", "n_gpus": env.n, "steps": args.steps,
+               "warmup": args.warmup, "ms_per_step": head["ms_per_step"], "higher_is_better": True,
+               "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+               "data": "synthetic worlds: the reference's .vox assets decoded like ogt_vox and tiled into the "
+                       "build-defined 1024^3 / 2048^3 u8 grids on device; fixed lights/camera (SURVEY.md §8(d))",
+               "config": {"workload": head["workload"], "width": head["width"], "height": head["height"],
+                          "world_n": head["world_n"], "max_bounces": head["max_bounces"], "spp": head["spp"],
+                          "parallelism": env.parallelism(), "lib_sha256": sha},
+               "rays_per_step": head["rays_per_step"], "mpix_per_s": head["mpix_per_s"],
+               "total_mray_s": head["total_mray_s"], "roofline": head["roofline"], "cpu_baseline": None}
+        if extra:
+            out["extra_configs"] = extra
+        if weak is not None:
+            out["weak_scaling"] = weak
+        if env.n == 1 and not args.no_cpu:
+            out["cpu_baseline"] = cpu_baseline(pkg, pkg.scene.CONFIGS[args.config](), args.cpu_budget)
+        print(json.dumps(out), flush=True)
+    if env.dist:
+        env.dist.destroy_process_group()
 
 
 if __name__ == "__main__":

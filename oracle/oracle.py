@@ -12,16 +12,24 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "liboracle.so")
+# the same source built -O3 -march=x86-64-v3 (AVX2/FMA/BMI2: the reference's /arch:AVX2) with
+# -ffp-contract=off, so bit-identical results (tests/test_cpu_oracle.py); bench.py's
+# cpu_baseline times this build
+PERF_LIB_PATH = os.path.join(HERE, "liboracle_perf.so")
+_LIBS = {}
 
 
-def build():
-    subprocess.run(["make", "-s", "-C", HERE, "liboracle.so"], check=True)
+def build(target="liboracle.so"):
+    subprocess.run(["make", "-s", "-C", HERE, target], check=True)
 
 
-def _lib(abi):
-    if not os.path.exists(LIB_PATH):
-        build()
-    lib = C.CDLL(LIB_PATH)
+def _lib(abi, perf=False):
+    path = PERF_LIB_PATH if perf else LIB_PATH
+    if path in _LIBS:
+        return _LIBS[path]
+    if not os.path.exists(path):
+        build(os.path.basename(path))
+    lib = C.CDLL(path)
     P = C.POINTER
     lib.oracle_find_nearest.argtypes = [C.c_void_p, P(abi.Ray), C.c_uint32, P(abi.Hit)]
     lib.oracle_is_occluded.argtypes = [C.c_void_p, P(abi.Ray), C.c_uint32, C.c_void_p, C.c_void_p]
@@ -69,6 +77,7 @@ def _lib(abi):
     lib.oracle_bvh_intersect.argtypes = [P(abi.BvhNode), P(abi.BvhTri), P(C.c_uint32), P(abi.Ray), C.c_uint32,
                                          P(C.c_float)]
     lib.oracle_bvh_intersect.restype = C.c_int
+    _LIBS[path] = lib
     return lib
 
 
@@ -123,9 +132,9 @@ def _scene_struct(abi):
 class Oracle:
     """CPU restatement bound to one SceneDesc (grids materialised on the host)."""
 
-    def __init__(self, abi, desc, grid_cells=None):
+    def __init__(self, abi, desc, grid_cells=None, perf=False):
         self.abi = abi
-        self.lib = _lib(abi)
+        self.lib = _lib(abi, perf)
         self.desc = desc
         self._keep = []
         cells = grid_cells if grid_cells is not None else [self.host_grid(g) for g in desc.grids]

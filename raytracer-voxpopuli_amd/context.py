@@ -16,6 +16,7 @@ class Context:
         self.h = h
         self.device = device
         self.scene = None
+        self.stream_handle = None
 
     # ------------------------------------------------------------------ lifetime
     def close(self):
@@ -40,6 +41,7 @@ class Context:
 
     def set_stream(self, stream_handle):
         self._chk(self.lib.vpx_set_stream(self.h, C.c_void_p(stream_handle or 0)), "vpx_set_stream")
+        self.stream_handle = stream_handle or None  # None: the context's own stream
 
     def synchronize(self):
         self._chk(self.lib.vpx_synchronize(self.h), "vpx_synchronize")

@@ -139,13 +139,26 @@ class ShardedFrame:
 class ShardedAccumFrame:
     """One rank's share with the accumulator sharded (see the module docstring).  GPU
     path: libvpx_hip.so + RCCL; `host_gather=True` routes the gather through host memory
-    (gloo), for rehearsing N ranks on one GPU."""
+    (gloo), for rehearsing N ranks on one GPU.
+
+    `render(frame)` accumulates one frame of this rank's tiles; `publish()` starts the
+    gather of the RGB8 of the last rendered frame to rank 0 (and completes the previous
+    publish, whose gather overlapped the renders since).  An accumulation window of spp
+    frames (C4: 16) renders spp times and publishes once; `step()` = one frame + publish.
+
+    The library must launch on torch's current stream: RCCL orders the gather after the
+    work queued on that stream, and `work.wait()` orders later renders after the gather."""
 
     def __init__(self, ctx, desc, rank, n_ranks, device, host_gather=False):
         import torch
 
         self.ctx, self.desc, self.rank, self.n = ctx, desc, rank, n_ranks
         self.host = host_gather
+        if not host_gather:
+            cur = torch.cuda.current_stream(device).cuda_stream
+            if ctx.stream_handle != cur:
+                raise ValueError("ShardedAccumFrame: the vpx context must render on torch's current stream "
+                                 "(ctx.set_stream(torch.cuda.current_stream().cuda_stream))")
         w, h = desc.width, desc.height
         self.L = ctx.packed_len(w, h, n_ranks)
         assert self.L == packed_len(w, h, n_ranks)
@@ -157,6 +170,8 @@ class ShardedAccumFrame:
             self.screen = torch.zeros(w * h, dtype=torch.int32, device=device)
         self.pending = None  # (work, buffer, params) of the frame whose gather is in flight
         self.frame = 0
+        self.buf = 0         # RGB8 buffer the renders write (the other one may be in flight)
+        self.last = None     # params of the last rendered frame
 
     def _finish(self):
         work, b, p = self.pending
@@ -166,17 +181,23 @@ class ShardedAccumFrame:
         if self.rank == 0:
             self.ctx.composite_rgb8(p, self.n, self.gathered[b].data_ptr(), self.screen.data_ptr())
 
-    def step(self):
+    def render(self, frame=None):
+        f = self.frame if frame is None else frame
+        p = self.desc.frame_params(frame_index=f)
+        self.ctx.render_tiles_accum(p, self.rank, self.n, self.accum.data_ptr(), self.rgb[self.buf].data_ptr())
+        self.last = p
+        self.frame = f + 1
+
+    def publish(self):
         import torch
         import torch.distributed as dist
 
-        p = self.desc.frame_params(frame_index=self.frame)
-        b = self.frame & 1
-        self.ctx.render_tiles_accum(p, self.rank, self.n, self.accum.data_ptr(), self.rgb[b].data_ptr())
+        b, p = self.buf, self.last
         if self.pending is not None:
-            self._finish()  # frame f-1: its gather overlapped this render
+            self._finish()  # the previous publish: its gather overlapped the renders since
         if self.host:
-            torch.cuda.current_stream().synchronize()
+            if self.rgb[b].is_cuda:
+                torch.cuda.current_stream().synchronize()
             parts = [torch.empty(self.L, dtype=torch.int32) for _ in range(self.n)] if self.rank == 0 else None
             dist.gather(self.rgb[b].cpu(), parts, dst=0)
             if self.rank == 0:
@@ -185,9 +206,13 @@ class ShardedAccumFrame:
         else:
             self.pending = (gather_async(self.rgb[b], self.rank, self.n, self.parts[b] if self.rank == 0 else None),
                             b, p)
-        self.frame += 1
+        self.buf ^= 1
+
+    def step(self):
+        self.render()
+        self.publish()
 
     def flush(self):
-        """Complete the last frame (its gather and rank 0's scatter)."""
+        """Complete the last publish (its gather and rank 0's scatter)."""
         if self.pending is not None:
             self._finish()

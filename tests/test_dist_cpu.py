@@ -5,6 +5,7 @@ GPUs): each rank produces its packed tile buffer — here from the CPU checker s
 for vpx_render_tiles — the buffers are gathered to rank 0, unpacked and compared with the
 monolithic frame bit for bit.
 """
+import ctypes as C
 import os
 import socket
 import sys
@@ -89,6 +90,83 @@ def _worker_rgb8(rank, world, port, w, h, q):
         dist.barrier()
     finally:
         dist.destroy_process_group()
+
+
+class _OracleTileCtx:
+    """Stands in for the vpx context on CPU: vpx_render_tiles_accum / vpx_composite_rgb8
+    with the oracle's samples, written through the same raw pointers."""
+
+    def __init__(self, pkg, orc, desc):
+        self.pkg, self.desc = pkg, desc
+        self.o = orc.Oracle(pkg.abi, desc)
+        self.stream_handle = None
+
+    def packed_len(self, w, h, n):
+        return self.pkg.dist.packed_len(w, h, n)
+
+    def render_tiles_accum(self, p, rank, n, acc_ptr, rgb_ptr):
+        w, h = self.desc.width, self.desc.height
+        ids = self.pkg.dist.rank_pixel_ids(w, h, rank, n)
+        L = ids.size
+        acc = np.ctypeslib.as_array((C.c_float * (4 * L)).from_address(acc_ptr)).reshape(L, 4)
+        rgb = np.ctypeslib.as_array((C.c_uint32 * L).from_address(rgb_ptr))
+        ok = ids >= 0
+        sample, _ = self.o.render_pixels(p, ids[ok].astype(np.uint32), threads=2)
+        a = np.ascontiguousarray(acc[ok])
+        r = np.zeros(int(ok.sum()), np.uint32)
+        for k in range(len(r)):
+            self.o.lib.oracle_accumulate_tonemap(sample[k].ctypes.data, p.frame_index, a[k].ctypes.data,
+                                                 r[k:k + 1].ctypes.data)
+        acc[ok] = a
+        rgb[ok] = r
+
+    def composite_rgb8(self, p, n, gathered_ptr, screen_ptr):
+        w, h = self.desc.width, self.desc.height
+        L = self.pkg.dist.packed_len(w, h, n)
+        g = np.ctypeslib.as_array((C.c_uint32 * (n * L)).from_address(gathered_ptr))
+        scr = np.ctypeslib.as_array((C.c_uint32 * (w * h)).from_address(screen_ptr))
+        scr[:] = self.pkg.dist.unpack_u32(g, w, h, n)
+
+
+def _worker_window(rank, world, port, w, h, spp, q):
+    """dist.ShardedAccumFrame itself (host gather over gloo): two accumulation windows of
+    `spp` frames each, one publish per window (bench.py's C4 step); rank 0's screen after
+    each flush equals the oracle's whole-frame RGB8 after frame spp - 1."""
+    sys.path.insert(0, REPO)
+    import __graft_entry__ as entry
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        pkg, orc = entry.load_package(), entry.load_oracle()
+        desc = pkg.scene.model_scene("monu3", 64, w, h, 1, city_lights=True)
+        desc.flags = pkg.abi.VPX_FLAG_AA
+        fr = pkg.dist.ShardedAccumFrame(_OracleTileCtx(pkg, orc, desc), desc, rank, world, torch.device("cpu"),
+                                        host_gather=True)
+        ok = True
+        acc = None
+        for f in range(spp):
+            acc, want, _ = orc.Oracle(pkg.abi, desc).render(desc.frame_params(f), accum=acc, threads=2)
+        for _ in range(2):
+            for f in range(spp):
+                fr.render(f)
+            fr.publish()
+            fr.flush()
+            if rank == 0:
+                ok &= bool(np.array_equal(fr.screen.numpy().view(np.uint32), want))
+        if rank == 0:
+            q.put(ok)
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_accum_frame_spp_window_two_ranks_gloo():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    mp.start_processes(_worker_window, args=(2, port, 40, 24, 3, q), nprocs=2, join=True, start_method="spawn")
+    assert q.get(timeout=60) is True
 
 
 def test_sharded_accumulator_rgb8_gather_two_ranks_gloo():

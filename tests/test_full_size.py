@@ -3,8 +3,8 @@
 The oracle cannot render these frames in seconds, so each test checks size-independent
 properties instead: the 1 GiB / 8 GiB device world equals the host generator (checksum of
 every byte), and a seeded sample of pixels of the full-size GPU frame equals the oracle's
-samples for the same pixels bit for bit (accumulator floats after frame 0 = the sample,
-and the RGB8 bytes).  Worlds are generated on the host too (up to 8 GiB), so these run
+samples for the same pixels bit for bit (accumulator floats after the config's last
+accumulated frame — C4: 16 spp — and the RGB8 bytes).  Worlds are generated on the host too (up to 8 GiB), so these run
 one config at a time and free everything afterwards.
 """
 import gc
@@ -34,9 +34,11 @@ def sample_ids(W, H, seed):
 def test_full_size_config_sampled(pkg, orc, cfg):
     desc = pkg.scene.CONFIGS[cfg]()
     W, H = desc.width, desc.height
+    spp = max(1, desc.spp)  # C4: 16 accumulated frames (w = 1/(n+1), renderer.cpp:1791-1828)
     r = pkg.renderer.Renderer(desc, 0)
     r.Init()
-    st = r.Tick(0.0, stats=True)
+    for _ in range(spp):
+        st = r.Tick(0.0, stats=True)
     torch.cuda.synchronize()
     acc = r.accumulator.view(-1, 4)
     ids = sample_ids(W, H, sum(map(ord, cfg)))
@@ -51,13 +53,18 @@ def test_full_size_config_sampled(pkg, orc, cfg):
     o = orc.Oracle(pkg.abi, desc)
     for i, c in enumerate(o.cells):  # the whole device world, byte for byte (checksum)
         assert sums[i] == o.lib.oracle_grid_checksum(c.ctypes.data, c.size), f"grid {i}"
-    sample, ost = o.render_pixels(desc.frame_params(0), ids)
-    assert np.array_equal(bits(acc_g), bits(sample)), f"{cfg}: accumulator mismatch"
     rgb_o = np.zeros(len(ids), np.uint32)
     acc_o = np.zeros((len(ids), 4), np.float32)
-    for k in range(len(ids)):
-        o.lib.oracle_accumulate_tonemap(sample[k].ctypes.data, 0, acc_o[k].ctypes.data, rgb_o[k:k + 1].ctypes.data)
+    for f in range(spp):
+        sample, ost = o.render_pixels(desc.frame_params(f), ids)
+        for k in range(len(ids)):
+            o.lib.oracle_accumulate_tonemap(sample[k].ctypes.data, f, acc_o[k].ctypes.data, rgb_o[k:k + 1].ctypes.data)
+    assert np.array_equal(bits(acc_g), bits(acc_o)), f"{cfg}: accumulator mismatch after {spp} frames"
     assert np.array_equal(rgb_g, rgb_o), f"{cfg}: RGB8 mismatch"
     assert st.primary_rays == W * H
+    # the last frame's shadow rays over the whole frame vs the sample's rate: a loose
+    # size-independent check that the device cast light samples like the oracle
+    rate_g, rate_o = st.shadow_rays / (W * H), ost.shadow_rays / len(ids)
+    assert st.shadow_rays > 0 and abs(rate_g - rate_o) <= 0.1 * max(rate_o, 0.5), (rate_g, rate_o)
     del o
     gc.collect()

@@ -227,6 +227,20 @@ def test_sharded_accumulator_equals_monolithic(pkg, orc):
     ctx.close()
 
 
+def test_sharded_accum_frame_refuses_a_foreign_stream(pkg):
+    """RCCL orders the gather after torch's current stream, so the sharded flow refuses a
+    context that renders on another stream instead of gathering stale RGB8."""
+    desc = pkg.scene.city_scene("monu3", 128, 64, 48, 0)
+    ctx = make_ctx(pkg, desc)  # the context's own stream
+    with pytest.raises(ValueError):
+        pkg.dist.ShardedAccumFrame(ctx, desc, 0, 2, torch.device("cuda", 0))
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        ctx.set_stream(s.cuda_stream)
+        pkg.dist.ShardedAccumFrame(ctx, desc, 0, 2, torch.device("cuda", 0))
+    ctx.close()
+
+
 def test_tiled_world_generator_matches_oracle(pkg, orc):
     for model, n in (("monu3", 256), ("roomGlass", 320)):
         spec, _, _ = pkg.scene.tiled_grid(model, n)

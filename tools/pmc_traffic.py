@@ -26,7 +26,11 @@ for k, d in vals.items():
     write = sum(d["WRITE_SIZE"]) / len(d["WRITE_SIZE"])
     kernels[k] = {"fetch_kib": round(fetch, 1), "write_kib": round(write, 1), "launches_sampled": len(d["FETCH_SIZE"]),
                   "hbm_bytes_per_launch": round((2.0 * fetch + write) * 1024.0)}
-json.dump({"config": config, "width": W, "height": H, "source": root,
+import os
+sha = None
+if os.path.exists(f"{root}/lib.sha256"):  # written on the GPU box by tools/gpu_pmc.sh
+    sha = open(f"{root}/lib.sha256").read().split()[0]
+json.dump({"config": config, "width": W, "height": H, "source": root, "lib_sha256": sha,
            "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes over bench.py; "
                      "bytes = (2 x FETCH_SIZE + WRITE_SIZE) KiB x 1024 per launch (gfx950 FETCH_SIZE correction)",
            "kernels": kernels}, open(out, "w"), indent=1)
