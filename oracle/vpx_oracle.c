@@ -600,6 +600,46 @@ static int tri_is_hit(const vpx_triangle* tr, const ray_t* r)
     return 1;
 }
 
+/* ------------------------------------------------- the reference's x86 approximations -- */
+/* Off by default (the build's decision: exact 1/x and 1/sqrtf).  On,
+   the restatement uses the reference's own operations where it uses them:
+   FastReciprocal (rcpps + one Newton step, renderer.cpp:929-934) for the object-space rD of
+   Renderer::FindNearest (:969), and normalize(__m128) = v * rsqrtps(dpps(v, v, 0x7F))
+   (tmpl8math.h:2356-2360) for the primary direction of Renderer::Update (:1735-1765, rD
+   from the unnormalised D, :1734).  rcpps / rsqrtps are approximations whose bits differ
+   between CPU vendors: results hold for the CPU this runs on.  Used only to measure how far
+   the exact decision moves the image (tests/test_cpu_oracle.py). */
+static int g_x86_approx = 0;
+int oracle_set_x86_approx(int on)
+{
+#ifdef ORACLE_X86
+    g_x86_approx = on != 0;
+    return 0;
+#else
+    return on ? -1 : 0;
+#endif
+}
+#ifdef ORACLE_X86
+static inline float rcp_approx(float x) { return _mm_cvtss_f32(_mm_rcp_ss(_mm_set_ss(x))); }
+static inline float rsqrt_approx(float x) { return _mm_cvtss_f32(_mm_rsqrt_ss(_mm_set_ss(x))); }
+static inline float fast_reciprocal1(float x)
+{
+    const float r = rcp_approx(x);
+    const float muls = x * (r * r);
+    return (r + r) - muls;
+}
+static v3 fast_reciprocal(v3 d) { return V3(fast_reciprocal1(d.x), fast_reciprocal1(d.y), fast_reciprocal1(d.z)); }
+/* primary ray of the AVX loop: rD = SlowReciprocal(D), D = normalize(D) (rsqrtps), Dsign */
+static void primary_rsqrt(ray_t* r, v3 dir)
+{
+    const float dp = (dir.x * dir.x + dir.y * dir.y) + dir.z * dir.z; /* dpps 0x7F */
+    const float inv = rsqrt_approx(dp);
+    r->rD = V3(1.0f / dir.x, 1.0f / dir.y, 1.0f / dir.z);
+    r->D = V3(dir.x * inv, dir.y * inv, dir.z * inv);
+    r->Dsign = compute_dsign(r->D);
+}
+#endif
+
 /* ------------------------------------------------------------- renderer level -- */
 /* Renderer::FindNearest, renderer.cpp:946-1018 */
 static int32_t renderer_find_nearest(tctx* c, ray_t* r)
@@ -613,6 +653,9 @@ static int32_t renderer_find_nearest(tctx* c, ray_t* r)
         r->O = xform_pos_ssem(backup.O, inv);
         r->D = xform_vec_ssem(backup.D, inv);
         r->rD = V3(1.0f / r->D.x, 1.0f / r->D.y, 1.0f / r->D.z); /* FastReciprocal -> exact */
+#ifdef ORACLE_X86
+        if (g_x86_approx) r->rD = fast_reciprocal(r->D);
+#endif
         r->Dsign = compute_dsign(r->D);
         if (scene_find_nearest(c, &sc->volumes[i], r)) vox = (int32_t)i;
         r->O = backup.O, r->D = backup.D, r->rD = backup.rD, r->Dsign = backup.Dsign;
@@ -993,6 +1036,68 @@ static void tctx_init(tctx* c, const oracle_scene* sc)
     c->area_samples = 3;
 }
 
+/* ------------------------------------------------------------ known-answer hooks -- */
+/* Single reference functions evaluated on given inputs, for the hand-derived known-answer
+   tests (tests/test_kat_reference.py).  Ray built with the Ray ctor (normalised D, Dsign). */
+int oracle_kat_normal(const float o[3], const float d[3], float t, uint32_t n, const float m[16], float out[3])
+{
+    const fpstate fs = fp_enter();
+    ray_t r = make_ray(v3f(o), v3f(d));
+    r.t = t;
+    const v3 v = normal_voxel(&r, n, m);
+    out[0] = v.x, out[1] = v.y, out[2] = v.z;
+    fp_leave(fs);
+    return VPX_OK;
+}
+
+/* One light evaluator (kind 0 point, 1 spot, 2 area, 3 directional; light `index` of that
+   kind in sc) at the hit O + t*D with normal N on material `mat`; the IsOccluded calls run
+   against sc.  *rng is the xorshift32 state (area samples draw from it). */
+int oracle_kat_light(const oracle_scene* sc, int kind, uint32_t index, const float o[3], const float d[3], float t,
+                     const float nrm[3], uint32_t mat, int32_t area_samples, uint32_t* rng, float out[3])
+{
+    if (!sc || !rng) return VPX_E_INVALID;
+    const fpstate fs = fp_enter();
+    tctx c;
+    tctx_init(&c, sc);
+    c.area_samples = area_samples;
+    c.rng = *rng;
+    ray_t r = make_ray(v3f(o), v3f(d));
+    r.t = t;
+    r.N = v3f(nrm);
+    r.mat = (uint8_t)mat;
+    v3 v = V3(0, 0, 0);
+    if (kind == 0) v = point_light(&c, &r, &sc->points[index]);
+    else if (kind == 1) v = spot_light(&c, &r, &sc->spots[index]);
+    else if (kind == 2) v = area_light(&c, &r, &sc->areas[index]);
+    else v = dir_light(&c, &r, &sc->dir);
+    out[0] = v.x, out[1] = v.y, out[2] = v.z;
+    *rng = c.rng;
+    fp_leave(fs);
+    return VPX_OK;
+}
+
+/* fn 0 SchlickReflectance(in0, in1); 1 SchlickReflectanceNonMetal(in0); 2 Refract(in0..2,
+   in3..5, in6); 3 Absorption(in0..2, in3, in4); 4 Reflect(in0..2, in3..5). */
+int oracle_kat_shading(int fn, const float* in, float* out)
+{
+    const fpstate fs = fp_enter();
+    v3 v;
+    switch (fn) {
+    case 0: out[0] = schlick(in[0], in[1]); break;
+    case 1: out[0] = schlick_nonmetal(in[0]); break;
+    case 2: v = refract(V3(in[0], in[1], in[2]), V3(in[3], in[4], in[5]), in[6]);
+            out[0] = v.x, out[1] = v.y, out[2] = v.z; break;
+    case 3: v = absorption(V3(in[0], in[1], in[2]), in[3], in[4]);
+            out[0] = v.x, out[1] = v.y, out[2] = v.z; break;
+    case 4: v = reflect(V3(in[0], in[1], in[2]), V3(in[3], in[4], in[5]));
+            out[0] = v.x, out[1] = v.y, out[2] = v.z; break;
+    default: fp_leave(fs); return VPX_E_INVALID;
+    }
+    fp_leave(fs);
+    return VPX_OK;
+}
+
 int oracle_find_nearest(const oracle_scene* sc, const vpx_ray* rays, uint32_t n, vpx_hit* hits)
 {
     if (!sc || (!rays && n) || (!hits && n)) return VPX_E_INVALID;
@@ -1091,8 +1196,14 @@ static v3 pixel_sample(tctx* c, const vpx_frame_params* p, uint32_t x, uint32_t 
         const v3 focal = vadd(cp, vmuls(vnormalize(vsub(P, cp)), cam->focal_distance));
         const v3 o = vadd(vadd(cp, vmuls(v3f(cam->right), jx)), vmuls(v3f(cam->up), jy));
         r = make_ray(o, vsub(focal, o));
+#ifdef ORACLE_X86
+        if (g_x86_approx) primary_rsqrt(&r, vsub(focal, o));
+#endif
     } else {
         r = make_ray(cp, vsub(P, cp));
+#ifdef ORACLE_X86
+        if (g_x86_approx) primary_rsqrt(&r, vsub(P, cp));
+#endif
     }
     return trace(c, &r, p->max_bounces);
 }

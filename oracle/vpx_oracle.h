@@ -123,6 +123,18 @@ uint32_t oracle_bvh_build(const vpx_bvh_tri* tris, uint32_t n, vpx_bvh_node* nod
 int oracle_bvh_intersect(const vpx_bvh_node* nodes, const vpx_bvh_tri* tris, const uint32_t* tri_idx,
                          const vpx_ray* rays, uint32_t n, float* t_out);
 
+/* The reference's x86 approximations on/off (FastReciprocal in FindNearest, rsqrtps in the
+   primary normalize); off by default.  Process-global; -1 on a non-x86 host. */
+int oracle_set_x86_approx(int on);
+/* Known-answer hooks (tests/test_kat_reference.py): GetNormalVoxel of the ray (o, d) at t;
+   one light evaluator at a hit; Schlick / SchlickNonMetal / Refract / Absorption / Reflect. */
+int oracle_kat_normal(const float o[3], const float d[3], float t, uint32_t n, const float m[16], float out[3]);
+int oracle_kat_light(const oracle_scene* sc, int kind, uint32_t index, const float o[3], const float d[3], float t,
+                     const float nrm[3], uint32_t mat, int32_t area_samples, uint32_t* rng, float out[3]);
+int oracle_kat_shading(int fn, const float* in, float* out);
+/* sinf/cosf/expf/powf(x,5) as the restatement evaluates them (fn 0..3), for the pin test. */
+void oracle_dm_eval(int fn, const float* x, float* out, uint32_t n);
+
 #ifdef __cplusplus
 }
 #endif

@@ -331,3 +331,36 @@ def test_transcendentals_are_correctly_rounded_floats(orc, abi, fn, name):
     for a in (ref32, out):  # FTZ (template/template.cpp:130; the path runs with it set)
         a[np.abs(a) < np.float32(2.0 ** -126)] = 0.0
     assert np.array_equal(bits(np.abs(out)), bits(np.abs(ref32))), f"{name}: {(bits(out) != bits(ref32)).sum()} mismatches"
+
+
+def test_reference_x86_approximations_stay_within_tolerance(pkg, orc):
+    """Parity hazard 1: the build uses exact 1/x and 1/sqrtf where the
+    reference uses FastReciprocal (rcpps + Newton, renderer.cpp:929-934) in FindNearest and
+    rsqrtps (tmpl8math.h:2356-2360) for the primary direction.  The oracle can run the
+    reference's own approximations on this x86 host (oracle_set_x86_approx); this measures
+    how many pixels the decision moves beyond north_star's 1e-4 per-channel tolerance
+    (the rates are specific to this CPU's rcpps/rsqrtps tables)."""
+    if not hasattr(os, "uname") or os.uname().machine not in ("x86_64", "i686"):
+        pytest.skip("x86 intrinsics")
+    abi, sc = pkg.abi, pkg.scene
+    lib = orc._lib(abi)
+    lib.oracle_set_x86_approx.argtypes = [C.c_int]
+    cases = {"C0": sc.model_scene("teapot", 128, 640, 360, 0), "C0'": sc.model_scene("monu3", 128, 640, 360, 0),
+             "roomGlass-128 d4": sc.model_scene("roomGlass", 128, 640, 360, 4)}
+    rates = {}
+    try:
+        for name, d in cases.items():
+            d.flags |= abi.VPX_FLAG_NO_TONEMAP  # the raw float sample (pre-tonemap), as north_star states it
+            o = orc.Oracle(abi, d)
+            lib.oracle_set_x86_approx(0)
+            exact, _, _ = o.render(d.frame_params(0))
+            lib.oracle_set_x86_approx(1)
+            approx, _, _ = o.render(d.frame_params(0))
+            lib.oracle_set_x86_approx(0)
+            beyond = (np.abs(exact[:, :3] - approx[:, :3]) > 1e-4).any(1)
+            rates[name] = float(beyond.mean())
+    finally:
+        lib.oracle_set_x86_approx(0)
+    print("fraction of pixels beyond 1e-4 (exact vs x86 approximations):", rates)
+    # measured on the survey container's Xeon: C0 0.0004 %, C0' 0.0043 %, roomGlass d4 0.033 %
+    assert all(r < 0.002 for r in rates.values()), rates
