@@ -40,6 +40,7 @@
  *   vpx_bvh_build_host       BasicBVH::BuildBVH          src/BVH/BasicBVH.cpp:72-136
  *   vpx_bvh_random_tris      BasicBVH::BasicBVH()        src/BVH/BasicBVH.cpp:4-16
  *   vpx_bvh_depth            (recursion depth of IntersectBVH, src/BVH/BasicBVH.cpp:47-61)
+ *   vpx_vox_decode           ogt_vox_read_scene ->models[0], ->palette, template/scene.cpp:474-475
  */
 #ifndef VPX_H_
 #define VPX_H_
@@ -379,6 +380,16 @@ uint32_t vpx_pixel_seed(uint32_t seed_base, uint32_t frame_index, uint32_t width
    number of nodes used is stored in *nodes_used. */
 int vpx_bvh_build_host(const vpx_bvh_tri* tris, uint32_t n, vpx_bvh_node* nodes, uint32_t* tri_idx,
                        uint32_t* nodes_used);
+/* MagicaVoxel .vox (versions 150 / 200) decoded as ogt_vox v0.997 hands it to
+   Scene::LoadModel (template/scene.cpp:449-529: read_scene_with_flags(buf, n, 0)->models[0]
+   and ->palette): size_out = (size_x, size_y, size_z); voxels (if not NULL, capacity
+   voxels_cap >= sx*sy*sz) = voxel_data, index x + y*sx + z*sx*sy, palette index, 0 = empty,
+   after the IMAP remap; palette_rgba (if not NULL) = 256 RGBA, voxel byte k's colour at
+   4k.  voxels == palette_rgba == NULL only queries the size.  VPX_E_INVALID for a malformed
+   file, VPX_E_STATE when a palette is asked of a file without an RGBA chunk (MagicaVoxel's
+   built-in default palette is not carried). */
+int vpx_vox_decode(const uint8_t* data, uint64_t len, uint32_t size_out[3], uint8_t* voxels,
+                   uint64_t voxels_cap, uint8_t palette_rgba[1024]);
 /* Depth of a tree built by vpx_bvh_build_host (a leaf root = 1; 0 when nodes_used == 0). */
 uint32_t vpx_bvh_depth(const vpx_bvh_node* nodes, uint32_t nodes_used);
 /* BasicBVH::BasicBVH() triangle set (BasicBVH.cpp:4-16): 64 triangles, vertex0 = r0*9-5,

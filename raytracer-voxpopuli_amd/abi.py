@@ -13,6 +13,7 @@ LIB_PATH = os.path.join(HERE, "libvpx_hip.so")
 ABI_VERSION = 1
 
 VPX_OK = 0
+VPX_E_INVALID, VPX_E_DEVICE, VPX_E_NOMEM, VPX_E_STATE = -1, -2, -3, -4  # include/vpx.h status codes
 VPX_FLAG_AA = 0x1
 VPX_FLAG_DOF = 0x2
 VPX_FLAG_NO_TONEMAP = 0x4
@@ -182,6 +183,7 @@ SIGNATURES = {
                                      C.POINTER(C.c_uint32)]),
     "vpx_bvh_random_tris": (C.c_int, [C.POINTER(C.c_uint32), C.POINTER(BvhTri)]),
     "vpx_bvh_depth": (C.c_uint32, [C.POINTER(BvhNode), C.c_uint32]),
+    "vpx_vox_decode": (C.c_int, [C.c_void_p, C.c_uint64, C.POINTER(C.c_uint32), C.c_void_p, C.c_uint64, C.c_void_p]),
 }
 
 _LIB = None

@@ -380,3 +380,118 @@ int vpx_bvh_random_tris(uint32_t* seed, vpx_bvh_tri out[64]) {
 }
 
 }  // extern "C"
+
+// ------------------------------------------------------------------ .vox decoder
+// MagicaVoxel .vox (versions 150 / 200) decoded to what Scene::LoadModel receives from
+// ogt_vox v0.997 (template/scene.cpp:474-475: ogt_vox_read_scene_with_flags(buf, n, 0)
+// ->models[0] and ->palette), restated from the format and ogt's documented read rules:
+//   - chunks are (id, size, child size, payload); MAIN's payload is its children;
+//   - every SIZE + XYZI pair is a model (voxel_data x + y*sx + z*sx*sy, palette index,
+//     0 = empty); a model whose XYZI holds no voxel is culled, so models[0] is the first
+//     model with voxels (de-duplication only ever drops later copies);
+//   - RGBA holds 256 RGBA colours, colour k of the file describing palette index k + 1;
+//   - IMAP (display index -> file index) reorders the palette into display order,
+//     palette[i] = file[(imap[i] + 255) & 255], and every voxel byte v of every model
+//     (empty ones included) becomes (uint8)(1 + inverse_imap[v]);
+//   - finally the palette is rotated by one so a voxel byte indexes it directly:
+//     palette[i] = file[i - 1], palette[0] = file[255] with alpha 0.
+namespace {
+struct VoxReader {
+    const uint8_t* p;
+    uint64_t n, at = 0;
+    bool u32(uint32_t& v) {
+        if (n - at < 4) return false;
+        std::memcpy(&v, p + at, 4);
+        at += 4;
+        return true;
+    }
+};
+constexpr uint32_t vox_id(char a, char b, char c, char d) {
+    return (uint32_t)(uint8_t)a | (uint32_t)(uint8_t)b << 8 | (uint32_t)(uint8_t)c << 16 | (uint32_t)(uint8_t)d << 24;
+}
+}  // namespace
+
+extern "C" {
+
+int vpx_vox_decode(const uint8_t* data, uint64_t len, uint32_t size_out[3], uint8_t* voxels, uint64_t voxels_cap,
+                   uint8_t palette_rgba[1024]) {
+    if (!data || !size_out) return VPX_E_INVALID;
+    VoxReader r{data, len};
+    uint32_t magic = 0, version = 0;
+    if (!r.u32(magic) || !r.u32(version) || magic != vox_id('V', 'O', 'X', ' ') || (version != 150 && version != 200))
+        return VPX_E_INVALID;
+    uint32_t sx = 0, sy = 0, sz = 0;
+    bool have_model = false, have_rgba = false, have_imap = false;
+    uint32_t m0[3] = {0, 0, 0};
+    std::vector<uint8_t> model;
+    uint8_t rgba[1024];
+    uint8_t imap[256];
+    while (len - r.at >= 12) {
+        uint32_t id, size, child;
+        r.u32(id), r.u32(size), r.u32(child);
+        if (id == vox_id('M', 'A', 'I', 'N')) continue;  // its children follow
+        if (size > len - r.at) return VPX_E_INVALID;
+        const uint8_t* body = data + r.at;
+        if (id == vox_id('S', 'I', 'Z', 'E')) {
+            if (size != 12) return VPX_E_INVALID;
+            std::memcpy(&sx, body, 4), std::memcpy(&sy, body + 4, 4), std::memcpy(&sz, body + 8, 4);
+            if (!sx || !sy || !sz) return VPX_E_INVALID;
+        } else if (id == vox_id('X', 'Y', 'Z', 'I')) {
+            if (!sx || size < 4) return VPX_E_INVALID;
+            uint32_t nv;
+            std::memcpy(&nv, body, 4);
+            if (nv && !have_model) {  // models[0]: the first model holding voxels
+                const uint64_t count = (uint64_t)sx * sy * sz;
+                if (count > (1ull << 32)) return VPX_E_INVALID;
+                model.assign(count, 0);
+                const uint64_t avail = (size - 4) / 4;
+                const uint64_t m = nv < avail ? nv : avail;
+                for (uint64_t i = 0; i < m; ++i) {
+                    const uint8_t* v = body + 4 + 4 * i;
+                    if (v[0] >= sx || v[1] >= sy || v[2] >= sz) return VPX_E_INVALID;
+                    model[v[0] + (uint64_t)v[1] * sx + (uint64_t)v[2] * sx * sy] = v[3];
+                }
+                m0[0] = sx, m0[1] = sy, m0[2] = sz;
+                have_model = true;
+            }
+        } else if (id == vox_id('R', 'G', 'B', 'A')) {
+            if (size != 1024) return VPX_E_INVALID;
+            std::memcpy(rgba, body, 1024);
+            have_rgba = true;
+        } else if (id == vox_id('I', 'M', 'A', 'P')) {
+            if (size != 256) return VPX_E_INVALID;
+            std::memcpy(imap, body, 256);
+            have_imap = true;
+        }
+        r.at += size;  // every other chunk (scene graph, layers, materials, cameras) is skipped
+    }
+    if (!have_model) return VPX_E_INVALID;
+    size_out[0] = m0[0], size_out[1] = m0[1], size_out[2] = m0[2];
+    const uint64_t count = (uint64_t)m0[0] * m0[1] * m0[2];
+    if (!voxels && !palette_rgba) return VPX_OK;  // size query
+    if (palette_rgba && !have_rgba) return VPX_E_STATE;  // MagicaVoxel's default palette is not carried
+    uint8_t inv[256] = {0};
+    if (have_imap) {
+        bool seen[256] = {false};
+        for (int i = 0; i < 256; ++i) {
+            if (seen[imap[i]]) return VPX_E_INVALID;  // not a permutation
+            seen[imap[i]] = true;
+            inv[imap[i]] = (uint8_t)i;
+        }
+    }
+    if (voxels) {
+        if (voxels_cap < count) return VPX_E_INVALID;
+        for (uint64_t i = 0; i < count; ++i) voxels[i] = have_imap ? (uint8_t)(1u + inv[model[i]]) : model[i];
+    }
+    if (palette_rgba) {
+        uint8_t disp[1024];  // display order
+        for (int i = 0; i < 256; ++i)
+            std::memcpy(disp + 4 * i, rgba + 4 * (have_imap ? ((imap[i] + 255) & 255) : i), 4);
+        for (int i = 1; i < 256; ++i) std::memcpy(palette_rgba + 4 * i, disp + 4 * (i - 1), 4);
+        std::memcpy(palette_rgba, disp + 4 * 255, 4);
+        palette_rgba[3] = 0;
+    }
+    return VPX_OK;
+}
+
+}  // extern "C"

@@ -1,8 +1,14 @@
 """Scene descriptions for the trace path: worlds, volumes, materials, lights, camera.
 
 Everything here is HOST-side input preparation restating the reference's scene setup:
-  - models: the ogt_vox-decoded .vox data (tests/golden/<name>.npz, produced by the
-    reference's own vendored decoder lib/ogt_vox.h — see tests/golden/make_golden.py);
+  - models: `decode_vox(path)` decodes a MagicaVoxel .vox file with the library's own
+    decoder (vpx_vox_decode: what ogt_vox hands Scene::LoadModel, template/scene.cpp:
+    474-475).  The benchmark / test workloads (C0-C4) name the reference's assets
+    (teapot, monu3, roomGlass); the .vox files themselves do not travel with this repo,
+    so `load_model(name)` decodes `<VPX_ASSETS_DIR>/<name>.vox` when that directory is
+    given and otherwise reads the same decoded data from tests/golden/<name>.npz (the
+    reference's vendored ogt_vox output; tests/test_vox_decode.py checks vpx_vox_decode
+    against it on all 12 reference assets);
   - `load_model_grid`  Scene::LoadModel placement      template/scene.cpp:449-529
   - `palette_materials` LoadModel's palette override    template/scene.cpp:516-520
   - lights / materials / camera defaults                renderer.cpp:93-100,357-443; camera.h
@@ -26,8 +32,28 @@ NONE = abi.MAT_NONE
 
 
 # ----------------------------------------------------------------------------- models
+def decode_vox(src):
+    """A .vox file (path or bytes) -> (size[3], voxels uint8[sx*sy*sz], palette uint8[256,4])
+    through vpx_vox_decode (models[0] and the palette as ogt_vox v0.997 returns them)."""
+    data = src if isinstance(src, (bytes, bytearray)) else open(src, "rb").read()
+    lib = abi.load_library()
+    buf = (C.c_uint8 * max(1, len(data))).from_buffer_copy(bytes(data) or b"\0")
+    size = (C.c_uint32 * 3)()
+    abi.check(lib, None, lib.vpx_vox_decode(buf, len(data), size, None, 0, None), "vpx_vox_decode (size)")
+    n = int(size[0]) * int(size[1]) * int(size[2])
+    vox = np.empty(n, np.uint8)
+    pal = np.empty((256, 4), np.uint8)
+    abi.check(lib, None, lib.vpx_vox_decode(buf, len(data), size, vox.ctypes.data, n, pal.ctypes.data),
+              "vpx_vox_decode")
+    return np.array(size[:], np.int64), vox, pal
+
+
 def load_model(name):
-    """(size[3], voxels uint8[sx*sy*sz], palette uint8[256,4]) as ogt_vox returns them."""
+    """(size[3], voxels uint8[sx*sy*sz], palette uint8[256,4]) as ogt_vox returns them:
+    decoded from $VPX_ASSETS_DIR/<name>.vox when set, else the decoded fixture."""
+    d = os.environ.get("VPX_ASSETS_DIR")
+    if d:
+        return decode_vox(os.path.join(d, name + ".vox"))
     z = np.load(os.path.join(GOLDEN, name + ".npz"))
     return z["size"].astype(np.int64), z["voxels"].astype(np.uint8), z["palette"].astype(np.uint8)
 

@@ -18,7 +18,8 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(os.path.dirname(HERE))
-MODELS = ("teapot", "monu3", "roomGlass")
+MODELS = ("teapot", "monu3", "roomGlass", "monu1", "monu2", "room", "player", "SmallBuilding01",
+          "SmallBuilding02", "TallBuilding01", "Text", "textWin")  # every .vox in the reference's assets/
 
 
 def dump(tool, vox_path):

@@ -1,0 +1,125 @@
+"""The library's .vox decoder (vpx_vox_decode) against ogt_vox v0.997.
+
+`Scene::LoadModel` (template/scene.cpp:449-529) takes models[0] and the palette of
+ogt_vox_read_scene_with_flags(buf, n, 0).  tests/golden/<name>.npz holds exactly that for
+every .vox of the reference's assets/ (the reference's own vendored lib/ogt_vox.h,
+compiled where it lies: tests/golden/make_golden.py).  Here:
+  - every reference asset decodes to its fixture byte for byte (needs the reference tree,
+    i.e. this container; the .vox files do not travel with the repo);
+  - hand-built files pin the rules one at a time: voxel layout, the first non-empty
+    model, the palette rotation, the IMAP remap (palette and voxels, empties included),
+    the size query, and malformed inputs.
+"""
+import ctypes as C
+import os
+import struct
+
+import numpy as np
+import pytest
+
+REF_ASSETS = "/root/reference/assets"
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+MODELS = ("teapot", "monu3", "roomGlass", "monu1", "monu2", "room", "player", "SmallBuilding01",
+          "SmallBuilding02", "TallBuilding01", "Text", "textWin")
+
+
+@pytest.mark.parametrize("name", MODELS)
+def test_reference_assets_decode_like_ogt_vox(pkg, name):
+    path = os.path.join(REF_ASSETS, name + ".vox")
+    if not os.path.exists(path):
+        pytest.skip("reference tree absent (the .vox assets do not travel)")
+    size, vox, pal = pkg.scene.decode_vox(path)
+    z = np.load(os.path.join(GOLDEN, name + ".npz"))
+    assert size.tolist() == z["size"].tolist()
+    assert np.array_equal(vox, z["voxels"])
+    assert np.array_equal(pal, z["palette"])
+
+
+# ------------------------------------------------------------------ hand-built files
+def chunk(cid, body=b"", children=b""):
+    return cid.encode() + struct.pack("<II", len(body), len(children)) + body + children
+
+
+def vox_file(models, rgba=None, imap=None, version=200, extra=b""):
+    kids = b""
+    for (sx, sy, sz), voxels in models:
+        kids += chunk("SIZE", struct.pack("<III", sx, sy, sz))
+        kids += chunk("XYZI", struct.pack("<I", len(voxels)) + b"".join(bytes(v) for v in voxels))
+    kids += extra
+    if rgba is not None:
+        kids += chunk("RGBA", bytes(np.asarray(rgba, np.uint8).reshape(-1)))
+    if imap is not None:
+        kids += chunk("IMAP", bytes(np.asarray(imap, np.uint8)))
+    return b"VOX " + struct.pack("<I", version) + chunk("MAIN", b"", kids)
+
+
+def file_palette():
+    p = np.zeros((256, 4), np.uint8)
+    p[:, 0] = np.arange(256)
+    p[:, 1] = 255 - np.arange(256)
+    p[:, 2] = (np.arange(256) * 7) & 255
+    p[:, 3] = 255
+    return p
+
+
+def test_layout_first_model_and_palette_rotation(pkg):
+    # an empty model first (culled), then a 3x2x2 model; voxel (x, y, z, index)
+    vs = [(0, 0, 0, 5), (2, 1, 0, 9), (1, 0, 1, 255), (2, 1, 1, 1)]
+    data = vox_file([((4, 4, 4), []), ((3, 2, 2), vs), ((1, 1, 1), [(0, 0, 0, 7)])], rgba=file_palette(),
+                    extra=chunk("nTRN", b"\0" * 28) + chunk("LAYR", b"\1" * 12))
+    size, vox, pal = pkg.scene.decode_vox(data)
+    assert size.tolist() == [3, 2, 2]
+    want = np.zeros(12, np.uint8)
+    for x, y, z, c in vs:
+        want[x + y * 3 + z * 6] = c
+    assert np.array_equal(vox, want)
+    fp = file_palette()
+    assert np.array_equal(pal[1:], fp[:255])          # palette[k] = file colour k - 1
+    assert np.array_equal(pal[0, :3], fp[255, :3]) and pal[0, 3] == 0  # file colour 255, alpha 0
+
+
+def test_imap_remaps_palette_and_every_voxel(pkg):
+    rng = np.random.default_rng(4)
+    imap = rng.permutation(256).astype(np.uint8)
+    inv = np.zeros(256, np.uint8)
+    inv[imap] = np.arange(256, dtype=np.uint8)
+    vs = [(0, 0, 0, 3), (1, 0, 0, 200), (0, 1, 0, 255)]
+    data = vox_file([((2, 2, 1), vs)], rgba=file_palette(), imap=imap)
+    size, vox, pal = pkg.scene.decode_vox(data)
+    raw = np.zeros(4, np.uint8)
+    for x, y, z, c in vs:
+        raw[x + y * 2] = c
+    assert np.array_equal(vox, (1 + inv[raw].astype(np.uint32)).astype(np.uint8))  # empties remapped too
+    fp = file_palette()
+    disp = fp[(imap.astype(np.int64) + 255) & 255]      # display order
+    assert np.array_equal(pal[1:], disp[:255])
+    assert np.array_equal(pal[0, :3], disp[255, :3]) and pal[0, 3] == 0
+
+
+def test_size_query_missing_palette_and_malformed(pkg):
+    lib, abi = pkg.load_library(), pkg.abi
+    data = vox_file([((2, 1, 1), [(1, 0, 0, 4)])])  # no RGBA chunk
+
+    def call(buf, want_vox=True, want_pal=False):
+        b = (C.c_uint8 * max(1, len(buf))).from_buffer_copy(buf or b"\0")
+        size = (C.c_uint32 * 3)()
+        vox = np.zeros(64, np.uint8)
+        pal = np.zeros(1024, np.uint8)
+        rc = lib.vpx_vox_decode(b, len(buf), size, vox.ctypes.data if want_vox else None, 64,
+                                pal.ctypes.data if want_pal else None)
+        return rc, list(size), vox
+
+    rc, size, _ = call(data, want_vox=False)
+    assert rc == abi.VPX_OK and size == [2, 1, 1]       # size query
+    rc, _, vox = call(data)
+    assert rc == abi.VPX_OK and vox[:2].tolist() == [0, 4]
+    assert call(data, want_pal=True)[0] == abi.VPX_E_STATE  # default palette not carried
+    bad = [b"", b"VOX ", b"XOV " + data[4:], data[:4] + struct.pack("<I", 151) + data[8:],
+           vox_file([((2, 1, 1), [(2, 0, 0, 4)])]),       # voxel outside SIZE
+           vox_file([((2, 1, 1), [])]),                    # no model with voxels
+           data[:-3],                                      # truncated chunk
+           vox_file([((2, 1, 1), [(1, 0, 0, 4)])], imap=np.zeros(256, np.uint8))]  # IMAP not a permutation
+    for b in bad:
+        assert call(b)[0] == abi.VPX_E_INVALID, b[:16]
+    assert vox_file([((2, 1, 1), [(1, 0, 0, 4)])], version=150)  # both versions accepted
+    assert call(vox_file([((2, 1, 1), [(1, 0, 0, 4)])], version=150))[0] == abi.VPX_OK
