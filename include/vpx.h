@@ -16,6 +16,7 @@
  * matrices are tmpl8 `mat4::cell` order (row-major, translation in cells 3/7/11).
  *
  * Reference interfaces replaced (file:line in the reference tree):
+ *   vpx_create[_multi]    Renderer::Init (device side) renderer.cpp:688-736
  *   vpx_render            Renderer::Update            renderer.cpp:1646-1891
  *                         (+ Renderer::Trace           renderer.cpp:1076-1328)
  *   vpx_find_nearest      Renderer::FindNearest       renderer.cpp:946-1018
@@ -194,6 +195,18 @@ typedef struct vpx_ctx vpx_ctx;
 
 /* ---- lifetime ------------------------------------------------------------------------ */
 int vpx_create(int device, vpx_ctx** out);
+/* A device set for a single-process host (the tmpl8 Renderer::Tick on a multi-GPU node):
+   one member context per entry of devices[0..ndev) (the world and tables are uploaded to
+   every member by the same calls as for one device).  vpx_render deals the 16x16 tiles
+   round-robin to the members, renders them concurrently, gathers the packed results to
+   devices[0] over RCCL (one communicator per device, ncclCommInitAll; device copies when
+   the set repeats a device) and composites there: with accum != NULL the float4 samples
+   travel and accum / rgb8 (devices[0] pointers) are bit-identical to vpx_render on one
+   device; with accum == NULL each member keeps the running average of its own tiles and
+   only RGB8 travels into rgb8.  vpx_set_stream sets devices[0]'s stream; unit entries,
+   profiles, vpx_render_reproject and the rank-level entries (vpx_render_tiles*,
+   vpx_composite_*) run on devices[0]; vpx_get_counters sums the members. */
+int vpx_create_multi(const int* devices, int ndev, vpx_ctx** out);
 int vpx_destroy(vpx_ctx* ctx);
 const char* vpx_last_error(const vpx_ctx* ctx);
 int vpx_abi_version(void);

@@ -131,6 +131,7 @@ def as_ptr(arr, struct=None):
 # name -> (restype, argtypes); every symbol include/vpx.h declares
 SIGNATURES = {
     "vpx_create": (C.c_int, [C.c_int, C.POINTER(C.c_void_p)]),
+    "vpx_create_multi": (C.c_int, [C.POINTER(C.c_int), C.c_int, C.POINTER(C.c_void_p)]),
     "vpx_destroy": (C.c_int, [C.c_void_p]),
     "vpx_last_error": (C.c_char_p, [C.c_void_p]),
     "vpx_abi_version": (C.c_int, []),

@@ -7,14 +7,24 @@ from . import abi
 
 
 class Context:
-    def __init__(self, device=0):
+    def __init__(self, device=0, devices=None):
+        """One device (vpx_create), or a device set (vpx_create_multi: `devices` list, the
+        frame tile-sharded over them and gathered to devices[0])."""
         self.lib = abi.load_library()
         h = C.c_void_p()
-        rc = self.lib.vpx_create(int(device), C.byref(h))
-        if rc != abi.VPX_OK:
-            raise abi.VpxError(f"vpx_create(device={device}) failed ({rc}): no usable HIP device")
+        if devices is not None:
+            arr = (C.c_int * len(devices))(*[int(d) for d in devices])
+            rc = self.lib.vpx_create_multi(arr, len(devices), C.byref(h))
+            if rc != abi.VPX_OK:
+                raise abi.VpxError(f"vpx_create_multi(devices={list(devices)}) failed ({rc})")
+            device = int(devices[0])
+        else:
+            rc = self.lib.vpx_create(int(device), C.byref(h))
+            if rc != abi.VPX_OK:
+                raise abi.VpxError(f"vpx_create(device={device}) failed ({rc}): no usable HIP device")
         self.h = h
         self.device = device
+        self.devices = list(devices) if devices is not None else [device]
         self.scene = None
         self.stream_handle = None
 

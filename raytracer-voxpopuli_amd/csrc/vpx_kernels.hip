@@ -9,6 +9,7 @@
 //   find_nearest_k / is_occluded_k / trace_k   per-ray unit entries.
 //   tiled_world_k / checksum_k    world generator and grid checksum.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cmath>
@@ -385,6 +386,10 @@ struct vpx_ctx {
     std::vector<vpx_volume> volumes;
     vpx_volume* d_volumes = nullptr;
     float4* d_vbounds = nullptr;  // per volume: world bounding sphere (centre, radius^2), see volume_bounds
+    void* d_tlas = nullptr;       // instance TLAS: nodes, then the leaf volume list (build_tlas)
+    uint32_t tlas_nodes = 0;
+    bool tlas_on = false;
+    uint64_t tlas_always = 0;
     void* d_bvh = nullptr;        // BasicBVH: nodes, then the triangles in tri_idx order (vpx_bvh_set)
     uint32_t bvh_nodes = 0, bvh_tris = 0;
     uint32_t d_volumes_cap = 0;
@@ -419,6 +424,16 @@ struct vpx_ctx {
     size_t rp_pixels = 0;
     size_t wave_bytes = 0;
     WaveBufs wave{};
+    // device set (vpx_create_multi): one member context per device; this context only
+    // forwards (VPX_GROUP_*) and runs the tile-sharded vpx_render (group_render)
+    std::vector<vpx_ctx*> members;
+    std::vector<ncclComm_t> comms;      // RCCL, one per member (distinct devices only)
+    std::vector<void*> g_packed;        // per member: packed float4 samples / RGB8 (member device)
+    std::vector<float*> g_accum;        // per member: packed accumulator (accum == NULL mode)
+    void* g_gathered = nullptr;         // member 0's device: the members' packed buffers back to back
+    size_t g_len = 0;                   // float4 elements per member buffer the above were sized for
+    std::vector<hipEvent_t> g_ev;       // per member: its render done (copy path)
+    hipEvent_t g_copied = nullptr;      // member 0: gather copies done (copy path)
 };
 
 namespace {
@@ -427,6 +442,29 @@ int fail(vpx_ctx* c, int code, const std::string& msg) {
     if (c) c->err = msg;
     return code;
 }
+
+// Device-set contexts forward to their members: every member (uploads / state) or member 0
+// (unit entries, profiles, the single-image static-camera path, the rank-level primitives).
+template <class F>
+int group_all(vpx_ctx* c, F f) {
+    for (vpx_ctx* m : c->members) {
+        if (hipSetDevice(m->device) != hipSuccess) return fail(c, VPX_E_DEVICE, "hipSetDevice");
+        const int rc = f(m);
+        if (rc) return fail(c, rc, "device " + std::to_string(m->device) + ": " + m->err);
+    }
+    return VPX_OK;
+}
+template <class F>
+int group_first(vpx_ctx* c, F f) {
+    vpx_ctx* m = c->members[0];
+    if (hipSetDevice(m->device) != hipSuccess) return fail(c, VPX_E_DEVICE, "hipSetDevice");
+    const int rc = f(m);
+    return rc ? fail(c, rc, m->err) : VPX_OK;
+}
+#define VPX_GROUP_ALL(c, call) \
+    if ((c) && !(c)->members.empty()) return group_all((c), [&](vpx_ctx* m_) { return call; })
+#define VPX_GROUP_FIRST(c, call) \
+    if ((c) && !(c)->members.empty()) return group_first((c), [&](vpx_ctx* m_) { return call; })
 
 #define VPX_HIP(c, expr)                                                                            \
     do {                                                                                            \
@@ -491,6 +529,10 @@ SceneView view_of(const vpx_ctx* c, const float sky[3], int32_t area_samples, bo
     sv.grids = c->d_grids;
     sv.volumes = c->d_volumes;
     sv.vbounds = c->d_vbounds;
+    sv.tlas = (const TlasNode*)c->d_tlas;
+    sv.tlas_on = c->tlas_on ? 1u : 0u;
+    sv.tlas_nodes = c->tlas_nodes;
+    sv.tlas_always = c->tlas_always;
     sv.materials = c->d_materials;
     sv.points = c->d_points;
     sv.spots = c->d_spots;
@@ -731,6 +773,24 @@ int vpx_create(int device, vpx_ctx** out) {
 
 int vpx_destroy(vpx_ctx* c) {
     if (!c) return VPX_E_INVALID;
+    if (!c->members.empty()) {  // device set: its buffers, communicators and members
+        for (size_t r = 0; r < c->members.size(); ++r) {
+            vpx_ctx* m = c->members[r];
+            (void)hipSetDevice(m->device);
+            (void)hipStreamSynchronize(m->stream);
+            if (r < c->g_packed.size() && c->g_packed[r]) (void)hipFree(c->g_packed[r]);
+            if (r < c->g_accum.size() && c->g_accum[r]) (void)hipFree(c->g_accum[r]);
+            if (r < c->g_ev.size() && c->g_ev[r]) (void)hipEventDestroy(c->g_ev[r]);
+            if (r == 0) {
+                if (c->g_gathered) (void)hipFree(c->g_gathered);
+                if (c->g_copied) (void)hipEventDestroy(c->g_copied);
+            }
+        }
+        for (ncclComm_t cm : c->comms) (void)ncclCommDestroy(cm);
+        for (vpx_ctx* m : c->members) vpx_destroy(m);
+        delete c;
+        return VPX_OK;
+    }
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (auto& g : c->grids) {
@@ -738,7 +798,7 @@ int vpx_destroy(vpx_ctx* c) {
         if (g.l1) (void)hipFree(g.l1);
         if (g.l2) (void)hipFree(g.l2);
     }
-    void* ptrs[] = {c->d_grids, c->d_volumes, c->d_vbounds, c->d_bvh, c->d_materials, c->d_points, c->d_spots, c->d_areas,
+    void* ptrs[] = {c->d_grids, c->d_volumes, c->d_vbounds, c->d_tlas, c->d_bvh, c->d_materials, c->d_points, c->d_spots, c->d_areas,
                     c->d_spheres, c->d_triangles, c->d_ctr, c->d_sum, c->d_scratch, c->d_wave, c->d_sky};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
@@ -756,11 +816,13 @@ const char* vpx_last_error(const vpx_ctx* c) { return c ? c->err.c_str() : "null
 
 int vpx_set_stream(vpx_ctx* c, void* s) {
     if (!c) return VPX_E_INVALID;
+    if (!c->members.empty()) return vpx_set_stream(c->members[0], s);  // a stream of the first device
     c->stream = s ? (hipStream_t)s : c->own_stream;
     return VPX_OK;
 }
 
 int vpx_synchronize(vpx_ctx* c) {
+    VPX_GROUP_ALL(c, vpx_synchronize(m_));
     if (!c) return VPX_E_INVALID;
     VPX_HIP(c, hipStreamSynchronize(c->stream));
     return VPX_OK;
@@ -843,6 +905,7 @@ static int build_masks_box(vpx_ctx* c, uint32_t id, uint32_t x0, uint32_t y0, ui
 }
 
 int vpx_grid_fill(vpx_ctx* c, uint32_t id, uint8_t value) {
+    VPX_GROUP_ALL(c, vpx_grid_fill(m_, id, value));
     if (!c) return VPX_E_INVALID;
     if (id >= c->grids.size() || !c->grids[id].ptr) return fail(c, VPX_E_INVALID, "unknown grid");
     auto& g = c->grids[id];
@@ -852,6 +915,7 @@ int vpx_grid_fill(vpx_ctx* c, uint32_t id, uint8_t value) {
 
 int vpx_grid_write_box(vpx_ctx* c, uint32_t id, const uint8_t* src, uint32_t x0, uint32_t y0, uint32_t z0,
                        uint32_t dx, uint32_t dy, uint32_t dz) {
+    VPX_GROUP_ALL(c, vpx_grid_write_box(m_, id, src, x0, y0, z0, dx, dy, dz));
     if (!c || !src) return fail(c, VPX_E_INVALID, "null argument");
     if (id >= c->grids.size() || !c->grids[id].ptr) return fail(c, VPX_E_INVALID, "unknown grid");
     auto& g = c->grids[id];
@@ -874,6 +938,7 @@ int vpx_grid_write_box(vpx_ctx* c, uint32_t id, const uint8_t* src, uint32_t x0,
 }
 
 int vpx_grid_emissive_sphere(vpx_ctx* c, uint32_t id, uint8_t mat, float radius) {
+    VPX_GROUP_ALL(c, vpx_grid_emissive_sphere(m_, id, mat, radius));
     if (!c) return VPX_E_INVALID;
     if (id >= c->grids.size() || !c->grids[id].ptr) return fail(c, VPX_E_INVALID, "unknown grid");
     auto& g = c->grids[id];
@@ -891,6 +956,7 @@ int vpx_grid_emissive_sphere(vpx_ctx* c, uint32_t id, uint8_t mat, float radius)
 }
 
 int vpx_upload_grid(vpx_ctx* c, uint32_t id, const uint8_t* cells, uint32_t n) {
+    VPX_GROUP_ALL(c, vpx_upload_grid(m_, id, cells, n));
     if (!c || !cells) return fail(c, VPX_E_INVALID, "null argument");
     int rc = alloc_grid(c, id, n);
     if (rc) return rc;
@@ -900,6 +966,7 @@ int vpx_upload_grid(vpx_ctx* c, uint32_t id, const uint8_t* cells, uint32_t n) {
 
 int vpx_generate_tiled_grid(vpx_ctx* c, uint32_t id, uint32_t n, const uint8_t* model, uint32_t mx, uint32_t my,
                             uint32_t mz, uint32_t px, uint32_t py, uint32_t pz, uint32_t ground) {
+    VPX_GROUP_ALL(c, vpx_generate_tiled_grid(m_, id, n, model, mx, my, mz, px, py, pz, ground));
     if (!c || !model) return fail(c, VPX_E_INVALID, "null argument");
     if (!mx || !my || !mz || !px || !py || !pz) return fail(c, VPX_E_INVALID, "zero model size or period");
     int rc = alloc_grid(c, id, n);
@@ -917,6 +984,7 @@ int vpx_generate_tiled_grid(vpx_ctx* c, uint32_t id, uint32_t n, const uint8_t* 
 }
 
 int vpx_grid_checksum(vpx_ctx* c, uint32_t id, uint64_t* out) {
+    VPX_GROUP_FIRST(c, vpx_grid_checksum(m_, id, out));
     if (!c || !out) return fail(c, VPX_E_INVALID, "null argument");
     if (id >= c->grids.size() || !c->grids[id].ptr) return fail(c, VPX_E_INVALID, "unknown grid");
     const uint64_t count = (uint64_t)c->grids[id].n * c->grids[id].n * c->grids[id].n;
@@ -972,7 +1040,91 @@ static float4 volume_bounds(const vpx_volume& v) {
     return make_float4((float)cen[0], (float)cen[1], (float)cen[2], (float)(rr * rr));
 }
 
+// Instance TLAS (the C4 lattice of 64 instances over the world volume): a BVH over the
+// inflated world bounding spheres (volume_bounds) of volumes 1..n-1, built once per
+// vpx_set_volumes (volume 0, first in the reference's loop, is walked before the tree is
+// asked, so the instances' candidates are bounded by its hit).
+// Boxes are the spheres' AABBs widened by a further 1e-4 of the scale and rounded outward
+// to float, so every volume misses_volume keeps is a candidate.  Median split on the
+// longest centroid axis (ties by index), leaves of <= 4 volumes (their bit mask), nodes in
+// depth-first order with skip links (TlasNode).  Volumes without finite bounds go to the
+// always-set.
+struct TlasBuild {
+    std::vector<TlasNode> nodes;
+    struct Item {
+        double lo[3], hi[3], c[3];
+        uint32_t id;
+    };
+    std::vector<Item> items;
+    void build(uint32_t first, uint32_t count) {
+        const uint32_t me = (uint32_t)nodes.size();
+        nodes.push_back(TlasNode{});
+        double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        double clo[3] = {INFINITY, INFINITY, INFINITY}, chi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        for (uint32_t i = first; i < first + count; ++i)
+            for (int k = 0; k < 3; ++k) {
+                lo[k] = std::min(lo[k], items[i].lo[k]), hi[k] = std::max(hi[k], items[i].hi[k]);
+                clo[k] = std::min(clo[k], items[i].c[k]), chi[k] = std::max(chi[k], items[i].c[k]);
+            }
+        TlasNode nd{};
+        for (int k = 0; k < 3; ++k) {
+            nd.lo[k] = std::nextafter((float)lo[k], -INFINITY);
+            nd.hi[k] = std::nextafter((float)hi[k], INFINITY);
+        }
+        if (count <= 4) {
+            nd.leaf = 1;
+            for (uint32_t i = first; i < first + count; ++i) nd.mask |= 1ull << (items[i].id - 1u);
+            nodes[me] = nd;
+            return;
+        }
+        int axis = 0;
+        for (int k = 1; k < 3; ++k)
+            if (chi[k] - clo[k] > chi[axis] - clo[axis]) axis = k;
+        std::stable_sort(items.begin() + first, items.begin() + first + count,
+                         [axis](const Item& x, const Item& y) { return x.c[axis] < y.c[axis]; });
+        const uint32_t half = count / 2;
+        build(first, half);
+        build(first + half, count - half);
+        nd.skip = (uint32_t)nodes.size();  // the node after this subtree
+        nodes[me] = nd;
+    }
+};
+
+#ifndef VPX_TLAS
+#define VPX_TLAS 1  // -DVPX_TLAS=0: the reference's linear volume loop (A/B builds)
+#endif
+int build_tlas(vpx_ctx* c, const std::vector<float4>& bounds) {
+    c->tlas_on = false;
+    c->tlas_nodes = 0;
+    c->tlas_always = 0;
+    const uint32_t count = (uint32_t)bounds.size();
+    if (!VPX_TLAS || count < 2 || count > kTlasMaxVolumes) return VPX_OK;  // one volume / too many: the linear loop
+    TlasBuild b;
+    for (uint32_t i = 1; i < count; ++i) {  // volume 0 is walked first, outside the tree
+        const float4 s = bounds[i];
+        if (!std::isfinite(s.w)) {
+            c->tlas_always |= 1ull << (i - 1u);
+            continue;
+        }
+        const double r = std::sqrt((double)s.w), cc[3] = {s.x, s.y, s.z};
+        const double pad = r * 1e-4 + 1e-4 * (1.0 + std::fabs(cc[0]) + std::fabs(cc[1]) + std::fabs(cc[2]) + r);
+        TlasBuild::Item it{};
+        for (int k = 0; k < 3; ++k) it.lo[k] = cc[k] - r - pad, it.hi[k] = cc[k] + r + pad, it.c[k] = cc[k];
+        it.id = i;
+        b.items.push_back(it);
+    }
+    if (!b.items.empty()) b.build(0, (uint32_t)b.items.size());
+    if (b.nodes.size() > kTlasMaxNodes) return fail(c, VPX_E_INVALID, "TLAS node budget exceeded");
+    if (!c->d_tlas) VPX_HIP(c, hipMalloc(&c->d_tlas, sizeof(TlasNode) * kTlasMaxNodes));
+    if (!b.nodes.empty())
+        VPX_HIP(c, hipMemcpy(c->d_tlas, b.nodes.data(), sizeof(TlasNode) * b.nodes.size(), hipMemcpyHostToDevice));
+    c->tlas_nodes = (uint32_t)b.nodes.size();
+    c->tlas_on = true;
+    return VPX_OK;
+}
+
 int vpx_set_volumes(vpx_ctx* c, const vpx_volume* v, uint32_t count) {
+    VPX_GROUP_ALL(c, vpx_set_volumes(m_, v, count));
     if (!c || (!v && count)) return fail(c, VPX_E_INVALID, "null argument");
     if (count > 65536) return fail(c, VPX_E_INVALID, "too many volumes");
     VPX_HIP(c, hipStreamSynchronize(c->stream));
@@ -992,10 +1144,11 @@ int vpx_set_volumes(vpx_ctx* c, const vpx_volume* v, uint32_t count) {
         VPX_HIP(c, hipMemcpy(c->d_volumes, v, sizeof(vpx_volume) * count, hipMemcpyHostToDevice));
         VPX_HIP(c, hipMemcpy(c->d_vbounds, bounds.data(), sizeof(float4) * count, hipMemcpyHostToDevice));
     }
-    return VPX_OK;
+    return build_tlas(c, bounds);
 }
 
 int vpx_set_materials(vpx_ctx* c, const vpx_material* m, uint32_t count) {
+    VPX_GROUP_ALL(c, vpx_set_materials(m_, m, count));
     if (!c || !m) return fail(c, VPX_E_INVALID, "null argument");
     if (count == 0 || count > VPX_NUM_MATERIALS) return fail(c, VPX_E_INVALID, "material count must be 1..256");
     vpx_material full[VPX_NUM_MATERIALS];
@@ -1012,6 +1165,7 @@ int vpx_set_materials(vpx_ctx* c, const vpx_material* m, uint32_t count) {
 
 int vpx_set_lights(vpx_ctx* c, const vpx_point_light* p, uint32_t np, const vpx_spot_light* s, uint32_t ns,
                    const vpx_area_light* a, uint32_t na, const vpx_dir_light* d) {
+    VPX_GROUP_ALL(c, vpx_set_lights(m_, p, np, s, ns, a, na, d));
     if (!c) return VPX_E_INVALID;
     VPX_HIP(c, hipStreamSynchronize(c->stream));
     int rc;
@@ -1025,6 +1179,7 @@ int vpx_set_lights(vpx_ctx* c, const vpx_point_light* p, uint32_t np, const vpx_
 }
 
 int vpx_set_shapes(vpx_ctx* c, const vpx_sphere* s, uint32_t ns, const vpx_triangle* t, uint32_t nt) {
+    VPX_GROUP_ALL(c, vpx_set_shapes(m_, s, ns, t, nt));
     if (!c) return VPX_E_INVALID;
     VPX_HIP(c, hipStreamSynchronize(c->stream));
     int rc;
@@ -1036,6 +1191,7 @@ int vpx_set_shapes(vpx_ctx* c, const vpx_sphere* s, uint32_t ns, const vpx_trian
 }
 
 int vpx_set_sky(vpx_ctx* c, const float* rgb, uint32_t width, uint32_t height, float hdr_contribution) {
+    VPX_GROUP_ALL(c, vpx_set_sky(m_, rgb, width, height, hdr_contribution));
     if (!c) return VPX_E_INVALID;
     VPX_HIP(c, hipSetDevice(c->device));
     if (!rgb || !width || !height) {  // remove the texture (misses use the constant sky)
@@ -1064,14 +1220,18 @@ int vpx_set_sky(vpx_ctx* c, const float* rgb, uint32_t width, uint32_t height, f
 }
 
 int vpx_set_camera(vpx_ctx* c, const vpx_camera* cam) {
+    VPX_GROUP_ALL(c, vpx_set_camera(m_, cam));
     if (!c || !cam) return fail(c, VPX_E_INVALID, "null argument");
     c->cam = *cam;
     c->have_camera = true;
     return VPX_OK;
 }
 
+static int group_render(vpx_ctx* c, const vpx_frame_params* p, float* accum, uint32_t* rgb8, vpx_stats* stats);
+
 int vpx_render(vpx_ctx* c, const vpx_frame_params* p, float* accum, uint32_t* rgb8, vpx_stats* stats) {
     if (!c) return VPX_E_INVALID;
+    if (!c->members.empty()) return group_render(c, p, accum, rgb8, stats);
     int rc = validate_frame(c, p);
     if (rc) return rc;
     if (!accum) return fail(c, VPX_E_INVALID, "accum (device float4[W*H]) is required");
@@ -1098,6 +1258,7 @@ int vpx_render(vpx_ctx* c, const vpx_frame_params* p, float* accum, uint32_t* rg
 
 int vpx_render_reproject(vpx_ctx* c, const vpx_frame_params* p, const vpx_prev_camera* prev, float* history,
                          uint32_t* rgb8, vpx_stats* stats) {
+    VPX_GROUP_FIRST(c, vpx_render_reproject(m_, p, prev, history, rgb8, stats));
     if (!c) return VPX_E_INVALID;
     int rc = validate_frame(c, p);
     if (rc) return rc;
@@ -1182,18 +1343,21 @@ static int render_tiles_impl(int MODE, vpx_ctx* c, const vpx_frame_params* p, ui
 
 int vpx_render_tiles(vpx_ctx* c, const vpx_frame_params* p, uint32_t tile_w, uint32_t tile_h, uint32_t rank,
                      uint32_t n_ranks, float* packed, vpx_stats* stats) {
+    VPX_GROUP_FIRST(c, vpx_render_tiles(m_, p, tile_w, tile_h, rank, n_ranks, packed, stats));
     return render_tiles_impl(kFinishPackedSample, c, p, tile_w, tile_h, rank, n_ranks, nullptr, nullptr,
                                                   reinterpret_cast<float4*>(packed), stats);
 }
 
 int vpx_render_tiles_accum(vpx_ctx* c, const vpx_frame_params* p, uint32_t tile_w, uint32_t tile_h, uint32_t rank,
                            uint32_t n_ranks, float* accum_packed, uint32_t* rgb8_packed, vpx_stats* stats) {
+    VPX_GROUP_FIRST(c, vpx_render_tiles_accum(m_, p, tile_w, tile_h, rank, n_ranks, accum_packed, rgb8_packed, stats));
     return render_tiles_impl(kFinishPackedAccum, c, p, tile_w, tile_h, rank, n_ranks,
                                                  reinterpret_cast<float4*>(accum_packed), rgb8_packed, nullptr, stats);
 }
 
 int vpx_composite_rgb8(vpx_ctx* c, const vpx_frame_params* p, uint32_t tile_w, uint32_t tile_h, uint32_t n_ranks,
                        const uint32_t* gathered, uint32_t* rgb8) {
+    VPX_GROUP_FIRST(c, vpx_composite_rgb8(m_, p, tile_w, tile_h, n_ranks, gathered, rgb8));
     if (!c || !p || !gathered || !rgb8) return fail(c, VPX_E_INVALID, "null argument");
     if (tile_w != kTile || tile_h != kTile || n_ranks == 0) return fail(c, VPX_E_INVALID, "tiles must be 16x16");
     if (p->width == 0 || p->height == 0) return fail(c, VPX_E_INVALID, "empty frame");
@@ -1206,6 +1370,7 @@ int vpx_composite_rgb8(vpx_ctx* c, const vpx_frame_params* p, uint32_t tile_w, u
 
 int vpx_composite_tiles(vpx_ctx* c, const vpx_frame_params* p, uint32_t tile_w, uint32_t tile_h, uint32_t n_ranks,
                         const float* gathered, float* accum, uint32_t* rgb8) {
+    VPX_GROUP_FIRST(c, vpx_composite_tiles(m_, p, tile_w, tile_h, n_ranks, gathered, accum, rgb8));
     if (!c || !p || !gathered || !accum) return fail(c, VPX_E_INVALID, "null argument");
     if (tile_w != kTile || tile_h != kTile || n_ranks == 0) return fail(c, VPX_E_INVALID, "tiles must be 16x16");
     if (p->width == 0 || p->height == 0) return fail(c, VPX_E_INVALID, "empty frame");
@@ -1219,6 +1384,16 @@ int vpx_composite_tiles(vpx_ctx* c, const vpx_frame_params* p, uint32_t tile_w, 
 
 int vpx_get_counters(vpx_ctx* c, vpx_stats* out, int reset) {
     if (!c || !out) return fail(c, VPX_E_INVALID, "null argument");
+    if (!c->members.empty()) {  // sum over the devices
+        std::memset(out, 0, sizeof(*out));
+        return group_all(c, [&](vpx_ctx* m) {
+            vpx_stats one;
+            const int rc = vpx_get_counters(m, &one, reset);
+            out->primary_rays += one.primary_rays, out->shadow_rays += one.shadow_rays;
+            out->bounce_rays += one.bounce_rays, out->dda_cells += one.dda_cells;
+            return rc;
+        });
+    }
     unsigned long long now[kCtrWords];
     int rc = snapshot_counters(c, now);
     if (rc) return rc;
@@ -1233,6 +1408,7 @@ int vpx_get_counters(vpx_ctx* c, vpx_stats* out, int reset) {
 }
 
 int vpx_find_nearest(vpx_ctx* c, const vpx_ray* rays, uint32_t n, vpx_hit* hits) {
+    VPX_GROUP_FIRST(c, vpx_find_nearest(m_, rays, n, hits));
     if (!c || (n && (!rays || !hits))) return fail(c, VPX_E_INVALID, "null argument");
     int rc = check_ready(c);
     if (rc) return rc;
@@ -1251,6 +1427,7 @@ int vpx_find_nearest(vpx_ctx* c, const vpx_ray* rays, uint32_t n, vpx_hit* hits)
 }
 
 int vpx_is_occluded(vpx_ctx* c, const vpx_ray* rays, uint32_t n, uint8_t* occ) {
+    VPX_GROUP_FIRST(c, vpx_is_occluded(m_, rays, n, occ));
     if (!c || (n && (!rays || !occ))) return fail(c, VPX_E_INVALID, "null argument");
     int rc = check_ready(c);
     if (rc) return rc;
@@ -1270,6 +1447,7 @@ int vpx_is_occluded(vpx_ctx* c, const vpx_ray* rays, uint32_t n, uint8_t* occ) {
 
 int vpx_trace(vpx_ctx* c, const vpx_ray* rays, const uint32_t* seeds, uint32_t n, int32_t depth, const float sky[3],
               int32_t area_samples, float* radiance) {
+    VPX_GROUP_FIRST(c, vpx_trace(m_, rays, seeds, n, depth, sky, area_samples, radiance));
     if (!c || (n && (!rays || !seeds || !radiance))) return fail(c, VPX_E_INVALID, "null argument");
     if (depth < -1 || depth > kMaxLevels - 2) return fail(c, VPX_E_INVALID, "depth must be in [-1, 14]");
     if (!sky && !c->d_sky) return fail(c, VPX_E_STATE, "sky == NULL (textured sky) without vpx_set_sky");
@@ -1299,6 +1477,7 @@ int vpx_trace(vpx_ctx* c, const vpx_ray* rays, const uint32_t* seeds, uint32_t n
 }
 
 int vpx_bvh_set(vpx_ctx* c, const vpx_bvh_tri* tris, uint32_t n) {
+    VPX_GROUP_ALL(c, vpx_bvh_set(m_, tris, n));
     if (!c || (n && !tris)) return fail(c, VPX_E_INVALID, "null argument");
     if (n > VPX_BVH_MAX_TRIS) return fail(c, VPX_E_INVALID, "more triangles than VPX_BVH_MAX_TRIS");
     VPX_HIP(c, hipStreamSynchronize(c->stream));
@@ -1325,6 +1504,7 @@ int vpx_bvh_set(vpx_ctx* c, const vpx_bvh_tri* tris, uint32_t n) {
 }
 
 int vpx_bvh_intersect(vpx_ctx* c, const vpx_ray* rays, uint32_t n, float* t_out) {
+    VPX_GROUP_FIRST(c, vpx_bvh_intersect(m_, rays, n, t_out));
     if (!c || (n && (!rays || !t_out))) return fail(c, VPX_E_INVALID, "null argument");
     if (!c->d_bvh) return fail(c, VPX_E_STATE, "no BVH set (vpx_bvh_set)");
     if (n == 0) return VPX_OK;
@@ -1344,6 +1524,7 @@ int vpx_bvh_intersect(vpx_ctx* c, const vpx_ray* rays, uint32_t n, float* t_out)
 }
 
 int vpx_focus_distance(vpx_ctx* c, uint32_t width, uint32_t height, float* fd) {
+    VPX_GROUP_FIRST(c, vpx_focus_distance(m_, width, height, fd));
     if (!c || !fd || !width || !height) return fail(c, VPX_E_INVALID, "bad argument");
     int rc = check_ready(c);
     if (rc) return rc;
@@ -1364,15 +1545,152 @@ uint32_t vpx_pixel_seed(uint32_t base, uint32_t frame, uint32_t w, uint32_t h, u
     return pixel_seed(base, frame, w, h, x, y);
 }
 
+
+// ------------------------------------------------------------------ device sets
+// One frame on a device set (vpx_create_multi): the 16x16 tiles are dealt round-robin to
+// the members (tile t -> member t % n, as dist.py deals them to ranks), each member renders
+// its tiles on its own device and stream, and the packed results are gathered to member 0
+// over RCCL (grouped ncclSend / ncclRecv: n - 1 point-to-point transfers into device 0,
+// each on its own xGMI link on an MI355X node) — or by device copies when the set repeats
+// a device (RCCL communicators need distinct devices).  Member 0 then composites:
+//   accum != NULL: float4 samples (16 B/pixel) -> vpx_composite_tiles into the caller's
+//     accumulator + screen, bit-identical to vpx_render on one device;
+//   accum == NULL: each member keeps the running average of ITS tiles (sharded
+//     accumulator, reset by frame_index 0) and only packed RGB8 (4 B/pixel) travels ->
+//     vpx_composite_rgb8 into the screen.
+static int group_render(vpx_ctx* c, const vpx_frame_params* p, float* accum, uint32_t* rgb8, vpx_stats* stats) {
+    if (!p) return fail(c, VPX_E_INVALID, "null params");
+    if (!accum && !rgb8) return fail(c, VPX_E_INVALID, "accum or rgb8 (device pointers on the first device) required");
+    const uint32_t n = (uint32_t)c->members.size();
+    const uint64_t L = vpx_tiles_packed_len(p->width, p->height, kTile, kTile, n);
+    if (!L) return fail(c, VPX_E_INVALID, "empty frame");
+    const bool samples = accum != nullptr;
+    const size_t elem = samples ? sizeof(float4) : sizeof(uint32_t);
+    int rc;
+    if (c->g_len < L) {  // (re)size the per-member buffers
+        for (uint32_t r = 0; r < n; ++r) {
+            vpx_ctx* m = c->members[r];
+            VPX_HIP(c, hipSetDevice(m->device));
+            VPX_HIP(c, hipStreamSynchronize(m->stream));
+            if (c->g_packed[r]) (void)hipFree(c->g_packed[r]);
+            if (c->g_accum[r]) (void)hipFree(c->g_accum[r]);
+            c->g_packed[r] = nullptr, c->g_accum[r] = nullptr;
+            VPX_HIP(c, hipMalloc(&c->g_packed[r], sizeof(float4) * L));
+            VPX_HIP(c, hipMalloc((void**)&c->g_accum[r], sizeof(float4) * L));
+            VPX_HIP(c, hipMemsetAsync(c->g_accum[r], 0, sizeof(float4) * L, m->stream));
+            if (r == 0) {
+                if (c->g_gathered) (void)hipFree(c->g_gathered);
+                c->g_gathered = nullptr;
+                VPX_HIP(c, hipMalloc(&c->g_gathered, sizeof(float4) * L * n));
+            }
+        }
+        c->g_len = L;
+    }
+    vpx_ctx* m0 = c->members[0];
+    if (stats) std::memset(stats, 0, sizeof(*stats));
+    // 1. every member renders its tiles (launches are asynchronous: the devices overlap)
+    for (uint32_t r = 0; r < n; ++r) {
+        vpx_ctx* m = c->members[r];
+        VPX_HIP(c, hipSetDevice(m->device));
+        if (c->comms.empty())  // copy path: the previous frame's copy of this buffer is done
+            VPX_HIP(c, hipStreamWaitEvent(m->stream, c->g_copied, 0));
+        vpx_stats one;
+        rc = samples ? vpx_render_tiles(m, p, kTile, kTile, r, n, (float*)c->g_packed[r], stats ? &one : nullptr)
+                     : vpx_render_tiles_accum(m, p, kTile, kTile, r, n, c->g_accum[r], (uint32_t*)c->g_packed[r],
+                                              stats ? &one : nullptr);
+        if (rc) return fail(c, rc, "device " + std::to_string(m->device) + ": " + m->err);
+        if (stats) {
+            stats->primary_rays += one.primary_rays, stats->shadow_rays += one.shadow_rays;
+            stats->bounce_rays += one.bounce_rays, stats->dda_cells += one.dda_cells;
+            stats->kernel_ms = std::max(stats->kernel_ms, one.kernel_ms);
+        }
+        if (c->comms.empty()) VPX_HIP(c, hipEventRecord(c->g_ev[r], m->stream));
+    }
+    // 2. gather the packed buffers to member 0
+    char* dst = (char*)c->g_gathered;
+    const size_t bytes = elem * L;
+    if (!c->comms.empty()) {
+        VPX_HIP(c, hipSetDevice(m0->device));
+        VPX_HIP(c, hipMemcpyAsync(dst, c->g_packed[0], bytes, hipMemcpyDeviceToDevice, m0->stream));
+        if (ncclGroupStart() != ncclSuccess) return fail(c, VPX_E_DEVICE, "ncclGroupStart");
+        for (uint32_t r = 1; r < n; ++r) {
+            if (ncclRecv(dst + bytes * r, bytes, ncclChar, (int)r, c->comms[0], m0->stream) != ncclSuccess ||
+                ncclSend(c->g_packed[r], bytes, ncclChar, 0, c->comms[r], c->members[r]->stream) != ncclSuccess) {
+                (void)ncclGroupEnd();
+                return fail(c, VPX_E_DEVICE, "RCCL gather");
+            }
+        }
+        if (ncclGroupEnd() != ncclSuccess) return fail(c, VPX_E_DEVICE, "ncclGroupEnd");
+    } else {
+        VPX_HIP(c, hipSetDevice(m0->device));
+        for (uint32_t r = 0; r < n; ++r) {
+            vpx_ctx* m = c->members[r];
+            VPX_HIP(c, hipStreamWaitEvent(m0->stream, c->g_ev[r], 0));
+            VPX_HIP(c, hipMemcpyPeerAsync(dst + bytes * r, m0->device, c->g_packed[r], m->device, bytes, m0->stream));
+        }
+        VPX_HIP(c, hipEventRecord(c->g_copied, m0->stream));
+    }
+    // 3. member 0 composites into the caller's buffers
+    rc = samples ? vpx_composite_tiles(m0, p, kTile, kTile, n, (const float*)dst, accum, rgb8)
+                 : vpx_composite_rgb8(m0, p, kTile, kTile, n, (const uint32_t*)dst, rgb8);
+    if (rc) return fail(c, rc, m0->err);
+    if (stats) stats->total_ms = stats->kernel_ms;
+    return VPX_OK;
+}
+
+int vpx_create_multi(const int* devices, int ndev, vpx_ctx** out) {
+    if (!out) return VPX_E_INVALID;
+    *out = nullptr;
+    if (!devices || ndev < 1 || ndev > 64) return VPX_E_INVALID;
+    vpx_ctx* c = new (std::nothrow) vpx_ctx();
+    if (!c) return VPX_E_NOMEM;
+    c->device = devices[0];
+    bool distinct = true;
+    for (int r = 0; r < ndev; ++r) {
+        for (int q = 0; q < r; ++q) distinct &= devices[q] != devices[r];
+        vpx_ctx* m = nullptr;
+        const int rc = vpx_create(devices[r], &m);
+        if (rc) {
+            vpx_destroy(c);
+            return rc;
+        }
+        c->members.push_back(m);
+        c->g_packed.push_back(nullptr);
+        c->g_accum.push_back(nullptr);
+        c->g_ev.push_back(nullptr);
+        if (hipEventCreateWithFlags(&c->g_ev.back(), hipEventDisableTiming) != hipSuccess) {
+            vpx_destroy(c);
+            return VPX_E_DEVICE;
+        }
+    }
+    (void)hipSetDevice(devices[0]);
+    if (hipEventCreateWithFlags(&c->g_copied, hipEventDisableTiming) != hipSuccess) {
+        vpx_destroy(c);
+        return VPX_E_DEVICE;
+    }
+    if (distinct && ndev > 1) {  // one RCCL communicator per device, all in this process
+        c->comms.assign(ndev, nullptr);
+        if (ncclCommInitAll(c->comms.data(), ndev, devices) != ncclSuccess) {
+            c->comms.clear();
+            vpx_destroy(c);
+            return VPX_E_DEVICE;
+        }
+    }
+    *out = c;
+    return VPX_OK;
+}
+
 }  // extern "C"
 
 extern "C" int vpx_profile_select(vpx_ctx* c, uint32_t stage_mask) {
+    VPX_GROUP_FIRST(c, vpx_profile_select(m_, stage_mask));
     if (!c) return VPX_E_INVALID;
     c->prof_mask = stage_mask;
     return VPX_OK;
 }
 
 extern "C" int vpx_profile_enable(vpx_ctx* c, uint32_t max_launches) {
+    VPX_GROUP_FIRST(c, vpx_profile_enable(m_, max_launches));
     if (!c) return VPX_E_INVALID;
     VPX_HIP(c, hipStreamSynchronize(c->stream));
     for (hipEvent_t e : c->prof_ev) (void)hipEventDestroy(e);
@@ -1389,6 +1707,7 @@ extern "C" int vpx_profile_enable(vpx_ctx* c, uint32_t max_launches) {
 }
 
 extern "C" int vpx_profile_read(vpx_ctx* c, vpx_profile* out, int reset) {
+    VPX_GROUP_FIRST(c, vpx_profile_read(m_, out, reset));
     if (!c || !out) return fail(c, VPX_E_INVALID, "null argument");
     std::memset(out, 0, sizeof(*out));
     unsigned long long now[kCtrWords];

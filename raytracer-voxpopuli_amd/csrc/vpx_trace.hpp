@@ -45,10 +45,28 @@ struct DevGrid {
     uint32_t nb3;  // macro parents per axis (l2 blocking) = ceil(nb2 / 4)
 };
 
+// Instance TLAS over the world bounds of volumes 1..n-1 (built on the host by vpx_set_volumes
+// for 2..kTlasMaxVolumes volumes: the world volume 0 and up to 64 instances, C4's scene).
+// Nodes in depth-first order, stackless: an interior node continues at i + 1 when its box
+// is hit and at `skip` (the node after its subtree) when missed; a leaf holds the bit mask
+// of its volumes (bit k = volume k + 1).
+constexpr uint32_t kTlasMaxVolumes = 65;
+constexpr uint32_t kTlasMaxNodes = 64;
+struct TlasNode {
+    float lo[3];
+    uint32_t skip;
+    float hi[3];
+    uint32_t leaf;
+    uint64_t mask;
+};
+
 struct SceneView {
     const DevGrid* grids;
     const vpx_volume* volumes;
     const float4* vbounds;  // per volume: world bounding sphere (xyz centre, w radius^2), inflated
+    const TlasNode* tlas;   // instance TLAS (global memory; the multi-volume kernels stage it in LDS)
+    uint32_t tlas_on, tlas_nodes;
+    uint64_t tlas_always;   // instances outside the tree (no finite bounds): always candidates
     const vpx_material* materials;
     const vpx_point_light* points;
     const vpx_spot_light* spots;
@@ -637,6 +655,67 @@ __device__ __forceinline__ bool misses_volume(const float4 b, f3 o, f3 d) {
     return outside && (bb < 0.0f || bb * bb < (oc2 - b.w) * dd);
 }
 
+// Conservative slab test of a TLAS box against the segment o + t d, 0 <= t <= bound: a NaN
+// slab (0 * inf on an axis the ray runs along a box face) never rejects.  A volume whose
+// box starts beyond `bound` is not a candidate: its cube entry lies beyond it too (the box
+// holds the cube with a margin far above float rounding), so the reference's walk of that
+// volume ends before its first cell (`while (s.t < ray.t)`, scene.cpp:761, 1015).
+__device__ __forceinline__ bool tlas_box(const TlasNode& nd, f3 o, f3 inv, float bound) {
+    float t0 = 0.0f, t1 = bound;
+    const float ta[3] = {(nd.lo[0] - o.x) * inv.x, (nd.lo[1] - o.y) * inv.y, (nd.lo[2] - o.z) * inv.z};
+    const float tb[3] = {(nd.hi[0] - o.x) * inv.x, (nd.hi[1] - o.y) * inv.y, (nd.hi[2] - o.z) * inv.z};
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        t0 = fmaxf(t0, fminf(ta[k], tb[k]));
+        t1 = fminf(t1, fmaxf(ta[k], tb[k]));
+    }
+    return !(t1 < t0);
+}
+
+// The volume loop of Renderer::FindNearest / IsOccluded over the TLAS.  Volume 0 (the world,
+// first in the reference's order) is walked by every lane first; then the wave traverses the
+// tree once, wave-uniform (a node is entered when any lane's segment reaches its box: the
+// ray packet of a 16x4 pixel strip), each lane collecting the leaves IT reaches before its
+// bound as it stands after volume 0.  Every volume whose walk the reference would start and
+// read a cell of is among them (boxes hold the inflated bounding spheres of misses_volume,
+// and a box starting beyond the bound holds a cube whose walk ends before its first cell,
+// `while (s.t < ray.t)`, scene.cpp:761, 1015).  The wave then walks the union of the lanes'
+// candidates in increasing index order, each lane only its own — the linear loop restricted
+// to volumes some lane can reach, one call site of the walk.  body(i) returns false to end
+// the lane's loop (IsOccluded's first occluder).
+template <class Body>
+__device__ __forceinline__ void for_volumes(const SceneView& sv, f3 o, f3 d, const float& bound, Body body) {
+    bool live = true, first = true;
+    uint64_t mine = 0, any = 0;  // this lane's / the wave's candidates, bit k = volume k + 1
+    for (;;) {
+        uint32_t i = 0;
+        if (!first) {
+            if (!any) break;
+            i = (uint32_t)__ffsll((unsigned long long)any);
+            any &= any - 1;
+        }
+        if (live && (first || ((mine >> (i - 1u)) & 1u))) live = body(i);
+        if (first) {
+            first = false;
+            mine = sv.tlas_always;
+            any = sv.tlas_always;
+            const f3 inv = mk(__fdiv_rn(1.0f, d.x), __fdiv_rn(1.0f, d.y), __fdiv_rn(1.0f, d.z));
+            for (uint32_t n = 0; n < sv.tlas_nodes;) {
+                const TlasNode nd = sv.tlas[n];
+                const bool h = live && tlas_box(nd, o, inv, bound);
+                const bool wave_h = __ballot(h) != 0;
+                if (nd.leaf) {
+                    if (h) mine |= nd.mask;
+                    if (wave_h) any |= nd.mask;
+                    ++n;
+                } else {
+                    n = wave_h ? n + 1 : nd.skip;
+                }
+            }
+        }
+    }
+}
+
 // Renderer::FindNearest, renderer.cpp:946-1018.  Linear loop over the volumes with the
 // SSE transforms; a later volume wins only with a strictly smaller t (ties -> lowest index).
 // The winner's normal and material are formed once after the loop (the reference forms
@@ -647,8 +726,8 @@ __device__ __forceinline__ int32_t find_nearest(const SceneView& sv, Ray& r, Cou
     int32_t vox = -2;
     ++k.nearest;
     uint32_t hx = 0, hy = 0, hz = 0;  // hit cell in volume `vox`
-    for (uint32_t i = 0; i < sv.num_volumes; ++i) {
-        if (misses_volume(sv.vbounds[i], r.O, r.D)) continue;  // Setup3DDDA would fail
+    auto visit = [&](uint32_t i) {
+        if (misses_volume(sv.vbounds[i], r.O, r.D)) return true;  // Setup3DDDA would fail
         const vpx_volume& vol = sv.volumes[i];
         const DevGrid g = sv.grids[vol.grid_id];
         skip::Walk w;
@@ -658,7 +737,7 @@ __device__ __forceinline__ int32_t find_nearest(const SceneView& sv, Ray& r, Cou
             o.D = xform_vec_ssem(r.D, vol.inv_matrix);
             o.rD = mk(__fdiv_rn(1.0f, o.D.x), __fdiv_rn(1.0f, o.D.y), __fdiv_rn(1.0f, o.D.z));
             Dda s;
-            if (!dda_setup(vol, g.n, o, s)) continue;
+            if (!dda_setup(vol, g.n, o, s)) return true;
             w = to_walk(s);
         }
         if (walk_wave<0, SKIPW, MINC>(grid_view(g), w, r.t, k.cells)) {
@@ -666,7 +745,14 @@ __device__ __forceinline__ int32_t find_nearest(const SceneView& sv, Ray& r, Cou
             hx = w.X, hy = w.Y, hz = w.Z;
             vox = (int32_t)i;
         }
-    }
+        return true;
+    };
+    // with the TLAS, volume 0 (the world, first in the reference's order) is walked before
+    // the tree is asked, so the instances' candidates are bounded by its hit
+    if (sv.tlas_on)
+        for_volumes(sv, r.O, r.D, r.t, visit);
+    else
+        for (uint32_t i = 0; i < sv.num_volumes; ++i) visit(i);
     if (vox >= 0) {
         const vpx_volume& vol = sv.volumes[vox];
         const DevGrid g = sv.grids[vol.grid_id];
@@ -691,10 +777,14 @@ __device__ __forceinline__ int32_t find_nearest(const SceneView& sv, Ray& r, Cou
     return vox;
 }
 
+#ifndef VPX_TLAS_SHADOW
+#define VPX_TLAS_SHADOW 0  // measured C4 IsOccluded: 2.67 ms through the TLAS vs 2.57 linear
+#endif
 // Renderer::IsOccluded, renderer.cpp:209-243 (scalar transforms, exact 1/D).
 __device__ __forceinline__ bool is_occluded(const SceneView& sv, const Ray& r, Counters& k) {
-    for (uint32_t i = 0; i < sv.num_volumes; ++i) {
-        if (misses_volume(sv.vbounds[i], r.O, r.D)) continue;  // Setup3DDDA would fail
+    bool occ = false;
+    auto visit = [&](uint32_t i) {
+        if (misses_volume(sv.vbounds[i], r.O, r.D)) return true;  // Setup3DDDA would fail
         const vpx_volume& vol = sv.volumes[i];
         ORay o;
         o.O = xform_pos(r.O, vol.inv_matrix);
@@ -702,10 +792,17 @@ __device__ __forceinline__ bool is_occluded(const SceneView& sv, const Ray& r, C
         o.rD = mk(__fdiv_rn(1.0f, o.D.x), __fdiv_rn(1.0f, o.D.y), __fdiv_rn(1.0f, o.D.z));
         const DevGrid g = sv.grids[vol.grid_id];
         Dda s;
-        if (!dda_setup(vol, g.n, o, s)) continue;
+        if (!dda_setup(vol, g.n, o, s)) return true;
         skip::Walk w = to_walk(s);
-        if (walk_wave<16, VPX_SKIPW_SHADOW, VPX_MINC_SHADOW>(grid_view(g), w, r.t, k.cells)) return true;  // first solid cell, t < bound
-    }
+        // first solid cell with t < bound: occluded, the reference returns (no later volume)
+        occ = walk_wave<16, VPX_SKIPW_SHADOW, VPX_MINC_SHADOW>(grid_view(g), w, r.t, k.cells);
+        return !occ;
+    };
+    if (VPX_TLAS_SHADOW && sv.tlas_on)
+        for_volumes(sv, r.O, r.D, r.t, visit);
+    else
+        for (uint32_t i = 0; i < sv.num_volumes && !occ; ++i) visit(i);
+    if (occ) return true;
     for (uint32_t i = 0; i < sv.num_spheres; ++i)
         if (sphere_is_hit(sv.spheres[i], r)) return true;
     for (uint32_t i = 0; i < sv.num_triangles; ++i)

@@ -495,6 +495,22 @@ __global__ __launch_bounds__(256) void k_resolve(SceneView sv, WaveBufs w) {
 
 #define VPX_WPE(n) __attribute__((amdgpu_waves_per_eu(n)))
 
+// The multi-volume kernels read the instance TLAS (vpx_trace.hpp TlasNode) from LDS: one
+// copy per workgroup (<= 2.5 KiB); the wave-uniform traversal then broadcasts each node
+// from LDS to its lanes.  Called by every thread.
+#ifndef VPX_TLAS_LDS
+#define VPX_TLAS_LDS 0  // measured: C4 FindNearest 1.70 ms from LDS vs 1.68 with scalar loads; IsOccluded 2.81 vs 2.68
+#endif
+__device__ __forceinline__ void stage_tlas(SceneView& sv) {
+    __shared__ TlasNode s_nodes[kTlasMaxNodes];
+    if (!VPX_TLAS_LDS || !sv.tlas_on) return;  // kernel argument: uniform
+    const uint32_t words = sv.tlas_nodes * (uint32_t)(sizeof(TlasNode) / 4);
+    for (uint32_t i = threadIdx.x; i < words; i += blockDim.x)
+        reinterpret_cast<uint32_t*>(s_nodes)[i] = reinterpret_cast<const uint32_t*>(sv.tlas)[i];
+    __syncthreads();
+    sv.tlas = s_nodes;
+}
+
 // One 256-thread workgroup per 16x16 tile.  Work is compacted inside the tile through LDS
 // (no global atomics), so a DDA wave only carries rays that will actually march, and the
 // waves of a sparse tile retire at once.
@@ -579,6 +595,7 @@ __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_NEAREST : VPX_WPE_MULTI_
                                                  unsigned long long* __restrict__ ctr) {
     __shared__ uint32_t sh[4];
     __shared__ uint32_t lst[256];
+    if (!ONE) stage_tlas(sv);
     const uint32_t p = blockIdx.x * 256u + threadIdx.x;
     Counters k{0u, 0u, 0u};
     uint32_t prim = 0;
@@ -683,6 +700,7 @@ __device__ __forceinline__ uint32_t group_scan(const uint32_t (&cnt)[G], uint32_
 // Renderer::FindNearest for the active paths of G tiles (bounce levels).
 template <bool ONE>
 __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_NEAREST : VPX_WPE_MULTI_NEAREST) void k_nearest_tile(SceneView sv, WaveBufs w, unsigned long long* __restrict__ ctr) {
+    if (!ONE) stage_tlas(sv);
     __shared__ uint32_t sh[4];
     __shared__ uint32_t lst[256 * kGroupTiles];
     const uint32_t base = blockIdx.x * 256u * kGroupTiles;
@@ -776,6 +794,7 @@ __device__ __forceinline__ void shadow_tile(const SceneView& sv, const WaveBufs&
 
 template <bool ONE>
 __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_SHADOW : VPX_WPE_MULTI_SHADOW) void k_shadow_tile(SceneView sv, WaveBufs w, unsigned long long* __restrict__ ctr) {
+    if (!ONE) stage_tlas(sv);
     shadow_tile<ONE>(sv, w, ctr);
 }
 
@@ -874,6 +893,7 @@ template <bool ONE, int MODE>
 __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_SHADOW : VPX_WPE_MULTI_SHADOW) void k_shadow_finish(
     SceneView sv, FrameArgs f, WaveBufs w, unsigned long long* __restrict__ ctr, float4* __restrict__ accum,
     uint32_t* __restrict__ rgb8, float4* __restrict__ packed) {
+    if (!ONE) stage_tlas(sv);
     shadow_tile<ONE>(sv, w, ctr);
     __syncthreads();
     const uint32_t p = blockIdx.x * 256u + threadIdx.x;

@@ -7,9 +7,11 @@
 //   ground slab y < 2 -> material 0; pillar cells where (x & 15) < 8 and (z & 15) < 8 and
 //   y < 2 + h, h = ((x >> 4) * 7 + (z >> 4) * 13) % 5 * n / 16 -> material 16 + (h % 4).
 //
-// usage: vpx_demo [n] [width] [height] [frames] [max_bounces] [out.rgb8] [mode]
+// usage: vpx_demo [n] [width] [height] [frames] [max_bounces] [out.rgb8] [mode] [devices]
 //   mode: letters — 's' staticCamera (the reprojection branch of Tick), 'k' activateSky
-//   with the demo sky texture (demo_sky below; tests rebuild it with numpy).
+//   with the demo sky texture (demo_sky below; tests rebuild it with numpy); '-' none.
+//   devices: comma-separated HIP devices, e.g. 0,1,2,3 — a device set (vpx_create_multi:
+//   tiles over the devices, RCCL gather to the first); default: device 0 alone.
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -66,8 +68,15 @@ int main(int argc, char** argv) {
     const char* mode = argc > 7 ? argv[7] : "";
     bool is_static = false, sky = false;
     for (const char* m = mode; *m; ++m) is_static |= *m == 's', sky |= *m == 'k';
+    std::vector<int> devices;
+    if (argc > 8)
+        for (const char* d = argv[8]; *d;) {
+            devices.push_back(atoi(d));
+            while (*d && *d != ',') ++d;
+            if (*d == ',') ++d;
+        }
 
-    vpxhost::Renderer r(0);
+    vpxhost::Renderer r = devices.empty() ? vpxhost::Renderer(0) : vpxhost::Renderer(devices);
     CHECK(r.Init(W, H));
     const std::vector<uint8_t> grid = pillars(n);
     CHECK(r.UploadGrid(0, grid.data(), n));

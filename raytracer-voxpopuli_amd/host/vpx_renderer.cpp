@@ -7,6 +7,10 @@ namespace vpxhost {
 
 Renderer::Renderer(int device) : device_(device) { status_ = vpx_create(device, &ctx_); }
 
+Renderer::Renderer(const std::vector<int>& devices) : device_(devices.empty() ? 0 : devices[0]) {
+    status_ = devices.empty() ? VPX_E_INVALID : vpx_create_multi(devices.data(), (int)devices.size(), &ctx_);
+}
+
 Renderer::~Renderer() {
     if (accumulator_) (void)hipFree(accumulator_);
     if (screen_) (void)hipFree(screen_);

@@ -23,6 +23,9 @@ namespace vpxhost {
 class Renderer {
 public:
     explicit Renderer(int device = 0);
+    // A device set (vpx_create_multi): frames tile-sharded over `devices`, gathered over
+    // RCCL to devices[0], where the accumulator and screen live.
+    explicit Renderer(const std::vector<int>& devices);
     ~Renderer();
     Renderer(const Renderer&) = delete;
     Renderer& operator=(const Renderer&) = delete;

@@ -227,6 +227,42 @@ def test_sharded_accumulator_equals_monolithic(pkg, orc):
     ctx.close()
 
 
+@pytest.mark.parametrize("devices", [[0], [0, 0], [0, 0, 0, 0]])
+def test_device_set_equals_single_device(pkg, orc, devices):
+    """vpx_create_multi: the frame's tiles dealt over the members, gathered to devices[0]
+    and composited there.  With an accumulator (float4 samples travel) the accumulator and
+    screen equal vpx_render's bit for bit over 3 AA frames at depth 1 with area lights; with
+    accum = NULL (members keep their tiles' running averages, RGB8 travels) the screen
+    does; the summed counters equal one device's."""
+    sc = pkg.scene
+    desc = sc.city_scene("monu3", 128, 100, 70, 1, areas=sc.C3_AREAS[:2])
+    desc.flags = pkg.abi.VPX_FLAG_AA
+    acc_ref, rgb_ref, st_ref = render_gpu(pkg, desc, frames=3)
+    ctx = pkg.context.Context(devices=devices)
+    ctx.load_scene(desc)
+    W, H = desc.width, desc.height
+    acc = torch.zeros(W * H * 4, dtype=torch.float32, device="cuda")
+    rgb = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+    rgb2 = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    ctx.counters(reset=True)
+    for f in range(3):
+        st = ctx.render(desc.frame_params(f), acc.data_ptr(), rgb.data_ptr(), stats=True)
+    ctx.synchronize()
+    assert np.array_equal(bits(acc.cpu().numpy().reshape(-1, 4)), bits(acc_ref))
+    assert np.array_equal(rgb.cpu().numpy().view(np.uint32), rgb_ref)
+    s, r = st, st_ref[-1]
+    assert (s.primary_rays, s.shadow_rays, s.bounce_rays, s.dda_cells) == (
+        r.primary_rays, r.shadow_rays, r.bounce_rays, r.dda_cells)
+    for f in range(3):
+        ctx.render(desc.frame_params(f), 0, rgb2.data_ptr())
+    ctx.synchronize()
+    assert np.array_equal(rgb2.cpu().numpy().view(np.uint32), rgb_ref)
+    tot = ctx.counters()
+    assert tot.primary_rays == 6 * W * H
+    ctx.close()
+
+
 def test_sharded_accum_frame_refuses_a_foreign_stream(pkg):
     """RCCL orders the gather after torch's current stream, so the sharded flow refuses a
     context that renders on another stream instead of gathering stale RGB8."""
@@ -321,6 +357,48 @@ def test_volume_cull_grazing_rays(pkg, orc):
     ctx.close()
 
 
+@pytest.mark.parametrize("n_inst", [40, 64, 100])
+def test_instance_tlas_many_volumes(pkg, orc, n_inst):
+    """The instance TLAS (vpx_set_volumes builds it for 2..65 volumes; 101 volumes take the
+    linear loop): a world volume plus a lattice of rotated, scaled instances (C4's shape),
+    an exact duplicate (tie -> lowest index) and a degenerate scale-0 volume (no finite
+    bounds: always a candidate).  Hits, cell counts, occlusion and a frame with area lights
+    (the multi-volume kernels read the TLAS from LDS) equal the oracle's linear loop."""
+    sc, abi = pkg.scene, pkg.abi
+    desc = sc.model_scene("monu3", 64, 48, 40, 1, city_lights=True)
+    size, vox, _ = sc.load_model("monu3")
+    desc.grids.append(sc.GridSpec(n=32, dense=sc.load_model_grid(size, vox, 32)))
+    rng = np.random.default_rng(n_inst)
+    vols = [sc.volume()]
+    for k in range(n_inst - 2):
+        i, j, l = k % 5, (k // 5) % 5, k // 25
+        pos = (0.2 * i - 0.4, 0.55 + 0.2 * j, 0.2 * l - 0.4)
+        vols.append(sc.volume(pos, tuple(rng.uniform(0.05, 0.15, 3)), tuple(rng.uniform(-3, 3, 3)), grid_id=1))
+    vols.append(vols[5])  # duplicate of volume 5: equal t, the lower index wins
+    vols.append(sc.volume((0.3, 0.3, 0.3), (0.0, 0.1, 0.1), (0.0, 0.0, 0.0), grid_id=1))  # singular
+    desc.volumes = (abi.Volume * len(vols))(*vols)
+    desc.areas = [sc.area_light((0.5, 2.0, 0.5), radius=0.4)]
+    ctx = make_ctx(pkg, desc)
+    o = orc.Oracle(pkg.abi, desc)
+    org, dirs = random_rays(4096, 17)
+    cen = np.array([np.array(v.matrix, np.float64).reshape(4, 4) @ [0.5, 0.5, 0.5, 1.0] for v in vols])[:, :3]
+    org2 = rng.uniform(-1.5, 2.5, (2048, 3))
+    dirs2 = cen[rng.integers(1, len(vols), 2048)] - org2 + rng.normal(0, 0.02, (2048, 3))
+    org, dirs = np.concatenate([org, org2]).astype(np.float32), np.concatenate([dirs, dirs2]).astype(np.float32)
+    rays = pkg.context.make_rays(org, dirs)
+    g = cmp_hits(pkg, ctx.find_nearest(rays), o.find_nearest(rays), len(rays))
+    assert (g["vox_index"] >= 1).sum() > 200
+    srays = pkg.context.make_rays(org, dirs, tmax=rng.uniform(0.05, 4.0, len(org)))
+    occ_o, _ = o.is_occluded(srays)
+    assert np.array_equal(ctx.is_occluded(srays), occ_o)
+    ctx.close()
+    acc_g, rgb_g, st = render_gpu(pkg, desc)
+    acc_o, rgb_o, ost = o.render(desc.frame_params(0))
+    assert np.array_equal(bits(acc_g), bits(acc_o)) and np.array_equal(rgb_g, rgb_o)
+    s = st[0]
+    assert (s.shadow_rays, s.bounce_rays, s.dda_cells) == (ost.shadow_rays, ost.bounce_rays, ost.dda_cells)
+
+
 @pytest.mark.parametrize("n", [64, 1, 7, 512])
 def test_bvh_intersect(pkg, orc, n):
     """BasicBVH::IntersectBVH on the device (LDS-staged tree, explicit stack) equals the
@@ -392,9 +470,13 @@ def test_degenerate_worlds(pkg, orc, fill):
     assert np.array_equal(bits(acc_g), bits(acc_o)) and np.array_equal(rgb_g, rgb_o)
 
 
-def test_cpp_host_demo_matches_oracle(pkg, orc, tmp_path):
+@pytest.mark.parametrize("devices", [None, "0", "0,0,0"])
+def test_cpp_host_demo_matches_oracle(pkg, orc, tmp_path, devices):
     """The C++ host mirror (host/vpx_renderer.cpp via host/vpx_demo) drives the C-ABI like the
-    integrated game loop would: 3 accumulated frames, depth 1, equal to the oracle."""
+    integrated game loop would: 3 accumulated frames, depth 1, equal to the oracle — on one
+    device, and through a device set (vpx_create_multi; this box has one GPU, so the sets
+    are {0} and three members on device 0, which gather by device copies: the RCCL path of
+    distinct devices is unmeasured here)."""
     import subprocess
 
     exe = os.path.join(os.path.dirname(pkg.__file__), "host", "vpx_demo")
@@ -402,8 +484,8 @@ def test_cpp_host_demo_matches_oracle(pkg, orc, tmp_path):
         pytest.fail("host/vpx_demo missing: run __graft_entry__.build()")
     n, w, h, frames, depth = 64, 96, 64, 3, 1
     out = tmp_path / "frame.rgb8"
-    r = subprocess.run([exe, str(n), str(w), str(h), str(frames), str(depth), str(out)], capture_output=True,
-                       text=True, timeout=300)
+    args = [exe, str(n), str(w), str(h), str(frames), str(depth), str(out)] + (["-", devices] if devices else [])
+    r = subprocess.run(args, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
     rgb_cpp = np.fromfile(out, np.uint32)
     desc = pkg.scene.pillars_scene(n, w, h, depth)
