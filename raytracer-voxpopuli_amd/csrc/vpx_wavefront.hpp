@@ -74,7 +74,7 @@ struct WaveBufs {
     float4* SD;    // [S][P] shadow direction, w = slot flags bits
     float4* SL;    // [S][P] unoccluded contribution of the slot
     float4* SM;    // [P] pending light: xyz = kd (area), w = bits(kind | discard<<3 | count<<4 | level<<8 | lc<<16)
-    uint32_t* smask;  // [P] shadow slots emitted this level (bit s = slot s)
+    uint32_t* smask;  // [P] shadow slots emitted this level (bit s = slot s, s < 15) | light key << 16
     float4* RD;    // [W*H] reprojection: level-0 intersection point, w = material bits (image order)
     uint32_t P;    // paths (pixels) this call
     uint32_t S;    // shadow slots per path
@@ -158,6 +158,12 @@ __device__ __forceinline__ void put_slot(const WaveBufs& w, uint32_t s, uint32_t
     w.SL[i] = make_float4(val.x, val.y, val.z, 0.f);
 }
 
+// Light keys of the shadow-list buckets (the light index modulo this): a tile's shadow rays
+// are walked grouped by the light they go to, so a wave's lanes head the same way and read
+// the same distance-field words.
+constexpr uint32_t kLightKeys = 16;
+constexpr uint32_t kSlotBits = 0x7fffu;  // smask: slots 0..14 (area_samples <= 15)
+
 // Renderer::Illumination (renderer.cpp:738-764) up to the IsOccluded calls: draws the
 // light index (and the area-light sample directions), computes each shadow ray exactly as
 // the evaluators build it, and the contribution it adds when unoccluded.  Returns the
@@ -240,6 +246,8 @@ __device__ __forceinline__ uint32_t emit_illumination(const SceneView& sv, const
             slots |= 1u;
         }
     }
+    // every slot of this call goes to light `idx`: the tile's shadow list is bucketed by it
+    if (slots) slots |= ((uint32_t)idx & (kLightKeys - 1u)) << 16;
     return kind | (discard ? 8u : 0u) | (count << 4) | ((uint32_t)lc << 16);
 }
 
@@ -733,6 +741,9 @@ __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_NEAREST : VPX_WPE_MULTI_
     flush_counters(k, 0u, ctr, VPX_STAGE_BOUNCE);
 }
 
+#ifndef VPX_SHADOW_BUCKETS
+#define VPX_SHADOW_BUCKETS 1
+#endif
 // Renderer::IsOccluded for the shadow slots of G tiles (entry = slot << 27 | path); sets
 // the slot's occluded flag.  The light sums are formed in slot order by k_resolve.
 template <bool ONE>
@@ -741,11 +752,46 @@ __device__ __forceinline__ void shadow_tile(const SceneView& sv, const WaveBufs&
     extern __shared__ uint32_t lst_dyn[];  // [S * 256 * G]
     const uint32_t base = blockIdx.x * 256u * kGroupTiles;
     Counters k{0u, 0u, 0u};
+#if VPX_SHADOW_BUCKETS
+    // counting sort of the tile's slots by light key: LDS histogram (the order inside a
+    // bucket is whatever the atomics give — it only orders independent walks), bucket
+    // offsets from one wave's prefix sum, then the scatter
+    __shared__ uint32_t hist[kLightKeys];
+    if (threadIdx.x < kLightKeys) hist[threadIdx.x] = 0u;
+    __syncthreads();
+    uint32_t m[kGroupTiles], key[kGroupTiles], pos[kGroupTiles];
+#pragma unroll
+    for (uint32_t g = 0; g < kGroupTiles; ++g) {
+        const uint32_t p = base + threadIdx.x * kGroupTiles + g;
+        const uint32_t sm = p < w.P ? w.smask[p] : 0u;
+        m[g] = sm & kSlotBits;
+        key[g] = sm >> 16;
+        pos[g] = m[g] ? atomicAdd(&hist[key[g]], (uint32_t)__popc(m[g])) : 0u;
+    }
+    __syncthreads();
+    uint32_t total = 0;
+    if (threadIdx.x < 64) {
+        const uint32_t v = threadIdx.x < kLightKeys ? hist[threadIdx.x] : 0u;
+        uint32_t t;
+        const uint32_t ex = wave_prefix(v, t);
+        if (threadIdx.x < kLightKeys) hist[threadIdx.x] = ex;
+        if (threadIdx.x == 0) sh[0] = t;
+    }
+    __syncthreads();
+    total = sh[0];
+#pragma unroll
+    for (uint32_t g = 0; g < kGroupTiles; ++g) {
+        const uint32_t p = base + threadIdx.x * kGroupTiles + g;
+        uint32_t at = m[g] ? hist[key[g]] + pos[g] : 0u;
+        for (uint32_t b = m[g]; b; b &= b - 1u) lst_dyn[at++] = ((uint32_t)__ffs(b) - 1u) << 27 | p;
+    }
+    __syncthreads();
+#else
     uint32_t m[kGroupTiles], cnt[kGroupTiles];
 #pragma unroll
     for (uint32_t g = 0; g < kGroupTiles; ++g) {
         const uint32_t p = base + threadIdx.x * kGroupTiles + g;
-        m[g] = p < w.P ? w.smask[p] : 0u;
+        m[g] = p < w.P ? w.smask[p] & kSlotBits : 0u;
         cnt[g] = (uint32_t)__popc(m[g]);
     }
     uint32_t total;
@@ -756,6 +802,7 @@ __device__ __forceinline__ void shadow_tile(const SceneView& sv, const WaveBufs&
         for (uint32_t b = m[g]; b; b &= b - 1u) lst_dyn[at++] = ((uint32_t)__ffs(b) - 1u) << 27 | p;
     }
     __syncthreads();
+#endif
     for (uint32_t i = threadIdx.x; i < total; i += 256u) {
         const uint32_t e = lst_dyn[i];
         const uint64_t slot = (uint64_t)(e >> 27) * w.P + (e & 0x07ffffffu);

@@ -1,11 +1,18 @@
-# parity tests, then bench under each VPX_PERSIST setting
+# A/B: full GPU parity suite on the in-tree library, then each var/ library's bench lines
+# for CFGS (default C1 C3), REPS repetitions interleaved (variants alternate per rep).
 set -u
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
-timeout -k 10 900 python -m pytest tests/test_gpu_parity.py -q -m gpu -x > gpurun_out/gputests.log 2>&1; rc=$?
-echo "tests rc=$rc"; tail -3 gpurun_out/gputests.log
-if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
-for p in 1 0; do
-  VPX_PERSIST=$p timeout -k 10 300 python bench.py --steps 10 --warmup 2 --no-cpu ${BENCH_ARGS:-} > gpurun_out/bench_p$p.log 2>&1; rc=$?
-  echo "persist=$p rc=$rc"; grep -o '"value": [0-9.]*\|"ms_per_step": [0-9.]*\|"dda_cells": [0-9.]*' gpurun_out/bench_p$p.log | tr '\n' ' '; echo
-  if [ $rc -ne 0 ]; then tail -5 gpurun_out/bench_p$p.log; exit $rc; fi
+if [ "${TESTS:-1}" = 1 ]; then
+  timeout -k 10 900 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread > gpurun_out/ab_tests.log 2>&1; rc=$?
+  echo "tests rc=$rc"; grep -v amdgpu.ids gpurun_out/ab_tests.log | tail -2; [ $rc -ne 0 ] && exit $rc
+fi
+for rep in $(seq 1 ${REPS:-2}); do
+  for L in var/lib_*.so; do
+    n=$(basename $L .so)
+    for c in ${CFGS:-C1 C3}; do
+      VPX_LIB=$L timeout -k 10 300 python bench.py --config $c --steps ${STEPS:-10} --warmup 2 --no-cpu --no-extra > gpurun_out/ab_${n}_$c.log 2>&1; rc=$?
+      echo "$rep $n $c rc=$rc $(grep -o '"ms_per_step": [0-9.]*\|"stages_ms": {[^}]*}' gpurun_out/ab_${n}_$c.log | tr '\n' ' ')"; [ $rc -ne 0 ] && { tail -3 gpurun_out/ab_${n}_$c.log; exit $rc; }
+    done
+  done
 done
+exit 0
