@@ -149,6 +149,26 @@ __device__ __forceinline__ void flush_counters(const Counters& k, uint32_t prima
     }
 }
 
+// The tile (logical block) a workgroup of the walking kernels takes.  Workgroups are dealt
+// round-robin to the 8 XCDs (blocks b and b + 8 share one, MI355X_MICROARCH.md "Workgroup
+// dispatch"), so consecutive tiles land in 8 different L2s.  With VPX_XCD_RUN = R > 0, runs
+// of R consecutive tiles go to one XCD and the runs are dealt round-robin: block b = 8k + x
+// takes tile ((k / R) * 8 + x) * R + k % R (the last partial round keeps t = b).  Contiguous
+// bands per XCD were measured and rejected: the image's cost is spatially uneven, and a
+// band per XCD left most XCDs idle (C1 primary 0.46 -> 0.80 ms).  A permutation of the
+// tiles — any kernel may use it or not; the fused tail uses it for its walks and finish.
+#ifndef VPX_XCD_RUN
+#define VPX_XCD_RUN 0
+#endif
+__device__ __forceinline__ uint32_t tile_block() {
+    constexpr uint32_t R = VPX_XCD_RUN;
+    if (R == 0) return blockIdx.x;
+    const uint32_t b = blockIdx.x, full = (gridDim.x / (8u * (R ? R : 1u))) * 8u * R;
+    if (b >= full) return b;
+    const uint32_t x = b & 7u, k = b >> 3;
+    return ((k / R) * 8u + x) * R + k % R;
+}
+
 // ------------------------------------------------------------------- stage 2
 __device__ __forceinline__ void put_slot(const WaveBufs& w, uint32_t s, uint32_t p, f3 o, f3 d, float tmax, f3 val,
                                          uint32_t fl) {
@@ -604,7 +624,7 @@ __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_NEAREST : VPX_WPE_MULTI_
     __shared__ uint32_t sh[4];
     __shared__ uint32_t lst[256];
     if (!ONE) stage_tlas(sv);
-    const uint32_t p = blockIdx.x * 256u + threadIdx.x;
+    const uint32_t p = tile_block() * 256u + threadIdx.x;
     Counters k{0u, 0u, 0u};
     uint32_t prim = 0;
     bool walk = false;
@@ -711,7 +731,7 @@ __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_NEAREST : VPX_WPE_MULTI_
     if (!ONE) stage_tlas(sv);
     __shared__ uint32_t sh[4];
     __shared__ uint32_t lst[256 * kGroupTiles];
-    const uint32_t base = blockIdx.x * 256u * kGroupTiles;
+    const uint32_t base = tile_block() * 256u * kGroupTiles;
     Counters k{0u, 0u, 0u};
     uint32_t cnt[kGroupTiles];
 #pragma unroll
@@ -750,7 +770,7 @@ template <bool ONE>
 __device__ __forceinline__ void shadow_tile(const SceneView& sv, const WaveBufs& w, unsigned long long* __restrict__ ctr) {
     __shared__ uint32_t sh[4];
     extern __shared__ uint32_t lst_dyn[];  // [S * 256 * G]
-    const uint32_t base = blockIdx.x * 256u * kGroupTiles;
+    const uint32_t base = tile_block() * 256u * kGroupTiles;
     Counters k{0u, 0u, 0u};
 #if VPX_SHADOW_BUCKETS
     // counting sort of the tile's slots by light key: LDS histogram (the order inside a
@@ -943,7 +963,7 @@ __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_SHADOW : VPX_WPE_MULTI_S
     if (!ONE) stage_tlas(sv);
     shadow_tile<ONE>(sv, w, ctr);
     __syncthreads();
-    const uint32_t p = blockIdx.x * 256u + threadIdx.x;
+    const uint32_t p = tile_block() * 256u + threadIdx.x;
     resolve_path(sv, w, p);
     finish_path<MODE>(f, w, p, accum, rgb8, packed);
 }
