@@ -496,6 +496,28 @@ def test_cpp_host_demo_matches_oracle(pkg, orc, tmp_path, devices):
     assert np.array_equal(rgb_cpp, rgb)
 
 
+def test_cpp_host_demo_asan(pkg, orc, tmp_path):
+    """The C++ host mirror built with ASan + UBSan on its host code (-Xarch_host), 3 frames
+    through the device, equal to the oracle and free of sanitizer reports."""
+    import subprocess
+
+    exe = os.path.join(os.path.dirname(pkg.__file__), "host", "vpx_demo_asan")
+    n, w, h, frames, depth = 64, 64, 40, 3, 1
+    out = tmp_path / "frame.rgb8"
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:protect_shadow_gap=0:abort_on_error=1",
+               UBSAN_OPTIONS="halt_on_error=1")
+    r = subprocess.run([exe, str(n), str(w), str(h), str(frames), str(depth), str(out)], capture_output=True,
+                       text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "Sanitizer" not in r.stderr
+    desc = pkg.scene.pillars_scene(n, w, h, depth)
+    o = orc.Oracle(pkg.abi, desc)
+    acc = None
+    for f in range(frames):
+        acc, rgb, _ = o.render(desc.frame_params(f), accum=acc)
+    assert np.array_equal(np.fromfile(out, np.uint32), rgb)
+
+
 def demo_sky(w=64, h=32):
     """host/vpx_demo.cpp demo_sky, restated in float32."""
     v, u = np.meshgrid(np.arange(h), np.arange(w), indexing="ij")
