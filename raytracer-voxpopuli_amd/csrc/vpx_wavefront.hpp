@@ -57,8 +57,26 @@ struct FrameArgs {
 // Per-path level forms: level l's 2-bit form at bits 2l..2l+1 and a sentinel 1 just above
 // the last recorded level, so a count of up to kMaxLevels - 1 = 15 levels (max_bounces 14)
 // takes bits 0..30 (a separate count field would not fit beside 30 form bits).
-static_assert(2 * (kMaxLevels - 1) < 32, "forms word: 2 bits per level + sentinel must fit 32 bits");
-__device__ __forceinline__ uint32_t forms_count(uint32_t forms) { return (31u - (uint32_t)__clz(forms)) >> 1; }
+// Bit 31 says the path ended on a leaf value (sky / emissive) held in `leaf`; without it the
+// leaf is 0 (Trace(ray, -1)) and is not read, so no kernel zero-fills the leaf buffer.
+constexpr uint32_t kLeafBit = 0x80000000u;
+static_assert(2 * (kMaxLevels - 1) < 31, "forms word: 2 bits per level + sentinel + leaf bit must fit 32 bits");
+__device__ __forceinline__ uint32_t forms_count(uint32_t forms) {
+    return (31u - (uint32_t)__clz(forms & ~kLeafBit)) >> 1;
+}
+
+// Where a kernel finds the ray (O, D) and hit record (H, HM) of the path it works on: the
+// global path buffers, or the workgroup's LDS in the fused head (k_primary<.., true>), whose
+// walkers and level-0 shade hand them over inside the workgroup (base = the tile's first
+// path).  Only the fused head uses LDS; every later kernel reads the global buffers.
+struct PathRay {
+    float4* O;
+    float4* D;
+    float4* H;
+    uint32_t* HM;
+    uint32_t base;
+    __device__ __forceinline__ uint32_t at(uint32_t p) const { return p - base; }
+};
 
 struct WaveBufs {
     float4* O;     // [P] ray origin, w = rng state bits
@@ -289,17 +307,17 @@ __device__ __forceinline__ uint32_t wave_prefix(uint32_t v, uint32_t& total) {
 // rays, which never start inside glass or smoke, so the interior exit marches (a whole DDA
 // walker each) drop out of that instance; the forms word is known (no levels yet).
 template <bool L0 = false>
-__device__ __forceinline__ void shade_path(const SceneView& sv, const FrameArgs& f, const WaveBufs& w, uint32_t p,
-                                           int level, Counters& k) {
+__device__ __forceinline__ void shade_path(const SceneView& sv, const FrameArgs& f, const WaveBufs& w,
+                                           const PathRay& pr, uint32_t p, int level, Counters& k) {
     uint32_t slots = 0;
     if (p < w.P) {
-        float4 od = w.D[p];
+        float4 od = pr.D[pr.at(p)];
         uint32_t flags = __float_as_uint(od.w);
         uint32_t pending = 0;  // SM word; 0 = no light sample this level
         if (flags & kActive) {
-            const float4 oo = w.O[p];
-            const float4 hh = w.H[p];
-            const uint32_t hm = w.HM[p];
+            const float4 oo = pr.O[pr.at(p)];
+            const float4 hh = pr.H[pr.at(p)];
+            const uint32_t hm = pr.HM[pr.at(p)];
             Ray ray;
             ray.O = mk(oo.x, oo.y, oo.z);
             ray.D = mk(od.x, od.y, od.z);
@@ -316,7 +334,7 @@ __device__ __forceinline__ void shade_path(const SceneView& sv, const FrameArgs&
             }
             const int32_t vox = (int32_t)((hm >> 8) & 0xffffu) - 2;
             Rng g{__float_as_uint(oo.w)};
-            int depth = w.depth[p];
+            int depth = L0 ? f.max_bounces : w.depth[p];  // the fused head's k_primary writes no depth
             // a path being shaded at `level` has recorded exactly `level` forms
             uint32_t forms = (L0 || level == 0) ? 1u : w.forms[p];
             const uint32_t nl = forms_count(forms);
@@ -454,7 +472,9 @@ __device__ __forceinline__ void shade_path(const SceneView& sv, const FrameArgs&
             }
             if (done) {  // sky / emissive leaf; the path stops
                 w.leaf[p] = make_float4(leaf.x, leaf.y, leaf.z, 0.f);
-                w.D[p] = make_float4(od.x, od.y, od.z, __uint_as_float(0u));
+                w.forms[p] = forms | kLeafBit;
+                // later levels' kernels skip it (after the last level no kernel reads D)
+                if (level < f.max_bounces) w.D[p] = make_float4(od.x, od.y, od.z, __uint_as_float(0u));
             }
         }
         if (!pending) w.SM[p] = make_float4(0.f, 0.f, 0.f, __uint_as_float(0u));
@@ -465,7 +485,7 @@ __device__ __forceinline__ void shade_path(const SceneView& sv, const FrameArgs&
 __global__ __launch_bounds__(256) void k_shade(SceneView sv, FrameArgs f, WaveBufs w, int level,
                                                unsigned long long* ctr) {
     Counters k{0u, 0u, 0u};
-    shade_path(sv, f, w, blockIdx.x * 256u + threadIdx.x, level, k);
+    shade_path(sv, f, w, PathRay{w.O, w.D, w.H, w.HM, 0u}, blockIdx.x * 256u + threadIdx.x, level, k);
     flush_counters(k, 0u, ctr, VPX_STAGE_SHADE);
 }
 
@@ -563,18 +583,18 @@ __device__ __forceinline__ uint32_t block_scan(uint32_t cnt, uint32_t& total, ui
 }
 
 template <uint32_t SKIPW = VPX_SKIPW_NEAREST, uint32_t MINC = VPX_MINC_NEAREST>
-__device__ __forceinline__ void nearest_record(SceneView sv, const WaveBufs& w, uint32_t p, Ray& r, Counters& k) {
+__device__ __forceinline__ void nearest_record(SceneView sv, const PathRay& pr, uint32_t p, Ray& r, Counters& k) {
     r.t = kBig;
     r.mat = kNone;
     r.N = mk(0.f, 0.f, 0.f);
     const int32_t vox = find_nearest<SKIPW, MINC>(sv, r, k);
-    w.H[p] = make_float4(r.t, r.N.x, r.N.y, r.N.z);
-    w.HM[p] = r.mat | ((uint32_t)(vox + 2) << 8) | (r.inside ? 0x80000000u : 0u);
+    pr.H[pr.at(p)] = make_float4(r.t, r.N.x, r.N.y, r.N.z);
+    pr.HM[pr.at(p)] = r.mat | ((uint32_t)(vox + 2) << 8) | (r.inside ? 0x80000000u : 0u);
 }
 
 // Object-space ray of path p in the single volume (FindNearest's SSE transforms).
-__device__ __forceinline__ ORay path_oray(const vpx_volume& vol, const WaveBufs& w, uint32_t p) {
-    const float4 o = w.O[p], d = w.D[p];
+__device__ __forceinline__ ORay path_oray(const vpx_volume& vol, const PathRay& pr, uint32_t p) {
+    const float4 o = pr.O[pr.at(p)], d = pr.D[pr.at(p)];
     ORay r;
     r.O = xform_pos_ssem(mk(o.x, o.y, o.z), vol.inv_matrix);
     r.D = xform_vec_ssem(mk(d.x, d.y, d.z), vol.inv_matrix);
@@ -587,7 +607,7 @@ __device__ __forceinline__ ORay path_oray(const vpx_volume& vol, const WaveBufs&
 // transformed again for the normal (the same operations, so the same values), which
 // keeps the walker's registers from spilling.
 template <uint32_t SKIPW = VPX_SKIPW_NEAREST, uint32_t MINC = VPX_MINC_NEAREST>
-__device__ __forceinline__ void nearest_record_1v(const SceneView& sv, const WaveBufs& w, uint32_t p, Counters& k) {
+__device__ __forceinline__ void nearest_record_1v(const SceneView& sv, const PathRay& w, uint32_t p, Counters& k) {
     const vpx_volume* vol = uni_ptr(&sv.volumes[0]);
     const DevGrid g = sv.grids[vol->grid_id];
     ++k.nearest;
@@ -602,19 +622,22 @@ __device__ __forceinline__ void nearest_record_1v(const SceneView& sv, const Wav
         }
     }
     asm volatile("" ::: "memory");  // re-read the ray below instead of keeping it live
-    const uint32_t inside = __float_as_uint(w.D[p].w) & kInside ? 0x80000000u : 0u;
+    const uint32_t inside = __float_as_uint(w.D[w.at(p)].w) & kInside ? 0x80000000u : 0u;
     if (!hit) {
-        w.H[p] = make_float4(kBig, 0.f, 0.f, 0.f);
-        w.HM[p] = kNone | inside;  // vox -2
+        w.H[w.at(p)] = make_float4(kBig, 0.f, 0.f, 0.f);
+        w.HM[w.at(p)] = kNone | inside;  // vox -2
         return;
     }
     const ORay o = path_oray(*vol, w, p);
     const f3 N = normal_voxel(o, wk.t, g.n, vol->matrix);
     const uint32_t mat = g.cells[(uint64_t)wk.X + (uint64_t)wk.Y * g.n + (uint64_t)wk.Z * ((uint64_t)g.n * g.n)];
-    w.H[p] = make_float4(wk.t, N.x, N.y, N.z);
-    w.HM[p] = mat | (2u << 8) | inside;  // vox 0
+    w.H[w.at(p)] = make_float4(wk.t, N.x, N.y, N.z);
+    w.HM[w.at(p)] = mat | (2u << 8) | inside;  // vox 0
 }
 
+#ifndef VPX_HEAD_LDS
+#define VPX_HEAD_LDS 1
+#endif
 // Primary rays + Renderer::FindNearest.  Every path's ray / RNG state is written; rays
 // that cannot hit a voxel or shape (one volume, no shapes, Setup3DDDA fails: the
 // reference returns before reading a cell) get their miss record directly.
@@ -623,17 +646,25 @@ __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_NEAREST : VPX_WPE_MULTI_
                                                  unsigned long long* __restrict__ ctr) {
     __shared__ uint32_t sh[4];
     __shared__ uint32_t lst[256];
+    // the fused head keeps the tile's rays and hit records in LDS: its walkers and its
+    // level-0 shade are the only readers (VPX_HEAD_LDS=0: the global path buffers)
+    __shared__ float4 s_ray[SHADE && VPX_HEAD_LDS ? 3 * 256 : 1];
+    __shared__ uint32_t s_hm[SHADE && VPX_HEAD_LDS ? 256 : 1];
     if (!ONE) stage_tlas(sv);
-    const uint32_t p = tile_block() * 256u + threadIdx.x;
+    const uint32_t tb = tile_block() * 256u;
+    const uint32_t p = tb + threadIdx.x;
+    const bool lds = SHADE && VPX_HEAD_LDS;
+    const PathRay pr = lds ? PathRay{s_ray, s_ray + 256, s_ray + 512, s_hm, tb} : PathRay{w.O, w.D, w.H, w.HM, 0u};
     Counters k{0u, 0u, 0u};
     uint32_t prim = 0;
     bool walk = false;
     if (p < w.P) {
         uint32_t x, y;
         bool go = path_pixel(f, p, x, y);
-        w.depth[p] = f.max_bounces;
-        w.forms[p] = 1u;  // no levels recorded
-        w.leaf[p] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (!SHADE) {  // the fused shade writes depth (paths that continue) and forms itself
+            w.depth[p] = f.max_bounces;
+            w.forms[p] = 1u;  // no levels recorded, no leaf
+        }
         Ray r;
         r.O = r.D = mk(0.f, 0.f, 0.f);
         uint32_t rng = 0, flags = 0;
@@ -648,8 +679,10 @@ __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_NEAREST : VPX_WPE_MULTI_
             go = false;
             flags = 0u;
         }
-        w.O[p] = make_float4(r.O.x, r.O.y, r.O.z, __uint_as_float(rng));
-        w.D[p] = make_float4(r.D.x, r.D.y, r.D.z, __uint_as_float(flags));
+        pr.O[pr.at(p)] = make_float4(r.O.x, r.O.y, r.O.z, __uint_as_float(rng));
+        pr.D[pr.at(p)] = make_float4(r.D.x, r.D.y, r.D.z, __uint_as_float(flags));
+        // an inactive path (no pixel) must read as such in the later levels' kernels
+        if (lds && !flags && f.max_bounces > 0) w.D[p] = make_float4(0.f, 0.f, 0.f, __uint_as_float(0u));
         if (go) {
             walk = true;
             if (ONE) {
@@ -662,34 +695,34 @@ __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_NEAREST : VPX_WPE_MULTI_
                 if (!dda_setup(vol, sv.grids[vol.grid_id].n, o, s)) {
                     walk = false;
                     ++k.nearest;
-                    w.H[p] = make_float4(kBig, 0.f, 0.f, 0.f);
-                    w.HM[p] = kNone;  // vox -2, not inside glass
+                    pr.H[pr.at(p)] = make_float4(kBig, 0.f, 0.f, 0.f);
+                    pr.HM[pr.at(p)] = kNone;  // vox -2, not inside glass
                 }
             }
         }
     }
     uint32_t total;
-    const uint32_t at = block_scan(walk ? 1u : 0u, total, sh);
+    const uint32_t at = block_scan(walk ? 1u : 0u, total, sh);  // (its barrier orders the LDS writes)
     if (walk) lst[at] = p;
     __syncthreads();
     if (threadIdx.x < total) {
         const uint32_t q = lst[threadIdx.x];
         if (ONE) {
-            nearest_record_1v(sv, w, q, k);
+            nearest_record_1v(sv, pr, q, k);
         } else {
-            const float4 o = w.O[q], d = w.D[q];
+            const float4 o = pr.O[pr.at(q)], d = pr.D[pr.at(q)];
             Ray r;
             r.O = mk(o.x, o.y, o.z);
             r.D = mk(d.x, d.y, d.z);
             r.inside = false;
-            nearest_record(sv, w, q, r, k);
+            nearest_record(sv, pr, q, r, k);
         }
     }
     flush_counters(k, prim, ctr, VPX_STAGE_PRIMARY);
     if (SHADE) {  // level 0's material switch for this thread's own path (k_primary_shade)
         __syncthreads();  // the tile's hit records, written by the compacted walkers
         Counters ks{0u, 0u, 0u};
-        shade_path<true>(sv, f, w, p, 0, ks);
+        shade_path<true>(sv, f, w, pr, p, 0, ks);
         flush_counters(ks, 0u, ctr, VPX_STAGE_SHADE);
     }
 }
@@ -748,7 +781,7 @@ __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_NEAREST : VPX_WPE_MULTI_
     for (uint32_t i = threadIdx.x; i < total; i += 256u) {
         const uint32_t q = lst[i];
         if (ONE) {
-            nearest_record_1v<VPX_SKIPW_BOUNCE, VPX_MINC_BOUNCE>(sv, w, q, k);
+            nearest_record_1v<VPX_SKIPW_BOUNCE, VPX_MINC_BOUNCE>(sv, PathRay{w.O, w.D, w.H, w.HM, 0u}, q, k);
             continue;
         }
         const float4 o = w.O[q], d = w.D[q];
@@ -756,7 +789,7 @@ __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_NEAREST : VPX_WPE_MULTI_
         r.O = mk(o.x, o.y, o.z);
         r.D = mk(d.x, d.y, d.z);
         r.inside = (__float_as_uint(d.w) & kInside) != 0u;
-        nearest_record<VPX_SKIPW_BOUNCE, VPX_MINC_BOUNCE>(sv, w, q, r, k);
+        nearest_record<VPX_SKIPW_BOUNCE, VPX_MINC_BOUNCE>(sv, PathRay{w.O, w.D, w.H, w.HM, 0u}, q, r, k);
     }
     flush_counters(k, 0u, ctr, VPX_STAGE_BOUNCE);
 }
@@ -902,9 +935,11 @@ __device__ __forceinline__ void finish_path(const FrameArgs& f, const WaveBufs& 
     const bool valid = path_pixel(f, p, x, y);
     f3 v = mk(0.f, 0.f, 0.f);
     if (valid) {
-        const float4 lf = w.leaf[p];
-        v = mk(lf.x, lf.y, lf.z);
         const uint32_t forms = w.forms[p];
+        if (forms & kLeafBit) {
+            const float4 lf = w.leaf[p];
+            v = mk(lf.x, lf.y, lf.z);
+        }
         for (int i = (int)forms_count(forms) - 1; i >= 0; --i) {
             const uint32_t form = (forms >> (2 * i)) & 3u;
             const uint64_t li = (uint64_t)i * w.P + p;
@@ -994,9 +1029,12 @@ __global__ __launch_bounds__(256) void k_finish_reproject(FrameArgs f, WaveBufs 
         const f3 ip = mk(o.x, o.y, o.z) + mk(d.x, d.y, d.z) * kBig;
         w.RD[px] = make_float4(ip.x, ip.y, ip.z, __uint_as_float(kNone));
     } else {
-        const float4 lf = w.leaf[p];
-        f3 v = mk(lf.x, lf.y, lf.z);
         const uint32_t forms = w.forms[p];
+        f3 v = mk(0.f, 0.f, 0.f);
+        if (forms & kLeafBit) {
+            const float4 lf = w.leaf[p];
+            v = mk(lf.x, lf.y, lf.z);
+        }
         const int nl = (int)forms_count(forms);
         if (nl == 0) {  // sky / emissive at the top: {colour, 1} (renderer.cpp:1333, 2330-2333)
             A = v;
