@@ -302,6 +302,26 @@ constexpr uint32_t kMinCube = VPX_MIN_CUBE;
 // every call and the class is formed with selects: the loads hit the cache while the
 // brick does not change, and a per-brick key cache with load branches measured 3.5 %
 // slower on C1 (the divergent branches cost more than the loads they avoid).
+// classify split in two: the level words of a cell (loads only) and the class from them,
+// so a walker can issue the loads of a later cell before it needs this one's class.
+struct Words {
+    uint64_t m1, m2;
+};
+VPX_HD Words load_words(uint32_t X, uint32_t Y, uint32_t Z, const GridView& g) {
+    return Words{load_mask(g.l1, blk_index(X >> 2, Y >> 2, Z >> 2, g.nb2)),
+                 load_mask(g.l2, blk_index(X >> 4, Y >> 4, Z >> 4, g.nb3))};
+}
+template <uint32_t MINC = kMinCube>
+VPX_HD int classify_words(Walk& w, const Words& m) {
+    w.m1 = m.m1, w.m2 = m.m2;
+    const uint32_t X = w.X, Y = w.Y, Z = w.Z;
+    const uint32_t bb = ((X >> 2) & 3u) | (((Y >> 2) & 3u) << 2) | (((Z >> 2) & 3u) << 4);
+    const uint32_t cb = (X & 3u) | ((Y & 3u) << 2) | ((Z & 3u) << 4);
+    const int cell = ((w.m1 >> cb) & 1ull) ? 0 : 1;
+    const int brick = ((uint32_t)(w.m1 >> w.osh) & 255u) >= MINC ? 2 : 3;
+    return ((w.m2 >> bb) & 1ull) ? cell : brick;
+}
+
 template <uint32_t MINC = kMinCube>
 VPX_HD int classify(Walk& w, const GridView& g) {
     const uint32_t X = w.X, Y = w.Y, Z = w.Z;
