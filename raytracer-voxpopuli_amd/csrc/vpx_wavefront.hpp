@@ -727,6 +727,9 @@ __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_NEAREST : VPX_WPE_MULTI_
     }
 }
 
+#ifndef VPX_BOUNCE_BUCKETS
+#define VPX_BOUNCE_BUCKETS 0  // 1: bounce walks grouped by direction octant (measured C2: 4.88 vs 4.82 ms, no gain)
+#endif
 // Sparse stages (bounce FindNearest, IsOccluded) can gather the work of G tiles per
 // workgroup (entries stay in tile order).  Measured on C1: G = 1, 2, 4, 8 -> 2.70, 2.87,
 // 3.22, 4.36 ms/frame.  Walk lengths are heavy-tailed (mean ~60 iterations, max ~400),
@@ -766,18 +769,49 @@ __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_NEAREST : VPX_WPE_MULTI_
     __shared__ uint32_t lst[256 * kGroupTiles];
     const uint32_t base = tile_block() * 256u * kGroupTiles;
     Counters k{0u, 0u, 0u};
+    uint32_t total;
+#if VPX_BOUNCE_BUCKETS
+    // bounce rays leave surfaces in scattered directions: the tile's walks are grouped by the
+    // octant of their direction (LDS histogram + one wave's prefix sum, as the shadow lists),
+    // so a wave's lanes head the same way (the distance-field byte they read, their steps)
+    static_assert(kGroupTiles == 1, "octant buckets assume one tile per workgroup");
+    __shared__ uint32_t hist[8];
+    if (threadIdx.x < 8) hist[threadIdx.x] = 0u;
+    __syncthreads();
+    const uint32_t p = base + threadIdx.x;
+    bool act = false;
+    uint32_t key = 0, pos = 0;
+    if (p < w.P) {
+        const float4 d = w.D[p];
+        act = (__float_as_uint(d.w) & kActive) != 0u;
+        key = (__float_as_uint(d.x) >> 31) | ((__float_as_uint(d.y) >> 31) << 1) | ((__float_as_uint(d.z) >> 31) << 2);
+        if (act) pos = atomicAdd(&hist[key], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        uint32_t t;
+        const uint32_t v = threadIdx.x < 8 ? hist[threadIdx.x] : 0u;
+        const uint32_t ex = wave_prefix(v, t);
+        if (threadIdx.x < 8) hist[threadIdx.x] = ex;
+        if (threadIdx.x == 0) sh[0] = t;
+    }
+    __syncthreads();
+    total = sh[0];
+    if (act) lst[hist[key] + pos] = p;
+    __syncthreads();
+#else
     uint32_t cnt[kGroupTiles];
 #pragma unroll
     for (uint32_t g = 0; g < kGroupTiles; ++g) {  // thread t scans paths base + t*G + g
         const uint32_t p = base + threadIdx.x * kGroupTiles + g;
         cnt[g] = (p < w.P && (__float_as_uint(w.D[p].w) & kActive)) ? 1u : 0u;
     }
-    uint32_t total;
     uint32_t at = group_scan<kGroupTiles>(cnt, total, sh);
 #pragma unroll
     for (uint32_t g = 0; g < kGroupTiles; ++g)
         if (cnt[g]) lst[at++] = base + threadIdx.x * kGroupTiles + g;
     __syncthreads();
+#endif
     for (uint32_t i = threadIdx.x; i < total; i += 256u) {
         const uint32_t q = lst[i];
         if (ONE) {
