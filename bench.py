@@ -210,7 +210,7 @@ def run_config(pkg, env, cfg, steps, warmup, weak=False, sha=None):
         # the library runs the last level's shadow -> resolve -> finish as one launch
         # (k_shadow_finish) unless built with VPX_FUSE_TAIL=0: then there is no
         # separate finish stage, and the shadow stage carries the 36 B per pixel
-        fused = "finish" not in split
+        fused = split.get("finish", (0.0, 0, 0))[1] == 0  # stages with no launch stay in the table
         kernels = dict(STAGE_KERNELS)
         if fused:
             kernels["shadow"] = "k_shadow_finish" if desc.max_bounces == 0 else "k_shadow_tile+k_shadow_finish"

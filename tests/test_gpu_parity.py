@@ -263,6 +263,35 @@ def test_device_set_equals_single_device(pkg, orc, devices):
     ctx.close()
 
 
+def test_zero_copy_screen_in_mapped_host_memory(pkg):
+    """SURVEY §8(f) rank 2, display path without GL interop in this image: Surface::pixels
+    allocated as mapped pinned host memory (hipHostMalloc(..., hipHostMallocMapped)) and its
+    device alias handed to vpx_render as rgb8 — the frame's RGB8 lands in the host buffer the
+    GL upload reads (template/opengl.cpp:144-149), with no hipMemcpy, byte-equal to the
+    device-buffer frame."""
+    import ctypes as C
+
+    hip = C.CDLL("libamdhip64.so")
+    desc = pkg.scene.city_scene("monu3", 128, 96, 64, 0)
+    acc_ref, rgb_ref, _ = render_gpu(pkg, desc)
+    n = desc.width * desc.height
+    host = C.c_void_p()
+    assert hip.hipHostMalloc(C.byref(host), C.c_size_t(4 * n), C.c_uint(0x2)) == 0  # hipHostMallocMapped
+    dev = C.c_void_p()
+    assert hip.hipHostGetDevicePointer(C.byref(dev), host, C.c_uint(0)) == 0
+    try:
+        ctx = make_ctx(pkg, desc)
+        acc = torch.zeros(n * 4, dtype=torch.float32, device="cuda")
+        torch.cuda.synchronize()
+        ctx.render(desc.frame_params(0), acc.data_ptr(), dev.value)
+        ctx.synchronize()
+        screen = np.ctypeslib.as_array((C.c_uint32 * n).from_address(host.value)).copy()
+        assert np.array_equal(screen, rgb_ref)
+        ctx.close()
+    finally:
+        hip.hipHostFree(host)
+
+
 def test_sharded_accum_frame_refuses_a_foreign_stream(pkg):
     """RCCL orders the gather after torch's current stream, so the sharded flow refuses a
     context that renders on another stream instead of gathering stale RGB8."""
