@@ -255,6 +255,22 @@ int vpx_set_camera(vpx_ctx* ctx, const vpx_camera* camera);
 int vpx_set_sky(vpx_ctx* ctx, const float* rgb, uint32_t width, uint32_t height,
                 float hdr_contribution);
 
+/* ---- display interop ---------------------------------------------
+   Replaces the per-frame host upload of Surface::pixels in GLTexture::CopyFrom
+   (template/opengl.cpp:144-149, called from template/template.cpp:305).  The host creates a
+   GL_PIXEL_UNPACK_BUFFER of W*H*4 bytes once and registers it with its GL context current on
+   the calling thread, on this context's GPU (device set: devices[0]); gl_buffer == 0
+   unregisters (vpx_destroy does too).  Per frame: vpx_gl_map returns the buffer's device
+   address (ordered on the context's stream), the host passes it as `rgb8` to vpx_render or
+   vpx_render_reproject, vpx_gl_unmap hands it back to GL, and glTexSubImage2D with the
+   buffer bound updates the texture — the frame never crosses PCIe.  `bytes` (may be NULL)
+   receives the buffer size; the host checks it against W*H*4.  Errors: VPX_E_DEVICE when
+   HIP cannot register the buffer (no current GL context, another GPU), VPX_E_STATE for
+   map / unmap / register out of order.  Unmeasured on hardware: no GL display here. */
+int vpx_gl_register_buffer(vpx_ctx* ctx, unsigned int gl_buffer);
+int vpx_gl_map(vpx_ctx* ctx, uint32_t** rgb8, size_t* bytes);
+int vpx_gl_unmap(vpx_ctx* ctx);
+
 /* ---- the hot path -------------------------------------------------------------------- */
 /* One frame: primary rays, Trace(ray, max_bounces) per pixel, running-average accumulate
    (w = 1/(frame_index+1)), Reinhard-Jodie tonemap, RGB8 pack.  `accum` (float4[W*H]) and

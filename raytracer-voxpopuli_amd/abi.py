@@ -137,6 +137,9 @@ SIGNATURES = {
     "vpx_abi_version": (C.c_int, []),
     "vpx_set_stream": (C.c_int, [C.c_void_p, C.c_void_p]),
     "vpx_synchronize": (C.c_int, [C.c_void_p]),
+    "vpx_gl_register_buffer": (C.c_int, [C.c_void_p, C.c_uint]),
+    "vpx_gl_map": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]),
+    "vpx_gl_unmap": (C.c_int, [C.c_void_p]),
     "vpx_upload_grid": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32]),
     "vpx_generate_tiled_grid": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p] + [C.c_uint32] * 7),
     "vpx_grid_checksum": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_uint64)]),

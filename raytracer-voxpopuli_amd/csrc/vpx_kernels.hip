@@ -9,6 +9,7 @@
 //   find_nearest_k / is_occluded_k / trace_k   per-ray unit entries.
 //   tiled_world_k / checksum_k    world generator and grid checksum.
 #include <hip/hip_runtime.h>
+#include <hip/hip_gl_interop.h>
 #include <rccl/rccl.h>
 
 #include <algorithm>
@@ -434,6 +435,10 @@ struct vpx_ctx {
     size_t g_len = 0;                   // float4 elements per member buffer the above were sized for
     std::vector<hipEvent_t> g_ev;       // per member: its render done (copy path)
     hipEvent_t g_copied = nullptr;      // member 0: gather copies done (copy path)
+    // display interop (vpx_gl_*): a registered GL pixel-unpack buffer on this context's
+    // device (device set: devices[0]); mapped between vpx_gl_map and vpx_gl_unmap
+    hipGraphicsResource_t gl_res = nullptr;
+    bool gl_mapped = false;
 };
 
 namespace {
@@ -773,6 +778,7 @@ int vpx_create(int device, vpx_ctx** out) {
 
 int vpx_destroy(vpx_ctx* c) {
     if (!c) return VPX_E_INVALID;
+    if (c->gl_res) (void)vpx_gl_register_buffer(c, 0u);
     if (!c->members.empty()) {  // device set: its buffers, communicators and members
         for (size_t r = 0; r < c->members.size(); ++r) {
             vpx_ctx* m = c->members[r];
@@ -818,6 +824,63 @@ int vpx_set_stream(vpx_ctx* c, void* s) {
     if (!c) return VPX_E_INVALID;
     if (!c->members.empty()) return vpx_set_stream(c->members[0], s);  // a stream of the first device
     c->stream = s ? (hipStream_t)s : c->own_stream;
+    return VPX_OK;
+}
+
+// ---------------------------------------------------------------- display interop
+// GLTexture::CopyFrom (template/opengl.cpp:144-149) uploads the host screen every frame; here
+// the RGB8 pack writes into a GL pixel-unpack buffer the host registered once, and the host
+// updates its texture from that buffer (glTexSubImage2D with the PBO bound) — the frame stays
+// on the GPU.  A device set registers and maps on devices[0], where vpx_render composites.
+static vpx_ctx* gl_home(vpx_ctx* c) { return c->members.empty() ? c : c->members[0]; }
+
+int vpx_gl_register_buffer(vpx_ctx* c, unsigned int gl_buffer) {
+    if (!c) return VPX_E_INVALID;
+    if (c->gl_mapped) return fail(c, VPX_E_STATE, "the GL buffer is mapped (vpx_gl_unmap first)");
+    vpx_ctx* h = gl_home(c);
+    VPX_HIP(c, hipSetDevice(h->device));
+    if (c->gl_res) {
+        const hipError_t e = hipGraphicsUnregisterResource(c->gl_res);
+        c->gl_res = nullptr;
+        if (e != hipSuccess) return fail(c, VPX_E_DEVICE, std::string("hipGraphicsUnregisterResource: ") + hipGetErrorString(e));
+    }
+    if (gl_buffer == 0u) return VPX_OK;
+    hipGraphicsResource_t r = nullptr;
+    const hipError_t e = hipGraphicsGLRegisterBuffer(&r, (GLuint)gl_buffer, hipGraphicsRegisterFlagsWriteDiscard);
+    if (e != hipSuccess || !r)
+        return fail(c, VPX_E_DEVICE, std::string("hipGraphicsGLRegisterBuffer (needs the buffer's GL context current on "
+                                                 "this thread, on this context's GPU): ") + hipGetErrorString(e));
+    c->gl_res = r;
+    return VPX_OK;
+}
+
+int vpx_gl_map(vpx_ctx* c, uint32_t** rgb8, size_t* bytes) {
+    if (!c || !rgb8) return VPX_E_INVALID;
+    if (!c->gl_res) return fail(c, VPX_E_STATE, "no GL buffer registered (vpx_gl_register_buffer)");
+    if (c->gl_mapped) return fail(c, VPX_E_STATE, "the GL buffer is already mapped");
+    vpx_ctx* h = gl_home(c);
+    VPX_HIP(c, hipSetDevice(h->device));
+    VPX_HIP(c, hipGraphicsMapResources(1, &c->gl_res, h->stream));
+    void* ptr = nullptr;
+    size_t n = 0;
+    const hipError_t e = hipGraphicsResourceGetMappedPointer(&ptr, &n, c->gl_res);
+    if (e != hipSuccess) {
+        (void)hipGraphicsUnmapResources(1, &c->gl_res, h->stream);
+        return fail(c, VPX_E_DEVICE, std::string("hipGraphicsResourceGetMappedPointer: ") + hipGetErrorString(e));
+    }
+    c->gl_mapped = true;
+    *rgb8 = static_cast<uint32_t*>(ptr);
+    if (bytes) *bytes = n;
+    return VPX_OK;
+}
+
+int vpx_gl_unmap(vpx_ctx* c) {
+    if (!c) return VPX_E_INVALID;
+    if (!c->gl_mapped) return fail(c, VPX_E_STATE, "the GL buffer is not mapped");
+    vpx_ctx* h = gl_home(c);
+    VPX_HIP(c, hipSetDevice(h->device));
+    c->gl_mapped = false;
+    VPX_HIP(c, hipGraphicsUnmapResources(1, &c->gl_res, h->stream));
     return VPX_OK;
 }
 

@@ -179,9 +179,9 @@ __device__ __forceinline__ void flush_counters(const Counters& k, uint32_t prima
 #define VPX_XCD_RUN 0
 #endif
 __device__ __forceinline__ uint32_t tile_block() {
-    constexpr uint32_t R = VPX_XCD_RUN;
-    if (R == 0) return blockIdx.x;
-    const uint32_t b = blockIdx.x, full = (gridDim.x / (8u * (R ? R : 1u))) * 8u * R;
+    if (VPX_XCD_RUN == 0) return blockIdx.x;
+    constexpr uint32_t R = VPX_XCD_RUN > 0 ? VPX_XCD_RUN : 1;
+    const uint32_t b = blockIdx.x, full = (gridDim.x / (8u * R)) * 8u * R;
     if (b >= full) return b;
     const uint32_t x = b & 7u, k = b >> 3;
     return ((k / R) * 8u + x) * R + k % R;

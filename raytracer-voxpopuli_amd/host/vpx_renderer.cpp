@@ -85,7 +85,10 @@ int Renderer::Update(vpx_stats* stats) {
     p.aa_strength = antiAliasingStrength;
     p.area_samples = numCheckShadowsAreaLight;
     p.sky[0] = sky[0], p.sky[1] = sky[1], p.sky[2] = sky[2];
-    const int rc = vpx_render(ctx_, &p, accumulator_, screen_, stats);
+    uint32_t* target = nullptr;
+    int rc = MapScreen(&target);
+    if (rc) return rc;
+    rc = UnmapScreen(vpx_render(ctx_, &p, accumulator_, target, stats));
     if (rc == VPX_OK) ++numRenderedFrames;
     return rc;
 }
@@ -123,7 +126,10 @@ int Renderer::UpdateStatic(vpx_stats* stats) {
     p.aa_strength = antiAliasingStrength;
     p.area_samples = numCheckShadowsAreaLight;
     p.sky[0] = sky[0], p.sky[1] = sky[1], p.sky[2] = sky[2];
-    const int rc = vpx_render_reproject(ctx_, &p, &prevCamera, history_, screen_, stats);
+    uint32_t* target = nullptr;
+    int rc = MapScreen(&target);
+    if (rc) return rc;
+    rc = UnmapScreen(vpx_render_reproject(ctx_, &p, &prevCamera, history_, target, stats));
     if (rc == VPX_OK) ++numRenderedFrames;
     return rc;
 }
@@ -150,13 +156,43 @@ int Renderer::Tick(float /*deltaTime*/, vpx_stats* stats) {
     return Update(stats);
 }
 
+int Renderer::UseGLBuffer(unsigned int pbo) {
+    if (status_) return status_;
+    const int rc = vpx_gl_register_buffer(ctx_, pbo);
+    glBuffer_ = rc == VPX_OK && pbo != 0u;
+    return rc;
+}
+
+int Renderer::MapScreen(uint32_t** out) const {
+    if (!glBuffer_) {
+        *out = screen_;
+        return VPX_OK;
+    }
+    size_t bytes = 0;
+    int rc = vpx_gl_map(ctx_, out, &bytes);
+    if (rc) return rc;
+    if (bytes < sizeof(uint32_t) * (size_t)width_ * height_) {
+        (void)vpx_gl_unmap(ctx_);
+        return VPX_E_INVALID;  // the GL buffer is smaller than the frame
+    }
+    return VPX_OK;
+}
+
+int Renderer::UnmapScreen(int rc) const {
+    if (!glBuffer_) return rc;
+    const int rc2 = vpx_gl_unmap(ctx_);
+    return rc ? rc : rc2;
+}
+
 int Renderer::CopyScreen(uint32_t* host_pixels) const {
     if (status_) return status_;
-    int rc = vpx_synchronize(ctx_);
+    uint32_t* src = nullptr;
+    int rc = MapScreen(&src);
     if (rc) return rc;
-    return hipMemcpy(host_pixels, screen_, sizeof(uint32_t) * width_ * height_, hipMemcpyDeviceToHost) == hipSuccess
-               ? VPX_OK
-               : VPX_E_DEVICE;
+    rc = vpx_synchronize(ctx_);
+    if (rc == VPX_OK && hipMemcpy(host_pixels, src, sizeof(uint32_t) * width_ * height_, hipMemcpyDeviceToHost) != hipSuccess)
+        rc = VPX_E_DEVICE;
+    return UnmapScreen(rc);
 }
 
 int Renderer::CopyAccumulator(float* host_rgba) const {

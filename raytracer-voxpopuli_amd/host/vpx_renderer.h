@@ -56,6 +56,12 @@ public:
     int Tick(float deltaTime, vpx_stats* stats = nullptr);
     // Surface::pixels (0x00RRGGBB, W*H) for display: device -> host copy of the frame.
     int CopyScreen(uint32_t* host_pixels) const;
+    // Display interop in place of GLTexture::CopyFrom (template/opengl.cpp:144-149): with a
+    // GL pixel-unpack buffer of W*H*4 bytes registered (its GL context current on this
+    // thread), Update / Tick pack the frame straight into it (vpx_gl_map -> render ->
+    // vpx_gl_unmap) and the window updates its texture from the buffer; CopyScreen then reads
+    // the screen out of it.  pbo == 0 returns to the HBM screen.
+    int UseGLBuffer(unsigned int pbo);
     int CopyAccumulator(float* host_rgba) const;
     int CopyHistory(float* host_rgba) const;  // illuminationHistoryBuffer (static branch)
 
@@ -76,6 +82,9 @@ public:
 
 private:
     int UpdateStatic(vpx_stats* stats);
+    int MapScreen(uint32_t** out) const;  // the frame's RGB8 target: the GL buffer or screen_
+    int UnmapScreen(int rc) const;
+    bool glBuffer_ = false;
     float camPos_[3] = {0, 0, 0}, camTarget_[3] = {0, 0, 1};
     bool havePrev_ = false;
     float* history_ = nullptr;      // illuminationHistoryBuffer float4[W*H] in HBM

@@ -292,6 +292,42 @@ def test_zero_copy_screen_in_mapped_host_memory(pkg):
         hip.hipHostFree(host)
 
 
+GL_PROBE = r"""
+import ctypes as C, sys
+sys.path.insert(0, sys.argv[1])
+import __graft_entry__ as entry
+pkg = entry.load_package()
+lib, abi = pkg.load_library(), pkg.abi
+h = C.c_void_p()
+assert lib.vpx_create(0, C.byref(h)) == abi.VPX_OK
+ptr, n = C.c_void_p(), C.c_size_t()
+assert lib.vpx_gl_map(h, C.byref(ptr), C.byref(n)) == abi.VPX_E_STATE      # nothing registered
+assert lib.vpx_gl_unmap(h) == abi.VPX_E_STATE                              # nothing mapped
+rc = lib.vpx_gl_register_buffer(h, 1)                                       # no GL context here
+assert rc == abi.VPX_E_DEVICE, rc
+assert b"hipGraphicsGLRegisterBuffer" in lib.vpx_last_error(h)
+assert lib.vpx_gl_map(h, C.byref(ptr), C.byref(n)) == abi.VPX_E_STATE      # the failed register left none
+assert lib.vpx_gl_register_buffer(h, 0) == abi.VPX_OK                       # unregister: a no-op
+assert lib.vpx_destroy(h) == abi.VPX_OK
+print("gl-refusal-ok")
+"""
+
+
+def test_gl_interop_refuses_cleanly_without_a_gl_context(pkg):
+    """§8(f)2 display interop (vpx_gl_register_buffer / vpx_gl_map / vpx_gl_unmap): this image
+    has libGL but no display, so no GL context can exist and the interop itself is
+    unmeasured; what is checked is the failure path — out-of-order calls are VPX_E_STATE,
+    registering without a current GL context is VPX_E_DEVICE with HIP's message, and the
+    context stays usable.  In a child process, so a HIP runtime that mishandles the missing
+    context cannot take the suite down."""
+    import subprocess
+    import sys
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", GL_PROBE, repo], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "gl-refusal-ok" in r.stdout, (r.returncode, r.stdout[-2000:], r.stderr[-2000:])
+
+
 def test_sharded_accum_frame_refuses_a_foreign_stream(pkg):
     """RCCL orders the gather after torch's current stream, so the sharded flow refuses a
     context that renders on another stream instead of gathering stale RGB8."""
