@@ -397,6 +397,20 @@ constexpr int kStepUnroll = VPX_STEP_UNROLL;  // cell steps per step-phase itera
 #ifndef VPX_STEP_SELECT
 #define VPX_STEP_SELECT 0  // 1: branch-free commit of the step with selects (measured: C1 0.792 vs 0.780 ms, C3 6.20 vs 6.16)
 #endif
+// Brick runs per walk kind: cap | passes << 8 — after its words load, a lane steps up to
+// `cap` cells inside its brick on the register copy; `passes` loads per step-phase iteration
+// (cap 0: one cell per load, VPX_STEP_UNROLL passes).  Measured (ms, one box, base 0 / 2):
+// primary C1 0.432 -> 0.402 with 3|2<<8; shadow C3 4.01 -> 3.82 with 3|1<<8; bounce C2
+// 0.654 -> 0.569 with 4|1<<8.  Caps above 4 spill (the runs are unrolled).
+#ifndef VPX_RUN_NEAREST
+#define VPX_RUN_NEAREST (3 | 2 << 8)
+#endif
+#ifndef VPX_RUN_BOUNCE
+#define VPX_RUN_BOUNCE (4 | 1 << 8)
+#endif
+#ifndef VPX_RUN_SHADOW
+#define VPX_RUN_SHADOW (3 | 1 << 8)
+#endif
 #ifndef VPX_STEP_PREFETCH
 #define VPX_STEP_PREFETCH 0  // 1: both cells of an iteration load their words together (measured slower: C1 0.815 vs 0.773 ms, C3 6.38 vs 6.14)
 #endif
@@ -420,9 +434,11 @@ __device__ unsigned long long g_phase[32];
 // Phases are wave-uniform: cell steps while enough lanes want one (see SKIPW), then the
 // waiting lanes skip together.  Each lane runs exactly skip::walk_skip's sequence (the
 // reference's cells with the reference's floats).
-template <int PHK = 0, uint32_t SKIPW = 0, uint32_t MINC = skip::kMinCube>
+template <int PHK = 0, uint32_t SKIPW = 0, uint32_t MINC = skip::kMinCube, uint32_t RUN = 0>
 __device__ __forceinline__ bool walk_wave(const skip::GridView& g, skip::Walk& w, float bound, uint32_t& cells) {
     enum : int { kStep = 0, kSkip = 1, kMiss = 2, kHit = 3 };
+    constexpr int kRun = (int)(RUN & 255u);
+    constexpr int kPasses = (RUN >> 8) ? (int)(RUN >> 8) : kStepUnroll;
     int mode = kStep;
     VPX_PH(uint64_t cs = 0, ck = 0, ns = 0, nk = 0, ls = 0, lk = 0, fb = 0, cf = 0;)
     for (;;) {
@@ -496,8 +512,13 @@ __device__ __forceinline__ bool walk_wave(const skip::GridView& g, skip::Walk& w
                 }
             }
 #else
+            // Brick runs: the class of a cell is a function of its brick's two words only, so
+            // once they are loaded a lane keeps stepping on the register copy while it stays
+            // in that brick — the cell mask (class 1) or "all empty" (class 3) decides each
+            // cell exactly as classify would — and reloads only when it crosses into another
+            // brick (or after kRun cells): fewer dependent memory round trips per cell.
 #pragma unroll
-            for (int u = 0; u < kStepUnroll; ++u) {
+            for (int u = 0; u < kPasses; ++u) {
                 if (mode == kStep) {
                     if (!(w.t < bound)) {
                         mode = kMiss;
@@ -508,9 +529,31 @@ __device__ __forceinline__ bool walk_wave(const skip::GridView& g, skip::Walk& w
                             mode = kHit;
                         } else if (cls == 2) {
                             mode = kSkip;
-                        } else {
+                        } else if (kRun == 0) {
                             ++cells;
                             if (!skip::step1(w, g.n)) mode = kMiss;
+                        } else {
+                            const uint64_t solid = cls == 1 ? w.m1 : 0ull;
+                            const uint32_t bk = (w.X >> 2) | ((w.Y >> 2) << 10) | ((w.Z >> 2) << 20);
+                            ++cells;
+#pragma unroll
+                            for (int r = 0; r < (kRun > 0 ? kRun : 1); ++r) {
+                                if (!skip::step1(w, g.n)) {
+                                    mode = kMiss;
+                                    break;
+                                }
+                                if (r + 1 == kRun || ((w.X >> 2) | ((w.Y >> 2) << 10) | ((w.Z >> 2) << 20)) != bk)
+                                    break;  // another brick (or the run's cap): the next pass loads
+                                if (!(w.t < bound)) {
+                                    mode = kMiss;
+                                    break;
+                                }
+                                ++cells;
+                                if ((solid >> ((w.X & 3u) | ((w.Y & 3u) << 2) | ((w.Z & 3u) << 4))) & 1ull) {
+                                    mode = kHit;
+                                    break;
+                                }
+                            }
                         }
                     }
                 }
@@ -787,7 +830,7 @@ __device__ __forceinline__ void for_volumes(const SceneView& sv, f3 o, f3 d, con
 // The winner's normal and material are formed once after the loop (the reference forms
 // them at every improving hit; the last one is the winner's, from the same object-space
 // ray and t), so only t and the hit cell are carried through the walks.
-template <uint32_t SKIPW = VPX_SKIPW_NEAREST, uint32_t MINC = VPX_MINC_NEAREST>
+template <uint32_t SKIPW = VPX_SKIPW_NEAREST, uint32_t MINC = VPX_MINC_NEAREST, uint32_t RUN = VPX_RUN_NEAREST>
 __device__ __forceinline__ int32_t find_nearest(const SceneView& sv, Ray& r, Counters& k) {
     int32_t vox = -2;
     ++k.nearest;
@@ -806,7 +849,7 @@ __device__ __forceinline__ int32_t find_nearest(const SceneView& sv, Ray& r, Cou
             if (!dda_setup(vol, g.n, o, s)) return true;
             w = to_walk(s);
         }
-        if (walk_wave<0, SKIPW, MINC>(grid_view(g), w, r.t, k.cells)) {
+        if (walk_wave<0, SKIPW, MINC, RUN>(grid_view(g), w, r.t, k.cells)) {
             r.t = w.t;
             hx = w.X, hy = w.Y, hz = w.Z;
             vox = (int32_t)i;
@@ -861,7 +904,7 @@ __device__ __forceinline__ bool is_occluded(const SceneView& sv, const Ray& r, C
         if (!dda_setup(vol, g.n, o, s)) return true;
         skip::Walk w = to_walk(s);
         // first solid cell with t < bound: occluded, the reference returns (no later volume)
-        occ = walk_wave<16, VPX_SKIPW_SHADOW, VPX_MINC_SHADOW>(grid_view(g), w, r.t, k.cells);
+        occ = walk_wave<16, VPX_SKIPW_SHADOW, VPX_MINC_SHADOW, VPX_RUN_SHADOW>(grid_view(g), w, r.t, k.cells);
         return !occ;
     };
     if (VPX_TLAS_SHADOW && sv.tlas_on)

@@ -582,12 +582,12 @@ __device__ __forceinline__ uint32_t block_scan(uint32_t cnt, uint32_t& total, ui
     return base + off;
 }
 
-template <uint32_t SKIPW = VPX_SKIPW_NEAREST, uint32_t MINC = VPX_MINC_NEAREST>
+template <uint32_t SKIPW = VPX_SKIPW_NEAREST, uint32_t MINC = VPX_MINC_NEAREST, uint32_t RUN = VPX_RUN_NEAREST>
 __device__ __forceinline__ void nearest_record(SceneView sv, const PathRay& pr, uint32_t p, Ray& r, Counters& k) {
     r.t = kBig;
     r.mat = kNone;
     r.N = mk(0.f, 0.f, 0.f);
-    const int32_t vox = find_nearest<SKIPW, MINC>(sv, r, k);
+    const int32_t vox = find_nearest<SKIPW, MINC, RUN>(sv, r, k);
     pr.H[pr.at(p)] = make_float4(r.t, r.N.x, r.N.y, r.N.z);
     pr.HM[pr.at(p)] = r.mat | ((uint32_t)(vox + 2) << 8) | (r.inside ? 0x80000000u : 0u);
 }
@@ -606,7 +606,7 @@ __device__ __forceinline__ ORay path_oray(const vpx_volume& vol, const PathRay& 
 // walk state lives across the walk — the ray is read back from the path buffers and
 // transformed again for the normal (the same operations, so the same values), which
 // keeps the walker's registers from spilling.
-template <uint32_t SKIPW = VPX_SKIPW_NEAREST, uint32_t MINC = VPX_MINC_NEAREST>
+template <uint32_t SKIPW = VPX_SKIPW_NEAREST, uint32_t MINC = VPX_MINC_NEAREST, uint32_t RUN = VPX_RUN_NEAREST>
 __device__ __forceinline__ void nearest_record_1v(const SceneView& sv, const PathRay& w, uint32_t p, Counters& k) {
     const vpx_volume* vol = uni_ptr(&sv.volumes[0]);
     const DevGrid g = sv.grids[vol->grid_id];
@@ -618,7 +618,7 @@ __device__ __forceinline__ void nearest_record_1v(const SceneView& sv, const Pat
         Dda s;
         if (dda_setup(*vol, g.n, o, s)) {
             wk = to_walk(s);
-            hit = walk_wave<0, SKIPW, MINC>(grid_view(g), wk, kBig, k.cells);
+            hit = walk_wave<0, SKIPW, MINC, RUN>(grid_view(g), wk, kBig, k.cells);
         }
     }
     asm volatile("" ::: "memory");  // re-read the ray below instead of keeping it live
@@ -815,7 +815,7 @@ __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_NEAREST : VPX_WPE_MULTI_
     for (uint32_t i = threadIdx.x; i < total; i += 256u) {
         const uint32_t q = lst[i];
         if (ONE) {
-            nearest_record_1v<VPX_SKIPW_BOUNCE, VPX_MINC_BOUNCE>(sv, PathRay{w.O, w.D, w.H, w.HM, 0u}, q, k);
+            nearest_record_1v<VPX_SKIPW_BOUNCE, VPX_MINC_BOUNCE, VPX_RUN_BOUNCE>(sv, PathRay{w.O, w.D, w.H, w.HM, 0u}, q, k);
             continue;
         }
         const float4 o = w.O[q], d = w.D[q];
@@ -823,7 +823,7 @@ __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_NEAREST : VPX_WPE_MULTI_
         r.O = mk(o.x, o.y, o.z);
         r.D = mk(d.x, d.y, d.z);
         r.inside = (__float_as_uint(d.w) & kInside) != 0u;
-        nearest_record<VPX_SKIPW_BOUNCE, VPX_MINC_BOUNCE>(sv, PathRay{w.O, w.D, w.H, w.HM, 0u}, q, r, k);
+        nearest_record<VPX_SKIPW_BOUNCE, VPX_MINC_BOUNCE, VPX_RUN_BOUNCE>(sv, PathRay{w.O, w.D, w.H, w.HM, 0u}, q, r, k);
     }
     flush_counters(k, 0u, ctr, VPX_STAGE_BOUNCE);
 }
@@ -909,7 +909,7 @@ __device__ __forceinline__ void shadow_tile(const SceneView& sv, const WaveBufs&
                 Dda s;
                 if (dda_setup(*vol, g.n, o, s)) {
                     skip::Walk wk = to_walk(s);
-                    hit = walk_wave<16, VPX_SKIPW_SHADOW, VPX_MINC_SHADOW>(grid_view(g), wk, so.w, k.cells);
+                    hit = walk_wave<16, VPX_SKIPW_SHADOW, VPX_MINC_SHADOW, VPX_RUN_SHADOW>(grid_view(g), wk, so.w, k.cells);
                 }
             }
             asm volatile("" ::: "memory");
