@@ -53,7 +53,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level
 METRIC = "Mray/s (primary+shadow) at 1920×1080, 1024³ world; 1/2/4/8-GPU"
 EXTRA_CONFIGS = ("C2", "C3", "C4")
 STAGE_KERNELS = {"primary": "k_primary", "shade": "k_shade", "shadow": "k_shadow_tile", "resolve": "k_resolve",
-                 "bounce": "k_nearest_tile", "finish": "k_finish"}
+                 "bounce": "k_nearest_tile", "finish": "k_finish", "frame": "k_frame0"}
 
 
 def weak_size(n, base=(1920, 1080)):
@@ -218,6 +218,8 @@ def run_config(pkg, env, cfg, steps, warmup, weak=False, sha=None):
         local_pix = float(st.primary_rays)
         if dom == "finish":
             alg_bytes = local_pix / K / spp * 36.0
+        elif dom == "frame":  # k_frame0: the whole depth-0 frame (every stage's cells + the finish)
+            alg_bytes = (sum(float(v[2]) for v in prof.values()) + local_pix * 36.0) / max(dom_launches, 1)
         else:
             alg_bytes = float(dom_cells) / max(dom_launches, 1)
             if dom == "shadow" and fused:

@@ -338,7 +338,9 @@ int vpx_get_counters(vpx_ctx* ctx, vpx_stats* out, int reset);
 #define VPX_STAGE_RESOLVE 3  /* light sums                                              */
 #define VPX_STAGE_BOUNCE 4   /* Renderer::FindNearest of bounce rays                    */
 #define VPX_STAGE_FINISH 5   /* fold + accumulate + tonemap (or tile pack)              */
-#define VPX_NUM_STAGES 6
+#define VPX_STAGE_FRAME 6    /* a whole Trace-depth-0 frame in one launch (small launches,
+                                single volume: stages 0, 1, 2, 3, 5 fused)    */
+#define VPX_NUM_STAGES 7
 typedef struct vpx_profile {
     float stage_ms[8];            /* summed device time per stage (HIP events on the stream) */
     uint32_t stage_launches[8];   /* kernel launches timed per stage                         */

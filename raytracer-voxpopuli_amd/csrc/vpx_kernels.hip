@@ -670,6 +670,14 @@ int launch_render(vpx_ctx* c, const SceneView& sv, const FrameArgs& f, uint32_t 
     const dim3 ggrid((tiles + kGroupTiles - 1) / kGroupTiles);
     // single volume, no analytic shapes: the DDA kernels' lean instances
     const bool one = sv.num_volumes == 1 && !(sv.num_spheres | sv.num_triangles);
+    const bool fuse_tail = kFuseTail && !rp && kGroupTiles == 1;
+    if (VPX_FUSE_FRAME && one && kFuseHead && fuse_tail && f.max_bounces == 0 && tiles <= VPX_FUSE_FRAME_TILES) {
+        prof_mark(c, VPX_STAGE_FRAME);  // the whole depth-0 frame, one launch (k_frame0)
+        hipLaunchKernelGGL((k_frame0<true, MODE>), grid, block, slds, c->stream, sv, f, w, c->d_ctr, accum, rgb8, packed);
+        prof_mark(c, -1);
+        VPX_HIP(c, hipGetLastError());
+        return VPX_OK;
+    }
     prof_mark(c, VPX_STAGE_PRIMARY);
     const bool fuse_head = kFuseHead && f.max_bounces >= 0;
     if (fuse_head)
@@ -680,7 +688,6 @@ int launch_render(vpx_ctx* c, const SceneView& sv, const FrameArgs& f, uint32_t 
                            w, c->d_ctr);
     prof_mark(c, -1);
     // the last level's shadow -> resolve -> finish as one launch (k_shadow_finish)
-    const bool fuse_tail = kFuseTail && !rp && kGroupTiles == 1;
     for (int level = 0; level <= f.max_bounces; ++level) {
         if (!(fuse_head && level == 0)) {
             prof_mark(c, VPX_STAGE_SHADE);

@@ -411,6 +411,9 @@ constexpr int kStepUnroll = VPX_STEP_UNROLL;  // cell steps per step-phase itera
 #ifndef VPX_RUN_SHADOW
 #define VPX_RUN_SHADOW (3 | 1 << 8)
 #endif
+#ifndef VPX_BRICK_PREFETCH
+#define VPX_BRICK_PREFETCH 0  // 1: a brick run first loads the words of the brick it will exit into
+#endif
 #ifndef VPX_STEP_PREFETCH
 #define VPX_STEP_PREFETCH 0  // 1: both cells of an iteration load their words together (measured slower: C1 0.815 vs 0.773 ms, C3 6.38 vs 6.14)
 #endif
@@ -440,6 +443,11 @@ __device__ __forceinline__ bool walk_wave(const skip::GridView& g, skip::Walk& w
     constexpr int kRun = (int)(RUN & 255u);
     constexpr int kPasses = (RUN >> 8) ? (int)(RUN >> 8) : kStepUnroll;
     int mode = kStep;
+    // brick-exit prefetch (VPX_BRICK_PREFETCH): the level words of brick pkey, loaded while
+    // the lane ran through the brick before it (the world is static, so they stay valid)
+    uint64_t pm1 = 0ull, pm2 = 0ull;
+    uint32_t pkey = ~0u;
+    (void)pm1, (void)pm2, (void)pkey;
     VPX_PH(uint64_t cs = 0, ck = 0, ns = 0, nk = 0, ls = 0, lk = 0, fb = 0, cf = 0;)
     for (;;) {
         VPX_PH(uint64_t t0 = __builtin_amdgcn_s_memtime();)
@@ -523,7 +531,12 @@ __device__ __forceinline__ bool walk_wave(const skip::GridView& g, skip::Walk& w
                     if (!(w.t < bound)) {
                         mode = kMiss;
                     } else {
-                        const int cls = skip::classify<MINC>(w, g);
+                        const uint32_t bk = (w.X >> 2) | ((w.Y >> 2) << 10) | ((w.Z >> 2) << 20);
+                        int cls;
+                        if (VPX_BRICK_PREFETCH && kRun > 0 && bk == pkey)
+                            cls = skip::classify_words<MINC>(w, skip::Words{pm1, pm2});
+                        else
+                            cls = skip::classify<MINC>(w, g);
                         if (cls == 0) {
                             ++cells;
                             mode = kHit;
@@ -534,7 +547,22 @@ __device__ __forceinline__ bool walk_wave(const skip::GridView& g, skip::Walk& w
                             if (!skip::step1(w, g.n)) mode = kMiss;
                         } else {
                             const uint64_t solid = cls == 1 ? w.m1 : 0ull;
-                            const uint32_t bk = (w.X >> 2) | ((w.Y >> 2) << 10) | ((w.Z >> 2) << 20);
+#if VPX_BRICK_PREFETCH
+                            {  // the brick this run will most likely exit into: first boundary crossing
+                                const float ex = w.tx + (float)(w.sx > 0 ? 3u - (w.X & 3u) : (w.X & 3u)) * w.dx;
+                                const float ey = w.ty + (float)(w.sy > 0 ? 3u - (w.Y & 3u) : (w.Y & 3u)) * w.dy;
+                                const float ez = w.tz + (float)(w.sz > 0 ? 3u - (w.Z & 3u) : (w.Z & 3u)) * w.dz;
+                                uint32_t nx = w.X >> 2, ny = w.Y >> 2, nz = w.Z >> 2;
+                                if (ex <= ey && ex <= ez) nx += (uint32_t)w.sx;
+                                else if (ey <= ez) ny += (uint32_t)w.sy;
+                                else nz += (uint32_t)w.sz;
+                                if ((nx << 2) < g.n && (ny << 2) < g.n && (nz << 2) < g.n && nx < 1024u && ny < 1024u && nz < 1024u) {
+                                    pm1 = skip::load_mask(g.l1, skip::blk_index(nx, ny, nz, g.nb2));
+                                    pm2 = skip::load_mask(g.l2, skip::blk_index(nx >> 2, ny >> 2, nz >> 2, g.nb3));
+                                    pkey = nx | (ny << 10) | (nz << 20);
+                                }
+                            }
+#endif
                             ++cells;
 #pragma unroll
                             for (int r = 0; r < (kRun > 0 ? kRun : 1); ++r) {
@@ -569,6 +597,7 @@ __device__ __forceinline__ bool walk_wave(const skip::GridView& g, skip::Walk& w
         }
         VPX_PH(++nk; lk += __popcll(skipping);)
         VPX_MARK("skip phase");
+        pkey = ~0u;  // the prefetch does not live across a skip phase (its registers are free there)
         if (mode == kSkip) {
             uint32_t lo[3], hi[3];
             skip::df_box(w, g.n, lo, hi);

@@ -641,9 +641,9 @@ __device__ __forceinline__ void nearest_record_1v(const SceneView& sv, const Pat
 // Primary rays + Renderer::FindNearest.  Every path's ray / RNG state is written; rays
 // that cannot hit a voxel or shape (one volume, no shapes, Setup3DDDA fails: the
 // reference returns before reading a cell) get their miss record directly.
-template <bool ONE, bool SHADE = false>
-__global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_NEAREST : VPX_WPE_MULTI_NEAREST) void k_primary(SceneView sv, FrameArgs f, WaveBufs w,
-                                                 unsigned long long* __restrict__ ctr) {
+template <bool ONE, bool SHADE>
+__device__ __forceinline__ void primary_tile(SceneView& sv, const FrameArgs& f, const WaveBufs& w,
+                                             unsigned long long* __restrict__ ctr) {
     __shared__ uint32_t sh[4];
     __shared__ uint32_t lst[256];
     // the fused head keeps the tile's rays and hit records in LDS: its walkers and its
@@ -725,6 +725,12 @@ __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_NEAREST : VPX_WPE_MULTI_
         shade_path<true>(sv, f, w, pr, p, 0, ks);
         flush_counters(ks, 0u, ctr, VPX_STAGE_SHADE);
     }
+}
+
+template <bool ONE, bool SHADE = false>
+__global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_NEAREST : VPX_WPE_MULTI_NEAREST) void k_primary(SceneView sv, FrameArgs f, WaveBufs w,
+                                                 unsigned long long* __restrict__ ctr) {
+    primary_tile<ONE, SHADE>(sv, f, w, ctr);
 }
 
 #ifndef VPX_BOUNCE_BUCKETS
@@ -1030,6 +1036,38 @@ __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_SHADOW : VPX_WPE_MULTI_S
     SceneView sv, FrameArgs f, WaveBufs w, unsigned long long* __restrict__ ctr, float4* __restrict__ accum,
     uint32_t* __restrict__ rgb8, float4* __restrict__ packed) {
     if (!ONE) stage_tlas(sv);
+    shadow_tile<ONE>(sv, w, ctr);
+    __syncthreads();
+    const uint32_t p = tile_block() * 256u + threadIdx.x;
+    resolve_path(sv, w, p);
+    finish_path<MODE>(f, w, p, accum, rgb8, packed);
+}
+
+// A Trace-depth-0 frame in one launch (VPX_FUSE_FRAME): the fused head (primary walk +
+// level-0 shade) and the fused tail (the tile's shadow walks, resolve, finish) of the same
+// tile, one barrier apart — the shade's slots are read back by the workgroup that wrote them
+// (as k_shadow_finish reads its own occluded flags), and a tile's shadow walks overlap other
+// tiles' primary walks instead of waiting for the slowest primary wave of the frame.
+// Used for single-volume launches of at most VPX_FUSE_FRAME_TILES tiles, where the walkers'
+// drain tails dominate (one MI355X, ms, two launches -> one, VPX_WPE_FRAME 5: C1 0.723 ->
+// 0.713; rank 0's share of C1 at 8 ranks 0.297 -> 0.228; C1 at 64x64 0.234 -> 0.198).  On
+// the big launches the two kernels stay apart (C3 5.84 vs 6.14; C4, 65 volumes, 59.3 vs
+// 64.5): there the separate kernels' 6 waves/SIMD pay more than the shared drain.
+#ifndef VPX_FUSE_FRAME
+#define VPX_FUSE_FRAME 1
+#endif
+#ifndef VPX_FUSE_FRAME_TILES
+#define VPX_FUSE_FRAME_TILES 12288
+#endif
+#ifndef VPX_WPE_FRAME
+#define VPX_WPE_FRAME 5  // 6: 272 spilled VGPRs; 5: 9; 4: none but slower
+#endif
+template <bool ONE, int MODE>
+__global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_FRAME : VPX_WPE_MULTI_NEAREST) void k_frame0(
+    SceneView sv, FrameArgs f, WaveBufs w, unsigned long long* __restrict__ ctr, float4* __restrict__ accum,
+    uint32_t* __restrict__ rgb8, float4* __restrict__ packed) {
+    primary_tile<ONE, true>(sv, f, w, ctr);
+    __syncthreads();
     shadow_tile<ONE>(sv, w, ctr);
     __syncthreads();
     const uint32_t p = tile_block() * 256u + threadIdx.x;

@@ -227,6 +227,45 @@ def test_sharded_accumulator_equals_monolithic(pkg, orc):
     ctx.close()
 
 
+def test_fused_frame_equals_two_launch_frame(pkg):
+    """The depth-0 frame runs as one launch (k_frame0) up to VPX_FUSE_FRAME_TILES (12288)
+    tiles and as k_primary + k_shadow_finish above.  The same 2048x1600 frame (12800 tiles)
+    rendered whole (two launches) and as two ranks' halves (6400 tiles each: fused) must
+    agree bit for bit over 2 AA frames with area lights; the profile names the stage each
+    path ran (frame vs primary + shadow) and the cells add up."""
+    sc = pkg.scene
+    desc = sc.city_scene("monu3", 128, 2048, 1600, 0, areas=sc.C3_AREAS[:2])
+    desc.flags = pkg.abi.VPX_FLAG_AA
+    W, H = desc.width, desc.height
+    ctx = make_ctx(pkg, desc)
+    acc = torch.zeros(W * H * 4, dtype=torch.float32, device="cuda")
+    rgb = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+    R = 2
+    L = ctx.packed_len(W, H, R)
+    accs = [torch.zeros(L * 4, dtype=torch.float32, device="cuda") for _ in range(R)]
+    gathered = torch.zeros(R * L, dtype=torch.int32, device="cuda")
+    rgb_sh = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    ctx.profile_enable(64)
+    for f in range(2):
+        p = desc.frame_params(f)
+        ctx.profile_read(reset=True)
+        ctx.render(p, acc.data_ptr(), rgb.data_ptr())
+        whole = ctx.profile_read(reset=True)
+        for rank in range(R):
+            ctx.render_tiles_accum(p, rank, R, accs[rank].data_ptr(), gathered.data_ptr() + rank * L * 4)
+        halves = ctx.profile_read(reset=True)
+        ctx.composite_rgb8(p, R, gathered.data_ptr(), rgb_sh.data_ptr())
+        assert whole["frame"][1] == 0 and whole["primary"][1] == 1 and whole["shadow"][1] == 1
+        assert halves["frame"][1] == R and halves["primary"][1] == 0 and halves["shadow"][1] == 0
+        assert sum(v[2] for v in whole.values()) == sum(v[2] for v in halves.values()) > 0
+    ctx.synchronize()
+    assert np.array_equal(rgb_sh.cpu().numpy(), rgb.cpu().numpy())
+    acc_img = pkg.dist.unpack(np.concatenate([a.cpu().numpy() for a in accs]), W, H, R)
+    assert np.array_equal(bits(acc_img).reshape(-1), bits(acc.cpu().numpy()).reshape(-1))
+    ctx.close()
+
+
 @pytest.mark.parametrize("devices", [[0], [0, 0], [0, 0, 0, 0]])
 def test_device_set_equals_single_device(pkg, orc, devices):
     """vpx_create_multi: the frame's tiles dealt over the members, gathered to devices[0]

@@ -13,6 +13,8 @@ pkg = entry.load_package()
 lib = pkg.abi.load_library()
 lib.vpx_debug_phase.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
 desc = pkg.scene.CONFIGS[os.environ.get("CFG", "C1")]()
+if os.environ.get("TW"):  # the same world and camera at another resolution (latency-floor studies)
+    desc = desc.with_size(int(os.environ["TW"]), int(os.environ["TH"]))
 ctx = pkg.context.Context(0)
 ctx.load_scene(desc)
 W, H = desc.width, desc.height

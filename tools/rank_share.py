@@ -1,0 +1,48 @@
+"""One rank's GPU time in the N-GPU strong-scaling run, measured on one GPU: rank 0's share
+of a config's frame (vpx_render_tiles_accum, rank 0 of R) for R = 1, 2, 4, 8 — the render
+part of bench.py --gpus R without the gather.  CFG (default C1), K frames per R.
+"""
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import __graft_entry__ as entry  # noqa: E402
+
+pkg = entry.load_package()
+cfg = os.environ.get("CFG", "C1")
+desc = pkg.scene.CONFIGS[cfg]()
+K = int(os.environ.get("K", "20"))
+s = torch.cuda.Stream()
+torch.cuda.set_stream(s)
+ctx = pkg.context.Context(0)
+ctx.set_stream(s.cuda_stream)
+ctx.load_scene(desc)
+W, H = desc.width, desc.height
+spp = max(1, int(desc.spp))
+out = []
+for R in (1, 2, 4, 8):
+    L = ctx.packed_len(W, H, R)
+    acc = torch.zeros(L * 4, dtype=torch.float32, device="cuda")
+    rgb = torch.zeros(L, dtype=torch.int32, device="cuda")
+    params = [desc.frame_params(frame_index=f) for f in range(spp)]
+
+    def step():
+        for p in params:
+            ctx.render_tiles_accum(p, 0, R, acc.data_ptr(), rgb.data_ptr())
+
+    for _ in range(2):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(K):
+        step()
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) * 1e3 / K
+    out.append((R, ms))
+    del acc, rgb
+base = out[0][1]
+print(cfg, " ".join(f"R={R}: {ms:.4f} ms (x{base / ms:.2f})" for R, ms in out))
+ctx.close()
