@@ -323,6 +323,24 @@ __global__ void df_plane_k(uint8_t* __restrict__ l1b, const uint64_t* __restrict
     l1b[(size_t)skip::blk_index(x, y, z, nb2) * 8 + o] = skip::df_value(x, y, z, o, nb1, occ, get);
 }
 
+// The octant planes from the built levels (after build_df): byte o of an empty brick's l1
+// word into plane o, 0 for an occupied brick (and for the padding bricks, never walked).
+__global__ void build_planes_k(const uint64_t* __restrict__ l1, const uint64_t* __restrict__ l2, uint32_t nb2,
+                               uint32_t nb3, uint8_t* __restrict__ dfp) {
+    const uint64_t plane = (uint64_t)nb2 * nb2 * nb2 * 64;
+    for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < plane; s += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t parent = s >> 6;
+        const uint32_t j = (uint32_t)(s & 63u);
+        const uint32_t bx = (uint32_t)(parent % nb2) * 4 + (j & 3u);
+        const uint32_t by = (uint32_t)((parent / nb2) % nb2) * 4 + ((j >> 2) & 3u);
+        const uint32_t bz = (uint32_t)(parent / ((uint64_t)nb2 * nb2)) * 4 + (j >> 4);
+        const bool occ = (l2[skip::blk_index(bx >> 2, by >> 2, bz >> 2, nb3)] >> ((bx & 3u) | ((by & 3u) << 2) | ((bz & 3u) << 4))) & 1ull;
+        const uint64_t m = occ ? 0ull : l1[s];
+#pragma unroll
+        for (uint32_t o = 0; o < 8; ++o) dfp[o * plane + s] = (uint8_t)(m >> (8 * o));
+    }
+}
+
 // Scatter a staged box (x fastest) into the grid.
 __global__ void write_box_k(uint8_t* __restrict__ grid, uint32_t n, const uint8_t* __restrict__ src, uint32_t x0,
                             uint32_t y0, uint32_t z0, uint32_t dx, uint32_t dy, uint32_t dz) {
@@ -379,7 +397,9 @@ struct vpx_ctx {
         uint8_t* ptr = nullptr;
         uint64_t* l1 = nullptr;
         uint64_t* l2 = nullptr;
+        uint8_t* dfp = nullptr;  // distance-field octant planes (build_planes_k)
         uint32_t n = 0, nb1 = 0, nb2 = 0, nb3 = 0;
+        uint64_t plane() const { return 64ull * nb2 * nb2 * nb2; }
     };
     std::vector<GridBuf> grids;
     DevGrid* d_grids = nullptr;
@@ -523,7 +543,7 @@ int sync_grids(vpx_ctx* c) {
     std::vector<DevGrid> h(n);
     for (uint32_t i = 0; i < n; ++i) {
         const auto& g = c->grids[i];
-        h[i] = DevGrid{g.ptr, g.l1, g.l2, g.n, g.nb1, g.nb2, g.nb3};
+        h[i] = DevGrid{g.ptr, g.l1, g.l2, g.n, g.nb1, g.nb2, g.nb3, g.dfp, g.plane()};
     }
     if (n) VPX_HIP(c, hipMemcpy(c->d_grids, h.data(), sizeof(DevGrid) * n, hipMemcpyHostToDevice));
     return VPX_OK;
@@ -810,6 +830,7 @@ int vpx_destroy(vpx_ctx* c) {
         if (g.ptr) (void)hipFree(g.ptr);
         if (g.l1) (void)hipFree(g.l1);
         if (g.l2) (void)hipFree(g.l2);
+        if (g.dfp) (void)hipFree(g.dfp);
     }
     void* ptrs[] = {c->d_grids, c->d_volumes, c->d_vbounds, c->d_tlas, c->d_bvh, c->d_materials, c->d_points, c->d_spots, c->d_areas,
                     c->d_spheres, c->d_triangles, c->d_ctr, c->d_sum, c->d_scratch, c->d_wave, c->d_sky};
@@ -910,7 +931,8 @@ static int alloc_grid(vpx_ctx* c, uint32_t id, uint32_t n) {
         (void)hipFree(g.ptr);
         (void)hipFree(g.l1);
         (void)hipFree(g.l2);
-        g.ptr = nullptr, g.l1 = nullptr, g.l2 = nullptr;
+        (void)hipFree(g.dfp);
+        g.ptr = nullptr, g.l1 = nullptr, g.l2 = nullptr, g.dfp = nullptr;
     }
     g.n = n;
     g.nb1 = (n + 3) / 4;
@@ -920,6 +942,7 @@ static int alloc_grid(vpx_ctx* c, uint32_t id, uint32_t n) {
         VPX_HIP(c, hipMalloc(&g.ptr, bytes));
         VPX_HIP(c, hipMalloc(&g.l1, sizeof(uint64_t) * (size_t)g.nb2 * g.nb2 * g.nb2 * 64));
         VPX_HIP(c, hipMalloc(&g.l2, sizeof(uint64_t) * (size_t)g.nb3 * g.nb3 * g.nb3 * 64));
+        VPX_HIP(c, hipMalloc(&g.dfp, 8 * g.plane()));
     }
     return sync_grids(c);
 }
@@ -934,6 +957,8 @@ static int build_df(vpx_ctx* c, const vpx_ctx::GridBuf& g) {
         hipLaunchKernelGGL(df_plane_k, dim3(blocks), dim3(256), 0, c->stream, (uint8_t*)g.l1, g.l2, g.nb1, g.nb2, g.nb3, s);
         VPX_HIP(c, hipGetLastError());
     }
+    hipLaunchKernelGGL(build_planes_k, dim3(2048), dim3(256), 0, c->stream, g.l1, g.l2, g.nb2, g.nb3, g.dfp);
+    VPX_HIP(c, hipGetLastError());
     return VPX_OK;
 }
 

@@ -239,11 +239,16 @@ namespace skip {
 // empty brick, its distance-field word: byte o (octant o = [sx<0] | [sy<0]<<1 | [sz<0]<<2)
 // = k >= 1 such that the k^3 bricks from this one toward the octant are all empty (bricks
 // outside the grid count as empty), capped at 255.
+// dfp (optional): the distance field again as 8 octant planes of one byte per brick (plane
+// o at dfp + o * plane, brick at blk_index), 0 for an occupied brick — a walk reads only
+// its own octant's plane, 1 byte per brick instead of an 8-byte word (classify_dfp).
 struct GridView {
     const uint8_t* cells;
     const uint64_t* l1;
     const uint64_t* l2;
     uint32_t n, nb1, nb2, nb3;
+    const uint8_t* dfp;
+    uint64_t plane;
 };
 
 struct Walk {
@@ -332,6 +337,32 @@ VPX_HD int classify(Walk& w, const GridView& g) {
     const int cell = ((w.m1 >> cb) & 1ull) ? 0 : 1;
     const int brick = ((uint32_t)(w.m1 >> w.osh) & 255u) >= MINC ? 2 : 3;
     return ((w.m2 >> bb) & 1ull) ? cell : brick;
+}
+
+// The same class from the octant plane `pl` (g.dfp + octant * g.plane): one byte per step
+// from a plane an eighth the size of l1, and the brick's cell mask only when the byte says
+// occupied (0) — a dependent second load, but walks step mostly through empty bricks.
+// For an empty brick m1 gets the byte at the octant's shift, as the l1 word holds it, so
+// df_box reads the cube the same way.
+VPX_HD uint32_t load_u8(const uint8_t* p, uint32_t i) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return ((const __attribute__((address_space(1))) uint8_t*)p)[i];
+#else
+    return p[i];
+#endif
+}
+template <uint32_t MINC = kMinCube>
+VPX_HD int classify_dfp(Walk& w, const GridView& g, const uint8_t* pl) {
+    const uint32_t X = w.X, Y = w.Y, Z = w.Z;
+    const uint32_t bi = blk_index(X >> 2, Y >> 2, Z >> 2, g.nb2);
+    const uint32_t k = load_u8(pl, bi);
+    if (k == 0u) {
+        w.m1 = load_mask(g.l1, bi);
+        const uint32_t cb = (X & 3u) | ((Y & 3u) << 2) | ((Z & 3u) << 4);
+        return ((w.m1 >> cb) & 1ull) ? 0 : 1;
+    }
+    w.m1 = (uint64_t)k << w.osh;
+    return k >= MINC ? 2 : 3;
 }
 
 // The empty box of a class-2 cell: its brick's distance-field cube toward the ray's
@@ -692,6 +723,20 @@ inline void build_masks_host(const uint8_t* cells, uint32_t n, uint64_t* l1, uin
                                    z = (o & 4u) ? nb1 - 1 - fz : fz;
                     if (!occ(x, y, z)) bytes[(size_t)blk_index(x, y, z, nb2) * 8 + o] = df_value(x, y, z, o, nb1, occ, get);
                 }
+}
+
+// The octant planes from built levels (as build_planes_k): dfp holds 8 * nb2^3 * 64 bytes.
+inline void build_planes_host(const uint64_t* l1, const uint64_t* l2, uint32_t n, uint8_t* dfp) {
+    const uint32_t nb1 = (n + 3) / 4, nb2 = (nb1 + 3) / 4, nb3 = (nb2 + 3) / 4;
+    const uint64_t plane = 64ull * nb2 * nb2 * nb2;
+    std::memset(dfp, 0, 8 * plane);
+    for (uint32_t z = 0; z < nb1; ++z)
+        for (uint32_t y = 0; y < nb1; ++y)
+            for (uint32_t x = 0; x < nb1; ++x) {
+                if ((l2[blk_index(x >> 2, y >> 2, z >> 2, nb3)] >> ((x & 3) + 4 * (y & 3) + 16 * (z & 3))) & 1ull) continue;
+                const uint32_t b = blk_index(x, y, z, nb2);
+                for (uint32_t o = 0; o < 8; ++o) dfp[o * plane + b] = (uint8_t)(l1[b] >> (8 * o));
+            }
 }
 #endif
 

@@ -43,6 +43,8 @@ struct DevGrid {
     uint32_t nb1;  // bricks per axis  = ceil(n / 4)
     uint32_t nb2;  // macros per axis  = ceil(nb1 / 4)
     uint32_t nb3;  // macro parents per axis (l2 blocking) = ceil(nb2 / 4)
+    const uint8_t* dfp;  // the distance field as 8 octant planes of bytes (vpx_skip.hpp GridView)
+    uint64_t plane;      // bytes per octant plane = nb2^3 * 64
 };
 
 // Instance TLAS over the world bounds of volumes 1..n-1 (built on the host by vpx_set_volumes
@@ -348,7 +350,7 @@ __device__ __forceinline__ T* uni_ptr(T* p) {
 }
 __device__ __forceinline__ skip::GridView grid_view(const DevGrid& g) {
     return skip::GridView{uni_ptr(g.cells), uni_ptr(g.l1), uni_ptr(g.l2), uni(g.n), uni(g.nb1), uni(g.nb2),
-                          uni(g.nb3)};
+                          uni(g.nb3),       uni_ptr(g.dfp), g.plane};
 }
 __device__ __forceinline__ skip::Walk to_walk(const Dda& s) {
     skip::Walk w;
@@ -402,14 +404,25 @@ constexpr int kStepUnroll = VPX_STEP_UNROLL;  // cell steps per step-phase itera
 // (cap 0: one cell per load, VPX_STEP_UNROLL passes).  Measured (ms, one box, base 0 / 2):
 // primary C1 0.432 -> 0.402 with 3|2<<8; shadow C3 4.01 -> 3.82 with 3|1<<8; bounce C2
 // 0.654 -> 0.569 with 4|1<<8.  Caps above 4 spill (the runs are unrolled).
+// Bit 16 of the run word: the walk classifies from its octant plane (skip::classify_dfp)
+// instead of the l1 + l2 words (VPX_DFP_*).
+#ifndef VPX_DFP_NEAREST
+#define VPX_DFP_NEAREST 1
+#endif
+#ifndef VPX_DFP_BOUNCE
+#define VPX_DFP_BOUNCE 1
+#endif
+#ifndef VPX_DFP_SHADOW
+#define VPX_DFP_SHADOW 1
+#endif
 #ifndef VPX_RUN_NEAREST
-#define VPX_RUN_NEAREST (3 | 2 << 8)
+#define VPX_RUN_NEAREST (3 | 2 << 8 | VPX_DFP_NEAREST << 16)
 #endif
 #ifndef VPX_RUN_BOUNCE
-#define VPX_RUN_BOUNCE (4 | 1 << 8)
+#define VPX_RUN_BOUNCE (4 | 1 << 8 | VPX_DFP_BOUNCE << 16)
 #endif
 #ifndef VPX_RUN_SHADOW
-#define VPX_RUN_SHADOW (3 | 1 << 8)
+#define VPX_RUN_SHADOW (3 | 1 << 8 | VPX_DFP_SHADOW << 16)
 #endif
 #ifndef VPX_BRICK_PREFETCH
 #define VPX_BRICK_PREFETCH 0  // 1: a brick run first loads the words of the brick it will exit into
@@ -441,7 +454,10 @@ template <int PHK = 0, uint32_t SKIPW = 0, uint32_t MINC = skip::kMinCube, uint3
 __device__ __forceinline__ bool walk_wave(const skip::GridView& g, skip::Walk& w, float bound, uint32_t& cells) {
     enum : int { kStep = 0, kSkip = 1, kMiss = 2, kHit = 3 };
     constexpr int kRun = (int)(RUN & 255u);
-    constexpr int kPasses = (RUN >> 8) ? (int)(RUN >> 8) : kStepUnroll;
+    constexpr int kPasses = (RUN >> 8) & 255u ? (int)((RUN >> 8) & 255u) : kStepUnroll;
+    constexpr bool kDfp = (RUN >> 16) & 1u;
+    const uint8_t* pl = kDfp ? g.dfp + (uint64_t)(w.osh >> 3) * g.plane : nullptr;  // the ray's octant plane
+    (void)pl;
     int mode = kStep;
     // brick-exit prefetch (VPX_BRICK_PREFETCH): the level words of brick pkey, loaded while
     // the lane ran through the brick before it (the world is static, so they stay valid)
@@ -535,6 +551,8 @@ __device__ __forceinline__ bool walk_wave(const skip::GridView& g, skip::Walk& w
                         int cls;
                         if (VPX_BRICK_PREFETCH && kRun > 0 && bk == pkey)
                             cls = skip::classify_words<MINC>(w, skip::Words{pm1, pm2});
+                        else if (kDfp)
+                            cls = skip::classify_dfp<MINC>(w, g, pl);
                         else
                             cls = skip::classify<MINC>(w, g);
                         if (cls == 0) {

@@ -16,7 +16,10 @@ struct World {
     uint32_t n, nb1, nb2, nb3;
     std::vector<uint8_t> cells;
     std::vector<uint64_t> l1, l2;
-    GridView view() const { return GridView{cells.data(), l1.data(), l2.data(), n, nb1, nb2, nb3}; }
+    std::vector<uint8_t> dfp;  // octant planes (classify_dfp)
+    GridView view() const {
+        return GridView{cells.data(), l1.data(), l2.data(), n, nb1, nb2, nb3, dfp.data(), 64ull * nb2 * nb2 * nb2};
+    }
 };
 
 static World make_world(uint32_t n, uint64_t seed, double density) {
@@ -37,7 +40,36 @@ static World make_world(uint32_t n, uint64_t seed, double density) {
     w.l1.assign((size_t)w.nb2 * w.nb2 * w.nb2 * 64, 0);
     w.l2.assign((size_t)w.nb3 * w.nb3 * w.nb3 * 64, 0);
     build_masks_host(w.cells.data(), n, w.l1.data(), w.l2.data());
+    w.dfp.assign(8 * 64ull * w.nb2 * w.nb2 * w.nb2, 0);
+    build_planes_host(w.l1.data(), w.l2.data(), n, w.dfp.data());
     return w;
+}
+
+// classify_dfp (octant plane, then the mask of an occupied brick) == classify (l1 + l2
+// words) at sampled cells for every octant: the same class and the same m1 where it is read
+// (the cell mask of an occupied brick, the octant's cube byte of an empty one).
+static long check_planes(const World& W, std::mt19937_64& r) {
+    const GridView g = W.view();
+    const uint64_t cells = (uint64_t)W.n * W.n * W.n;
+    const uint64_t samples = cells < 3000000 ? cells : 3000000;
+    long bad = 0;
+    for (uint64_t i = 0; i < samples; ++i) {
+        const uint64_t c = samples == cells ? i : r() % cells;
+        for (uint32_t o = 0; o < 8; ++o) {
+            Walk a{};
+            a.X = (uint32_t)(c % W.n), a.Y = (uint32_t)((c / W.n) % W.n), a.Z = (uint32_t)(c / ((uint64_t)W.n * W.n));
+            a.sx = (o & 1) ? -1 : 1, a.sy = (o & 2) ? -1 : 1, a.sz = (o & 4) ? -1 : 1;
+            walk_begin(a);
+            Walk b = a;
+            const int ca = classify(a, g), cb = classify_dfp(b, g, g.dfp + o * g.plane);
+            const bool m1_read = ca == 1 || ca == 0 ? a.m1 == b.m1 : ((a.m1 >> a.osh) & 255u) == ((b.m1 >> b.osh) & 255u);
+            if (ca != cb || !m1_read) {
+                if (bad < 5) printf("plane mismatch n=%u cell (%u,%u,%u) octant %u: class %d/%d\n", W.n, a.X, a.Y, a.Z, o, ca, cb);
+                ++bad;
+            }
+        }
+    }
+    return bad;
 }
 
 // Setup3DDDA for the unit cube (template/scene.cpp:719-749); false = misses the cube.
@@ -143,6 +175,7 @@ int main(int argc, char** argv) {
             if (n > 256 && dens > 0.5) continue;
             World W = make_world(n, n * 31 + (uint64_t)(dens * 100), dens);
             std::mt19937_64 r(n + 7);
+            bad += check_planes(W, r);
             std::uniform_real_distribution<float> U(0.f, 1.f);
             for (long i = 0; i < rays; ++i) {
                 float O[3], T[3], D[3];
