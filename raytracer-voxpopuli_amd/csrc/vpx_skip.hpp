@@ -351,18 +351,22 @@ VPX_HD uint32_t load_u8(const uint8_t* p, uint32_t i) {
     return p[i];
 #endif
 }
+// (k: the brick's plane byte, already loaded)
 template <uint32_t MINC = kMinCube>
-VPX_HD int classify_dfp(Walk& w, const GridView& g, const uint8_t* pl) {
+VPX_HD int classify_dfp_byte(Walk& w, const GridView& g, uint32_t k) {
     const uint32_t X = w.X, Y = w.Y, Z = w.Z;
-    const uint32_t bi = blk_index(X >> 2, Y >> 2, Z >> 2, g.nb2);
-    const uint32_t k = load_u8(pl, bi);
     if (k == 0u) {
+        const uint32_t bi = blk_index(X >> 2, Y >> 2, Z >> 2, g.nb2);
         w.m1 = load_mask(g.l1, bi);
         const uint32_t cb = (X & 3u) | ((Y & 3u) << 2) | ((Z & 3u) << 4);
         return ((w.m1 >> cb) & 1ull) ? 0 : 1;
     }
     w.m1 = (uint64_t)k << w.osh;
     return k >= MINC ? 2 : 3;
+}
+template <uint32_t MINC = kMinCube>
+VPX_HD int classify_dfp(Walk& w, const GridView& g, const uint8_t* pl) {
+    return classify_dfp_byte<MINC>(w, g, load_u8(pl, blk_index(w.X >> 2, w.Y >> 2, w.Z >> 2, g.nb2)));
 }
 
 // The empty box of a class-2 cell: its brick's distance-field cube toward the ray's
