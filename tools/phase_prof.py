@@ -31,4 +31,4 @@ for name, off in (("nearest", 0), ("shadow", 16)):
     print(f"[{name}] walk calls(waves)={walks}  step: cycles={cs:.3e} iters={ns} lanes/iter={ls / max(ns, 1):.1f} "
           f"cyc/iter={cs / max(ns, 1):.0f} | skip: cycles={ck:.3e} iters={nk} lanes/iter={lk / max(nk, 1):.1f} "
           f"cyc/iter={ck / max(nk, 1):.0f} | per walk: step it={ns / walks:.1f} skip it={nk / walks:.1f} | "
-          f"refused lanes/iter={fb / max(nk, 1):.2f}")
+          f"refused lanes/iter={fb / max(nk, 1):.2f} | finished lanes/step iter={cf / max(ns, 1):.1f}")
