@@ -451,8 +451,15 @@ __device__ unsigned long long g_phase[32];
 // Phases are wave-uniform: cell steps while enough lanes want one (see SKIPW), then the
 // waiting lanes skip together.  Each lane runs exactly skip::walk_skip's sequence (the
 // reference's cells with the reference's floats).
-template <int PHK = 0, uint32_t SKIPW = 0, uint32_t MINC = skip::kMinCube, uint32_t RUN = 0>
-__device__ __forceinline__ bool walk_wave(const skip::GridView& g, skip::Walk& w, float bound, uint32_t& cells) {
+//
+// BUDGET > 0: the wave stops after BUDGET step iterations + skip phases (wave-uniform) and
+// *open tells which lanes are unfinished: their state is a walk to be continued (mode kStep
+// at an unclassified cell, or kSkip at a classified one — classify is idempotent, so
+// resuming both as kStep repeats no count).  The caller repacks the open walks of its tile
+// into fewer waves and continues them with another walk_wave call.
+template <int PHK = 0, uint32_t SKIPW = 0, uint32_t MINC = skip::kMinCube, uint32_t RUN = 0, uint32_t BUDGET = 0>
+__device__ __forceinline__ bool walk_wave(const skip::GridView& g, skip::Walk& w, float bound, uint32_t& cells,
+                                          bool* open = nullptr) {
     enum : int { kStep = 0, kSkip = 1, kMiss = 2, kHit = 3 };
     constexpr int kRun = (int)(RUN & 255u);
     // bits 24..31: the cap for runs through an all-empty brick (class 3), which read no
@@ -472,11 +479,17 @@ __device__ __forceinline__ bool walk_wave(const skip::GridView& g, skip::Walk& w
     uint32_t pkey = ~0u;
     (void)pm1, (void)pm2, (void)pkey;
     VPX_PH(uint64_t cs = 0, ck = 0, ns = 0, nk = 0, ls = 0, lk = 0, fb = 0, cf = 0;)
+    uint32_t spent = 0;  // BUDGET: step iterations + skip phases so far (wave-uniform)
+    bool over = false;
     for (;;) {
         VPX_PH(uint64_t t0 = __builtin_amdgcn_s_memtime();)
         for (;;) {
             const uint64_t stepping = __ballot(mode == kStep);
             if (!stepping) break;
+            if (BUDGET && ++spent > BUDGET) {
+                over = true;
+                break;
+            }
             // cost-weighted: a skip phase costs several step phases, so keep stepping while
             // steppers x SKIPW >= waiting skippers (SKIPW = 0: while >= kStepThreshold step)
             if (SKIPW ? (uint32_t)__popcll(stepping) * SKIPW < (uint32_t)__popcll(__ballot(mode == kSkip))
@@ -621,6 +634,7 @@ __device__ __forceinline__ bool walk_wave(const skip::GridView& g, skip::Walk& w
         }
         VPX_MARK("step phase end");
         VPX_PH(uint64_t t1 = __builtin_amdgcn_s_memtime(); cs += t1 - t0;)
+        if (BUDGET && over) break;
         const uint64_t skipping = __ballot(mode == kSkip);
         if (!skipping) {
             if (!__ballot(mode == kStep)) break;
@@ -628,6 +642,7 @@ __device__ __forceinline__ bool walk_wave(const skip::GridView& g, skip::Walk& w
         }
         VPX_PH(++nk; lk += __popcll(skipping);)
         VPX_MARK("skip phase");
+        if (BUDGET) ++spent;
         pkey = ~0u;  // the prefetch does not live across a skip phase (its registers are free there)
         if (mode == kSkip) {
             uint32_t lo[3], hi[3];
@@ -657,6 +672,7 @@ __device__ __forceinline__ bool walk_wave(const skip::GridView& g, skip::Walk& w
         atomicAdd(&g_phase[PHK + 8], cf);
     }
 #endif
+    if (BUDGET && open) *open = over && (mode == kStep || mode == kSkip);
     return mode == kHit;
 }
 

@@ -606,21 +606,35 @@ __device__ __forceinline__ ORay path_oray(const vpx_volume& vol, const PathRay& 
 // walk state lives across the walk — the ray is read back from the path buffers and
 // transformed again for the normal (the same operations, so the same values), which
 // keeps the walker's registers from spilling.
-template <uint32_t SKIPW = VPX_SKIPW_NEAREST, uint32_t MINC = VPX_MINC_NEAREST, uint32_t RUN = VPX_RUN_NEAREST>
-__device__ __forceinline__ void nearest_record_1v(const SceneView& sv, const PathRay& w, uint32_t p, Counters& k) {
+// Its two halves (walk continuations, k_nearest_tile): the walk state of path p's ray
+// (false: Setup3DDDA fails, no cell is read) and the hit record from the finished walk.
+__device__ __forceinline__ bool nearest_begin_1v(const SceneView& sv, const PathRay& w, uint32_t p, Counters& k,
+                                                 skip::Walk& wk) {
     const vpx_volume* vol = uni_ptr(&sv.volumes[0]);
     const DevGrid g = sv.grids[vol->grid_id];
     ++k.nearest;
+    const ORay o = path_oray(*vol, w, p);
+    Dda s;
+    if (!dda_setup(*vol, g.n, o, s)) return false;
+    wk = to_walk(s);
+    return true;
+}
+__device__ __forceinline__ void nearest_end_1v(const SceneView& sv, const PathRay& w, uint32_t p, const skip::Walk& wk,
+                                               bool hit);
+
+template <uint32_t SKIPW = VPX_SKIPW_NEAREST, uint32_t MINC = VPX_MINC_NEAREST, uint32_t RUN = VPX_RUN_NEAREST>
+__device__ __forceinline__ void nearest_record_1v(const SceneView& sv, const PathRay& w, uint32_t p, Counters& k) {
     bool hit = false;
     skip::Walk wk;
-    {
-        const ORay o = path_oray(*vol, w, p);
-        Dda s;
-        if (dda_setup(*vol, g.n, o, s)) {
-            wk = to_walk(s);
-            hit = walk_wave<0, SKIPW, MINC, RUN>(grid_view(g), wk, kBig, k.cells);
-        }
-    }
+    if (nearest_begin_1v(sv, w, p, k, wk))
+        hit = walk_wave<0, SKIPW, MINC, RUN>(grid_view(sv.grids[uni_ptr(&sv.volumes[0])->grid_id]), wk, kBig, k.cells);
+    nearest_end_1v(sv, w, p, wk, hit);
+}
+
+__device__ __forceinline__ void nearest_end_1v(const SceneView& sv, const PathRay& w, uint32_t p, const skip::Walk& wk,
+                                               bool hit) {
+    const vpx_volume* vol = uni_ptr(&sv.volumes[0]);
+    const DevGrid g = sv.grids[vol->grid_id];
     asm volatile("" ::: "memory");  // re-read the ray below instead of keeping it live
     const uint32_t inside = __float_as_uint(w.D[w.at(p)].w) & kInside ? 0x80000000u : 0u;
     if (!hit) {
@@ -733,6 +747,39 @@ __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_NEAREST : VPX_WPE_MULTI_
     primary_tile<ONE, SHADE>(sv, f, w, ctr);
 }
 
+// Walk continuations (bounce and shadow walks of one-volume scenes): a tile's walks first
+// run for at most VPX_CONT_* step iterations + skip phases; the unfinished ones are saved
+// to LDS, repacked densely after a workgroup barrier and continued by the first threads,
+// so the long walks of a tile share waves instead of each keeping a mostly finished wave
+// stepping (0: one unbounded pass).  Measured (one box, ms/step, base C1 0.706 / C2 4.28 /
+// C3 5.71): bounce budgets 12 / 24 -> C2 4.37 / 4.23 (noise); shadow budgets 12 / 24 / 40 ->
+// C3 6.14 / 5.95 / 5.86, C1 0.740 / 0.723 / 0.723 — the tile's longest walks set its time
+// either way, and the repack adds a barrier and LDS round trips.  Left off.
+#ifndef VPX_CONT_BOUNCE
+#define VPX_CONT_BOUNCE 0
+#endif
+#ifndef VPX_CONT_SHADOW
+#define VPX_CONT_SHADOW 0
+#endif
+constexpr uint32_t kContWords = 13;  // per open walk: t, heads, deltas, bound, X, Y, Z, signs, id
+__device__ __forceinline__ void cont_save(uint32_t* c, const skip::Walk& w, float bound, uint32_t id) {
+    c[0] = __float_as_uint(w.t), c[1] = __float_as_uint(w.tx), c[2] = __float_as_uint(w.ty), c[3] = __float_as_uint(w.tz);
+    c[4] = __float_as_uint(w.dx), c[5] = __float_as_uint(w.dy), c[6] = __float_as_uint(w.dz), c[7] = __float_as_uint(bound);
+    c[8] = w.X, c[9] = w.Y, c[10] = w.Z;
+    c[11] = (w.sx < 0 ? 1u : 0u) | (w.sy < 0 ? 2u : 0u) | (w.sz < 0 ? 4u : 0u);
+    c[12] = id;
+}
+__device__ __forceinline__ float cont_load(const uint32_t* c, skip::Walk& w, uint32_t& id) {
+    w.t = __uint_as_float(c[0]), w.tx = __uint_as_float(c[1]), w.ty = __uint_as_float(c[2]), w.tz = __uint_as_float(c[3]);
+    w.dx = __uint_as_float(c[4]), w.dy = __uint_as_float(c[5]), w.dz = __uint_as_float(c[6]);
+    w.X = c[8], w.Y = c[9], w.Z = c[10];
+    const uint32_t sg = c[11];
+    w.sx = sg & 1u ? -1 : 1, w.sy = sg & 2u ? -1 : 1, w.sz = sg & 4u ? -1 : 1;
+    skip::walk_begin(w);
+    id = c[12];
+    return __uint_as_float(c[7]);
+}
+
 #ifndef VPX_BOUNCE_BUCKETS
 #define VPX_BOUNCE_BUCKETS 0  // 1: bounce walks grouped by direction octant (measured C2: 4.88 vs 4.82 ms, no gain)
 #endif
@@ -818,6 +865,36 @@ __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_NEAREST : VPX_WPE_MULTI_
         if (cnt[g]) lst[at++] = base + threadIdx.x * kGroupTiles + g;
     __syncthreads();
 #endif
+    if (ONE && VPX_CONT_BOUNCE) {
+        static_assert(kGroupTiles == 1, "continuations assume one tile per workgroup");
+        __shared__ uint32_t cont[256 * kContWords];
+        __shared__ uint32_t ncont;
+        const PathRay pr{w.O, w.D, w.H, w.HM, 0u};
+        const skip::GridView gv = grid_view(sv.grids[uni_ptr(&sv.volumes[0])->grid_id]);
+        if (threadIdx.x == 0) ncont = 0u;
+        __syncthreads();
+        if (threadIdx.x < total) {
+            const uint32_t q = lst[threadIdx.x];
+            skip::Walk wk;
+            bool hit = false, open = false;
+            if (nearest_begin_1v(sv, pr, q, k, wk))
+                hit = walk_wave<0, VPX_SKIPW_BOUNCE, VPX_MINC_BOUNCE, VPX_RUN_BOUNCE, VPX_CONT_BOUNCE>(gv, wk, kBig, k.cells, &open);
+            if (open)
+                cont_save(cont + atomicAdd(&ncont, 1u) * kContWords, wk, kBig, q);
+            else
+                nearest_end_1v(sv, pr, q, wk, hit);
+        }
+        __syncthreads();
+        if (threadIdx.x < ncont) {
+            skip::Walk wk;
+            uint32_t q;
+            cont_load(cont + threadIdx.x * kContWords, wk, q);
+            const bool hit = walk_wave<0, VPX_SKIPW_BOUNCE, VPX_MINC_BOUNCE, VPX_RUN_BOUNCE>(gv, wk, kBig, k.cells);
+            nearest_end_1v(sv, pr, q, wk, hit);
+        }
+        flush_counters(k, 0u, ctr, VPX_STAGE_BOUNCE);
+        return;
+    }
     for (uint32_t i = threadIdx.x; i < total; i += 256u) {
         const uint32_t q = lst[i];
         if (ONE) {
@@ -896,6 +973,55 @@ __device__ __forceinline__ void shadow_tile(const SceneView& sv, const WaveBufs&
     }
     __syncthreads();
 #endif
+    if (ONE && VPX_CONT_SHADOW) {  // continuations: first pass over up to 256 slots per round
+        __shared__ uint32_t cont[256 * kContWords];
+        __shared__ uint32_t ncont;
+        const vpx_volume* vol = uni_ptr(&sv.volumes[0]);
+        const skip::GridView gv = grid_view(sv.grids[vol->grid_id]);
+        for (uint32_t base = 0; base < total; base += 256u) {
+            if (base) __syncthreads();  // the previous round's readers of cont / ncont are done
+            if (threadIdx.x == 0) ncont = 0u;
+            __syncthreads();
+            const uint32_t i = base + threadIdx.x;
+            if (i < total) {
+                const uint32_t e = lst_dyn[i];
+                const uint64_t slot = (uint64_t)(e >> 27) * w.P + (e & 0x07ffffffu);
+                ++k.shadow;
+                bool hit = false, open = false;
+                skip::Walk wk;
+                float bound = 0.f;
+                {
+                    const float4 so = w.SO[slot], sd = w.SD[slot];
+                    ORay o;
+                    o.O = xform_pos(mk(so.x, so.y, so.z), vol->inv_matrix);
+                    o.D = xform_vec(mk(sd.x, sd.y, sd.z), vol->inv_matrix);
+                    o.rD = mk(__fdiv_rn(1.0f, o.D.x), __fdiv_rn(1.0f, o.D.y), __fdiv_rn(1.0f, o.D.z));
+                    Dda s;
+                    bound = so.w;
+                    if (dda_setup(*vol, gv.n, o, s)) {
+                        wk = to_walk(s);
+                        hit = walk_wave<16, VPX_SKIPW_SHADOW, VPX_MINC_SHADOW, VPX_RUN_SHADOW, VPX_CONT_SHADOW>(gv, wk, bound, k.cells, &open);
+                    }
+                }
+                asm volatile("" ::: "memory");
+                if (open)
+                    cont_save(cont + atomicAdd(&ncont, 1u) * kContWords, wk, bound, e);
+                else if (hit)
+                    w.SD[slot].w = __uint_as_float(__float_as_uint(w.SD[slot].w) | 4u /* occluded */);
+            }
+            __syncthreads();
+            if (threadIdx.x < ncont) {
+                skip::Walk wk;
+                uint32_t e2;
+                const float bound = cont_load(cont + threadIdx.x * kContWords, wk, e2);
+                const uint64_t slot = (uint64_t)(e2 >> 27) * w.P + (e2 & 0x07ffffffu);
+                if (walk_wave<16, VPX_SKIPW_SHADOW, VPX_MINC_SHADOW, VPX_RUN_SHADOW>(gv, wk, bound, k.cells))
+                    w.SD[slot].w = __uint_as_float(__float_as_uint(w.SD[slot].w) | 4u /* occluded */);
+            }
+        }
+        flush_counters(k, 0u, ctr, VPX_STAGE_SHADOW);
+        return;
+    }
     for (uint32_t i = threadIdx.x; i < total; i += 256u) {
         const uint32_t e = lst_dyn[i];
         const uint64_t slot = (uint64_t)(e >> 27) * w.P + (e & 0x07ffffffu);
