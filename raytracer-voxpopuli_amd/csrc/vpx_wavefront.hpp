@@ -528,8 +528,14 @@ __global__ __launch_bounds__(256) void k_resolve(SceneView sv, WaveBufs w) {
 #ifndef VPX_WPE_NEAREST
 #define VPX_WPE_NEAREST 6
 #endif
+#ifndef VPX_WPE_BOUNCE
+#define VPX_WPE_BOUNCE VPX_WPE_NEAREST
+#endif
+// Shadow kernels (k_shadow_tile, k_shadow_finish) at 7 with the octant planes (13 spilled
+// VGPRs): C3 5.68 -> 5.60 ms, C2 unchanged; 8 measured 6.03 / 4.51.  Bounce walks: 5 / 7
+// measured 4.35 / 4.29 vs 4.28 ms on C2, kept at 6.
 #ifndef VPX_WPE_SHADOW
-#define VPX_WPE_SHADOW 6
+#define VPX_WPE_SHADOW 7
 #endif
 // The multi-volume / shape instances (C4) carry the volume loop's state across the walks:
 // at 6 waves/SIMD they spilled 45-53 VGPRs.  Measured C4 (ms, FindNearest / IsOccluded
@@ -816,7 +822,7 @@ __device__ __forceinline__ uint32_t group_scan(const uint32_t (&cnt)[G], uint32_
 
 // Renderer::FindNearest for the active paths of G tiles (bounce levels).
 template <bool ONE>
-__global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_NEAREST : VPX_WPE_MULTI_NEAREST) void k_nearest_tile(SceneView sv, WaveBufs w, unsigned long long* __restrict__ ctr) {
+__global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_BOUNCE : VPX_WPE_MULTI_NEAREST) void k_nearest_tile(SceneView sv, WaveBufs w, unsigned long long* __restrict__ ctr) {
     if (!ONE) stage_tlas(sv);
     __shared__ uint32_t sh[4];
     __shared__ uint32_t lst[256 * kGroupTiles];
