@@ -175,10 +175,27 @@ __device__ __forceinline__ void flush_counters(const Counters& k, uint32_t prima
 // bands per XCD were measured and rejected: the image's cost is spatially uneven, and a
 // band per XCD left most XCDs idle (C1 primary 0.46 -> 0.80 ms).  A permutation of the
 // tiles — any kernel may use it or not; the fused tail uses it for its walks and finish.
+// Launches of more than VPX_XCD_BIG_TILES tiles (C3 / C4 at 3840x2160: 32400) use runs of
+// VPX_XCD_RUN_BIG: 8-tile strips per XCD measured C3 5.61 -> 5.52 ms (runs of 4: 5.62, of
+// 30 — a column band per XCD — 10.1); C1-sized launches keep t = b (runs of 8: 0.705 ->
+// 0.716 ms).
 #ifndef VPX_XCD_RUN
 #define VPX_XCD_RUN 0
 #endif
+#ifndef VPX_XCD_RUN_BIG
+#define VPX_XCD_RUN_BIG 8
+#endif
+#ifndef VPX_XCD_BIG_TILES
+#define VPX_XCD_BIG_TILES 16384
+#endif
 __device__ __forceinline__ uint32_t tile_block() {
+    if (VPX_XCD_RUN_BIG && gridDim.x > VPX_XCD_BIG_TILES) {
+        constexpr uint32_t R = VPX_XCD_RUN_BIG;
+        const uint32_t b = blockIdx.x, full = (gridDim.x / (8u * R)) * 8u * R;
+        if (b >= full) return b;
+        const uint32_t x = b & 7u, k = b >> 3;
+        return ((k / R) * 8u + x) * R + k % R;
+    }
     if (VPX_XCD_RUN == 0) return blockIdx.x;
     constexpr uint32_t R = VPX_XCD_RUN > 0 ? VPX_XCD_RUN : 1;
     const uint32_t b = blockIdx.x, full = (gridDim.x / (8u * R)) * 8u * R;
