@@ -78,7 +78,7 @@ def pmc_traffic(kernel, config, W, H, sha):
     correction); None when no summary for this exact build / workload exists."""
     import glob
     best = None
-    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_traffic.json"))):
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_traffic*.json"))):
         try:
             d = json.load(open(f))
         except (OSError, ValueError):
