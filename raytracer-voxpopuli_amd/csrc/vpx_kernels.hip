@@ -721,12 +721,23 @@ int launch_render(vpx_ctx* c, const SceneView& sv, const FrameArgs& f, uint32_t 
             prof_mark(c, -1);
             break;
         }
-        prof_mark(c, VPX_STAGE_SHADOW);
-        hipLaunchKernelGGL(one ? k_shadow_tile<true> : k_shadow_tile<false>, ggrid, block, slds, c->stream, sv, w, c->d_ctr);
-        prof_mark(c, -1);
-        prof_mark(c, VPX_STAGE_RESOLVE);
-        hipLaunchKernelGGL(k_resolve, grid, block, 0, c->stream, sv, w);
-        prof_mark(c, -1);
+#if VPX_FUSE_RESOLVE
+        if (fuse_tail) {  // shadow walks + resolve as one launch (k_shadow_resolve)
+            prof_mark(c, VPX_STAGE_SHADOW);
+            hipLaunchKernelGGL(one ? k_shadow_resolve<true> : k_shadow_resolve<false>, grid, block, slds, c->stream, sv, w,
+                               c->d_ctr);
+            prof_mark(c, -1);
+        } else
+#endif
+        {
+            prof_mark(c, VPX_STAGE_SHADOW);
+            hipLaunchKernelGGL(one ? k_shadow_tile<true> : k_shadow_tile<false>, ggrid, block, slds, c->stream, sv, w,
+                               c->d_ctr);
+            prof_mark(c, -1);
+            prof_mark(c, VPX_STAGE_RESOLVE);
+            hipLaunchKernelGGL(k_resolve, grid, block, 0, c->stream, sv, w);
+            prof_mark(c, -1);
+        }
         if (level < f.max_bounces) {
             prof_mark(c, VPX_STAGE_BOUNCE);
             hipLaunchKernelGGL(one ? k_nearest_tile<true> : k_nearest_tile<false>, ggrid, block, 0, c->stream, sv, w, c->d_ctr);

@@ -1192,6 +1192,23 @@ __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_SHADOW : VPX_WPE_MULTI_S
     finish_path<MODE>(f, w, p, accum, rgb8, packed);
 }
 
+// The other levels' tail the same way (VPX_FUSE_RESOLVE): the tile's IsOccluded walks, the
+// barrier, then each thread's light resolve — k_shadow_tile -> k_resolve as one launch, so
+// the resolve's loads and stores of finished tiles overlap other tiles' walks.  Measured on
+// C2 (three runs each): 4.32-4.34 vs 4.30-4.31 ms with the two launches — the barrier holds
+// the tile's finished waves longer than the separate 14-µs resolve costs.  Left off.
+#ifndef VPX_FUSE_RESOLVE
+#define VPX_FUSE_RESOLVE 0
+#endif
+template <bool ONE>
+__global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_SHADOW : VPX_WPE_MULTI_SHADOW) void k_shadow_resolve(
+    SceneView sv, WaveBufs w, unsigned long long* __restrict__ ctr) {
+    if (!ONE) stage_tlas(sv);
+    shadow_tile<ONE>(sv, w, ctr);
+    __syncthreads();
+    resolve_path(sv, w, tile_block() * 256u + threadIdx.x);
+}
+
 // A Trace-depth-0 frame in one launch (VPX_FUSE_FRAME): the fused head (primary walk +
 // level-0 shade) and the fused tail (the tile's shadow walks, resolve, finish) of the same
 // tile, one barrier apart — the shade's slots are read back by the workgroup that wrote them
