@@ -215,7 +215,10 @@ int vpx_set_stream(vpx_ctx* ctx, void* hip_stream);
 int vpx_synchronize(vpx_ctx* ctx);
 
 /* ---- world ----------------------------------------------------------------------------- */
-/* Upload a dense N^3 grid of MatType bytes, index x + y*N + z*N*N (scene.h:241-248). */
+/* Upload a dense N^3 grid of MatType bytes, index x + y*N + z*N*N (scene.h:241-248).
+   Device memory per grid: N^3 bytes + the walkers' levels built from them, about N^3 / 4
+   bytes (l1 cell masks N^3/8, distance-field octant planes N^3/8, l2 N^3/512): 1.25 GiB
+   at N = 1024, 10 GiB at 2048, 80 GiB at 4096 (the maximum). */
 int vpx_upload_grid(vpx_ctx* ctx, uint32_t grid_id, const uint8_t* cells, uint32_t n);
 /* Build-defined world generator on device: a grid-oriented model
    (mx*my*mz bytes, index x + y*mx + z*mx*my) tiled with period (px,py,pz) above a
