@@ -619,7 +619,7 @@ int validate_frame(vpx_ctx* c, const vpx_frame_params* p) {
 int ensure_wave(vpx_ctx* c, uint32_t P, uint32_t L, uint32_t S) {
     const size_t f4 = sizeof(float4);
     const size_t bytes = (size_t)P * (f4 * (5 + 2 * (size_t)L + 3 * (size_t)S + 1) + 3 * sizeof(uint32_t)) +
-                         sizeof(uint32_t) * (size_t)P + 16 * 256;
+                         sizeof(uint32_t) * (size_t)P + (size_t)P + 17 * 256;
     if (bytes > c->wave_bytes) {
         if (c->d_wave) {
             VPX_HIP(c, hipStreamSynchronize(c->stream));
@@ -639,6 +639,7 @@ int ensure_wave(vpx_ctx* c, uint32_t P, uint32_t L, uint32_t S) {
     WaveBufs& w = c->wave;
     w.P = P;
     w.S = S;
+    w.cost = (uint8_t*)take(P);  // first: its address survives L / S changes (a scheduling hint only)
     w.O = (float4*)take(f4 * P);
     w.D = (float4*)take(f4 * P);
     w.H = (float4*)take(f4 * P);

@@ -457,9 +457,10 @@ __device__ unsigned long long g_phase[32];
 // at an unclassified cell, or kSkip at a classified one — classify is idempotent, so
 // resuming both as kStep repeats no count).  The caller repacks the open walks of its tile
 // into fewer waves and continues them with another walk_wave call.
+// iters (optional): += the step iterations and skip phases this lane took part in.
 template <int PHK = 0, uint32_t SKIPW = 0, uint32_t MINC = skip::kMinCube, uint32_t RUN = 0, uint32_t BUDGET = 0>
 __device__ __forceinline__ bool walk_wave(const skip::GridView& g, skip::Walk& w, float bound, uint32_t& cells,
-                                          bool* open = nullptr) {
+                                          bool* open = nullptr, uint32_t* iters = nullptr) {
     enum : int { kStep = 0, kSkip = 1, kMiss = 2, kHit = 3 };
     constexpr int kRun = (int)(RUN & 255u);
     // bits 24..31: the cap for runs through an all-empty brick (class 3), which read no
@@ -490,6 +491,7 @@ __device__ __forceinline__ bool walk_wave(const skip::GridView& g, skip::Walk& w
                 over = true;
                 break;
             }
+            if (iters && mode == kStep) ++*iters;
             // cost-weighted: a skip phase costs several step phases, so keep stepping while
             // steppers x SKIPW >= waiting skippers (SKIPW = 0: while >= kStepThreshold step)
             if (SKIPW ? (uint32_t)__popcll(stepping) * SKIPW < (uint32_t)__popcll(__ballot(mode == kSkip))
@@ -643,6 +645,7 @@ __device__ __forceinline__ bool walk_wave(const skip::GridView& g, skip::Walk& w
         VPX_PH(++nk; lk += __popcll(skipping);)
         VPX_MARK("skip phase");
         if (BUDGET) ++spent;
+        if (iters && mode == kSkip) ++*iters;
         pkey = ~0u;  // the prefetch does not live across a skip phase (its registers are free there)
         if (mode == kSkip) {
             uint32_t lo[3], hi[3];

@@ -94,6 +94,8 @@ struct WaveBufs {
     float4* SM;    // [P] pending light: xyz = kd (area), w = bits(kind | discard<<3 | count<<4 | level<<8 | lc<<16)
     uint32_t* smask;  // [P] shadow slots emitted this level (bit s = slot s, s < 15) | light key << 16
     float4* RD;    // [W*H] reprojection: level-0 intersection point, w = material bits (image order)
+    uint8_t* cost; // [P] the path's last primary walk length (iterations, capped): the order of the
+                   // tile's primary walkers in the next frame (VPX_COST_SORT), never a result
     uint32_t P;    // paths (pixels) this call
     uint32_t S;    // shadow slots per path
 };
@@ -675,6 +677,18 @@ __device__ __forceinline__ void nearest_end_1v(const SceneView& sv, const PathRa
 #ifndef VPX_HEAD_LDS
 #define VPX_HEAD_LDS 1
 #endif
+// Primary walkers ordered by the previous frame's walk length of their pixel (w.cost):
+// 16 buckets of 2^VPX_COST_SHIFT iterations.  The CPU wave-cost model (tools/wavecost.py)
+// gives 0.81-0.83 of the pixel-order wave cost; measured (one box, ms): C1 0.697-0.704 vs
+// 0.712-0.715, C3 5.43 vs 5.54 — the lanes a wave wastes are not what sets a tile's time
+// (its longest walk is), and a per-pixel history is a frame-to-frame dependency the path
+// otherwise does not have.  Left off.
+#ifndef VPX_COST_SORT
+#define VPX_COST_SORT 0
+#endif
+#ifndef VPX_COST_SHIFT
+#define VPX_COST_SHIFT 2
+#endif
 // Primary rays + Renderer::FindNearest.  Every path's ray / RNG state is written; rays
 // that cannot hit a voxel or shape (one volume, no shapes, Setup3DDDA fails: the
 // reference returns before reading a cell) get their miss record directly.
@@ -739,12 +753,47 @@ __device__ __forceinline__ void primary_tile(SceneView& sv, const FrameArgs& f, 
         }
     }
     uint32_t total;
+#if VPX_COST_SORT
+    // the tile's walkers counting-sorted by their pixel's walk length in the previous frame
+    // (longest first), so a wave's lanes finish together: an LDS histogram of 16 buckets,
+    // one wave's prefix sum, the scatter (any order gives the same per-ray results)
+    __shared__ uint32_t hist[16];
+    if (threadIdx.x < 16) hist[threadIdx.x] = 0u;
+    __syncthreads();
+    uint32_t key = 0, pos = 0;
+    if (walk) {
+        const uint32_t c = w.cost[p] >> VPX_COST_SHIFT;
+        key = 15u - (c < 15u ? c : 15u);
+        pos = atomicAdd(&hist[key], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        uint32_t t;
+        const uint32_t v = threadIdx.x < 16 ? hist[threadIdx.x] : 0u;
+        const uint32_t ex = wave_prefix(v, t);
+        if (threadIdx.x < 16) hist[threadIdx.x] = ex;
+        if (threadIdx.x == 0) sh[0] = t;
+    }
+    __syncthreads();
+    total = sh[0];
+    if (walk) lst[hist[key] + pos] = p;
+#else
     const uint32_t at = block_scan(walk ? 1u : 0u, total, sh);  // (its barrier orders the LDS writes)
     if (walk) lst[at] = p;
+#endif
     __syncthreads();
     if (threadIdx.x < total) {
         const uint32_t q = lst[threadIdx.x];
-        if (ONE) {
+        if (ONE && VPX_COST_SORT) {
+            skip::Walk wk;
+            bool hit = false;
+            uint32_t it = 0;
+            if (nearest_begin_1v(sv, pr, q, k, wk))
+                hit = walk_wave<0, VPX_SKIPW_NEAREST, VPX_MINC_NEAREST, VPX_RUN_NEAREST>(
+                    grid_view(sv.grids[uni_ptr(&sv.volumes[0])->grid_id]), wk, kBig, k.cells, nullptr, &it);
+            w.cost[q] = (uint8_t)(it < 255u ? it : 255u);
+            nearest_end_1v(sv, pr, q, wk, hit);
+        } else if (ONE) {
             nearest_record_1v(sv, pr, q, k);
         } else {
             const float4 o = pr.O[pr.at(q)], d = pr.D[pr.at(q)];

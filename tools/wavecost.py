@@ -79,3 +79,14 @@ for B in (20, 40, 60, 80, 120):
         rem = c[c > B] - B
         tot += first + waves(rem)
     print(f"  compact after {B:4d}: {tot:.0f} ({tot / base:.2f} of no compaction)")
+# Ordering the tile's walking rays by their cost before dealing them to waves (e.g. sorted
+# by the previous frame's per-pixel walk cost): sum over waves of the max.
+srt = sum(waves(np.sort(cost[t][okt[t]])) for t in range(T))
+print(f"  sorted by cost within the tile: {srt:.0f} ({srt / base:.2f} of pixel order)")
+for q in (4, 8, 16):  # coarse buckets of the cost (what a counting sort on a quantised cost gives)
+    tot = 0
+    for t in range(T):
+        c = cost[t][okt[t]]
+        key = np.minimum((c * q / max(c.max() if len(c) else 1, 1)).astype(int), q - 1)
+        tot += waves(c[np.argsort(key, kind="stable")])
+    print(f"  {q} cost buckets: {tot:.0f} ({tot / base:.2f})")
