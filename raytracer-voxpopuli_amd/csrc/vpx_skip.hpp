@@ -472,6 +472,9 @@ VPX_HD int skip_box(Walk& w, const uint32_t lo[3], const uint32_t hi[3], float b
 }
 
 // ------------------------------------------------------- lean tier
+#ifndef VPX_SEG2_BRANCH
+#define VPX_SEG2_BRANCH 1  // the second closed-form segment only when a lane of the wave needs it
+#endif
 // skip_box in straight-line integer code.  Each axis's sequence is put in closed form as
 // up to two segments (its own binade, then the next one after one plain IEEE step), and
 // the box is first clipped, per axis, to the events those two segments reach.  So every
@@ -571,7 +574,44 @@ struct Axis {
 };
 
 // l = the events wanted inside the box, clipped to what the two segments reach (0 when
-// not even the first applies: then only A(0) = h is read).
+// not even the first applies: then only A(0) = h is read).  In three parts: the first
+// segment (axis_seg1, sets fit1 = the events it reaches), the second (axis_seg2, returns
+// the events both reach; skipped when no lane of the wave wants more than fit1 on any
+// axis — its parameters are then never read: every index used is <= m1), the clip.
+VPX_HD bool axis_seg1(float h, float d, Axis& a, uint32_t& fit1) {
+    const bool ok1 = seg_params_nb(h, d, a.b1, a.c1, a.e1);
+    // A(i), 1 <= i <= fit1, stay below 2^24 u (a tie base may be 2^24 itself: fit1 = 0)
+    const uint32_t room = a.b1 <= 0xffffffu ? 0xffffffu - a.b1 : 0u;
+    fit1 = floor_div_cap(room, a.c1 ? a.c1 : 1u);  // (c1 == 0: not ok1)
+    a.b2 = 0u, a.c2 = 1u, a.e2 = 0u;
+    return ok1;
+}
+VPX_HD uint32_t axis_seg2(float h, float d, Axis& a, uint32_t fit1) {
+    const uint32_t amc = (a.e1 << 23) | (mad24(fit1, a.c1, a.b1) & 0x7fffffu);
+    const uint32_t am = fit1 ? amc : fbits(h);
+    const float A = bitsf(am) + d;  // the plain IEEE step into the next binade
+    uint32_t b2;
+    const bool ok2 = seg_params_nb(A, d, b2, a.c2, a.e2);
+    const bool exact2 = b2 == ((fbits(A) & 0x7fffffu) | 0x800000u);  // closed form from j = 0
+    a.b2 = b2;
+    const uint32_t room2 = b2 <= 0xffffffu ? 0xffffffu - b2 : 0u;
+    const uint32_t fit2 = floor_div_cap(room2, a.c2 ? a.c2 : 1u);
+    return (ok2 & exact2) ? fit1 + 1u + fit2 : fit1;
+}
+VPX_HD void axis_clip(Axis& a, uint32_t l, bool ok1, uint32_t reach, uint32_t fit1) {
+    const uint32_t lim = ok1 ? reach : 0u;
+    a.l = l < lim ? l : lim;
+    a.m1 = a.l < fit1 ? a.l : fit1;
+}
+// True when any lane of the wave (calling it together) passes true; the host: this call's.
+VPX_HD bool any_lane(bool b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __ballot(b) != 0ull;
+#else
+    return b;
+#endif
+}
+
 VPX_HD void axis_setup(float h, float d, uint32_t l, Axis& a) {
     const bool ok1 = seg_params_nb(h, d, a.b1, a.c1, a.e1);
     // A(i), 1 <= i <= fit1, stay below 2^24 u (a tie base may be 2^24 itself: fit1 = 0)
@@ -611,12 +651,30 @@ VPX_HD uint32_t axis_count(const Axis& a, float h, float T, bool strict, uint32_
 // Cross the empty box [lo, hi] around the current cell, clipped per axis as above (lo / hi
 // receive the clipped box).  0: landed just before the event that leaves the clipped box
 // (cells += skipped visits); 1: the walk ends inside it (cells += visits); 2: refused.
+template <bool SEG2_BRANCH = VPX_SEG2_BRANCH != 0>
 VPX_HD int skip_box_lean(Walk& w, uint32_t lo[3], uint32_t hi[3], float bound, uint32_t& cells) {
     if (!((w.tx > 0.0f) & (w.ty > 0.0f) & (w.tz > 0.0f))) return 2;
     Axis ax, ay, az;
+    if (SEG2_BRANCH) {
+    const uint32_t wx = w.sx > 0 ? hi[0] - w.X : w.X - lo[0], wy = w.sy > 0 ? hi[1] - w.Y : w.Y - lo[1],
+                   wz = w.sz > 0 ? hi[2] - w.Z : w.Z - lo[2];
+    uint32_t fx, fy, fz;
+    const bool okx = axis_seg1(w.tx, w.dx, ax, fx), oky = axis_seg1(w.ty, w.dy, ay, fy),
+               okz = axis_seg1(w.tz, w.dz, az, fz);
+    uint32_t rx = fx, ry = fy, rz = fz;
+    if (any_lane((okx & (wx > fx)) | (oky & (wy > fy)) | (okz & (wz > fz)))) {  // a box crosses a binade
+        rx = axis_seg2(w.tx, w.dx, ax, fx);
+        ry = axis_seg2(w.ty, w.dy, ay, fy);
+        rz = axis_seg2(w.tz, w.dz, az, fz);
+    }
+    axis_clip(ax, wx, okx, rx, fx);
+    axis_clip(ay, wy, oky, ry, fy);
+    axis_clip(az, wz, okz, rz, fz);
+    } else {
     axis_setup(w.tx, w.dx, w.sx > 0 ? hi[0] - w.X : w.X - lo[0], ax);
     axis_setup(w.ty, w.dy, w.sy > 0 ? hi[1] - w.Y : w.Y - lo[1], ay);
     axis_setup(w.tz, w.dz, w.sz > 0 ? hi[2] - w.Z : w.Z - lo[2], az);
+    }
     const uint32_t lx = ax.l, ly = ay.l, lz = az.l;
     if (w.sx > 0) hi[0] = w.X + lx; else lo[0] = w.X - lx;
     if (w.sy > 0) hi[1] = w.Y + ly; else lo[1] = w.Y - ly;

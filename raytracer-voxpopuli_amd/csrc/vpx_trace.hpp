@@ -415,14 +415,27 @@ constexpr int kStepUnroll = VPX_STEP_UNROLL;  // cell steps per step-phase itera
 #ifndef VPX_DFP_SHADOW
 #define VPX_DFP_SHADOW 1
 #endif
+// Bit 17: the skip's second closed-form segment only when a lane of the wave needs it
+// (skip_box_lean<true>; VPX_S2_*).  Measured (ms, one box): C1 0.713 -> 0.693, C3 5.57 ->
+// 5.34, rank 0's C1 share at 8 ranks 0.234 -> 0.222; bounce walks (rays leaving surfaces,
+// whose boxes cross binades in most waves) C2 4.27 -> 4.34 with it, so off there.
+#ifndef VPX_S2_NEAREST
+#define VPX_S2_NEAREST 1
+#endif
+#ifndef VPX_S2_BOUNCE
+#define VPX_S2_BOUNCE 0
+#endif
+#ifndef VPX_S2_SHADOW
+#define VPX_S2_SHADOW 1
+#endif
 #ifndef VPX_RUN_NEAREST
-#define VPX_RUN_NEAREST (3 | 2 << 8 | VPX_DFP_NEAREST << 16)
+#define VPX_RUN_NEAREST (3 | 2 << 8 | VPX_DFP_NEAREST << 16 | VPX_S2_NEAREST << 17)
 #endif
 #ifndef VPX_RUN_BOUNCE
-#define VPX_RUN_BOUNCE (4 | 1 << 8 | VPX_DFP_BOUNCE << 16)
+#define VPX_RUN_BOUNCE (4 | 1 << 8 | VPX_DFP_BOUNCE << 16 | VPX_S2_BOUNCE << 17)
 #endif
 #ifndef VPX_RUN_SHADOW
-#define VPX_RUN_SHADOW (3 | 1 << 8 | VPX_DFP_SHADOW << 16)
+#define VPX_RUN_SHADOW (3 | 1 << 8 | VPX_DFP_SHADOW << 16 | VPX_S2_SHADOW << 17)
 #endif
 #ifndef VPX_BRICK_PREFETCH
 #define VPX_BRICK_PREFETCH 0  // 1: a brick run first loads the words (octant plane: the byte) of the brick it will exit into
@@ -471,6 +484,7 @@ __device__ __forceinline__ bool walk_wave(const skip::GridView& g, skip::Walk& w
     constexpr int kRunMax = kRunE > kRun ? kRunE : kRun;
     constexpr int kPasses = (RUN >> 8) & 255u ? (int)((RUN >> 8) & 255u) : kStepUnroll;
     constexpr bool kDfp = (RUN >> 16) & 1u;
+    constexpr bool kSeg2Branch = (RUN >> 17) & 1u;
     const uint8_t* pl = kDfp ? g.dfp + (uint64_t)(w.osh >> 3) * g.plane : nullptr;  // the ray's octant plane
     (void)pl;
     int mode = kStep;
@@ -650,7 +664,7 @@ __device__ __forceinline__ bool walk_wave(const skip::GridView& g, skip::Walk& w
         if (mode == kSkip) {
             uint32_t lo[3], hi[3];
             skip::df_box(w, g.n, lo, hi);
-            const int sr = skip::skip_box_lean(w, lo, hi, bound, cells);  // 2 (refused): a plain step
+            const int sr = skip::skip_box_lean<kSeg2Branch>(w, lo, hi, bound, cells);  // 2 (refused): a plain step
             VPX_MARK("skip end");
             VPX_PH(fb += __popcll(__ballot(sr == 2));)
             if (sr == 1) {

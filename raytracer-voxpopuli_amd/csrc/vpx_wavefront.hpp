@@ -322,6 +322,14 @@ __device__ __forceinline__ uint32_t wave_prefix(uint32_t v, uint32_t& total) {
     return x - v;
 }
 
+// Order a wave's LDS / global writes before its lanes read each other's (the wave-local
+// counterpart of __syncthreads: the same workgroup-scope release / acquire, no s_barrier).
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
 // L0: the call shades level 0 (the fused head in k_primary).  Level 0 rays are primary
 // rays, which never start inside glass or smoke, so the interior exit marches (a whole DDA
 // walker each) drop out of that instance; the forms word is known (no levels yet).
@@ -692,7 +700,9 @@ __device__ __forceinline__ void nearest_end_1v(const SceneView& sv, const PathRa
 // Primary rays + Renderer::FindNearest.  Every path's ray / RNG state is written; rays
 // that cannot hit a voxel or shape (one volume, no shapes, Setup3DDDA fails: the
 // reference returns before reading a cell) get their miss record directly.
-template <bool ONE, bool SHADE>
+// WAVE: every wave of the tile runs its own 64 pixels (a 16x4 strip) through the head
+// with wave-local compaction and no workgroup barrier (k_frame0<.., WAVE>).
+template <bool ONE, bool SHADE, bool WAVE = false>
 __device__ __forceinline__ void primary_tile(SceneView& sv, const FrameArgs& f, const WaveBufs& w,
                                              unsigned long long* __restrict__ ctr) {
     __shared__ uint32_t sh[4];
@@ -753,6 +763,13 @@ __device__ __forceinline__ void primary_tile(SceneView& sv, const FrameArgs& f, 
         }
     }
     uint32_t total;
+    const uint32_t lbase = WAVE ? threadIdx.x & ~63u : 0u;  // this wave's part of lst
+    const uint32_t li = WAVE ? threadIdx.x & 63u : threadIdx.x;
+    if (WAVE) {
+        const uint32_t at = wave_prefix(walk ? 1u : 0u, total);
+        if (walk) lst[lbase + at] = p;
+        wave_sync();
+    } else {
 #if VPX_COST_SORT
     // the tile's walkers counting-sorted by their pixel's walk length in the previous frame
     // (longest first), so a wave's lanes finish together: an LDS histogram of 16 buckets,
@@ -782,9 +799,10 @@ __device__ __forceinline__ void primary_tile(SceneView& sv, const FrameArgs& f, 
     if (walk) lst[at] = p;
 #endif
     __syncthreads();
-    if (threadIdx.x < total) {
-        const uint32_t q = lst[threadIdx.x];
-        if (ONE && VPX_COST_SORT) {
+    }
+    if (li < total) {
+        const uint32_t q = lst[lbase + li];
+        if (ONE && VPX_COST_SORT && !WAVE) {
             skip::Walk wk;
             bool hit = false;
             uint32_t it = 0;
@@ -806,7 +824,10 @@ __device__ __forceinline__ void primary_tile(SceneView& sv, const FrameArgs& f, 
     }
     flush_counters(k, prim, ctr, VPX_STAGE_PRIMARY);
     if (SHADE) {  // level 0's material switch for this thread's own path (k_primary_shade)
-        __syncthreads();  // the tile's hit records, written by the compacted walkers
+        if (WAVE)
+            wave_sync();  // the wave's hit records, written by its compacted walkers
+        else
+            __syncthreads();  // the tile's hit records, written by the compacted walkers
         Counters ks{0u, 0u, 0u};
         shade_path<true>(sv, f, w, pr, p, 0, ks);
         flush_counters(ks, 0u, ctr, VPX_STAGE_SHADE);
@@ -1277,15 +1298,78 @@ __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_SHADOW : VPX_WPE_MULTI_S
 #ifndef VPX_WPE_FRAME
 #define VPX_WPE_FRAME 5  // 6: 272 spilled VGPRs; 5: 9; 4: none but slower
 #endif
+// shadow_tile for one wave's 64 paths (single volume): the slots counting-sorted by light
+// key in a wave-local histogram, walked by the wave's lanes, no workgroup barrier.
+__device__ __forceinline__ void shadow_wave(const SceneView& sv, const WaveBufs& w, unsigned long long* __restrict__ ctr) {
+    extern __shared__ uint32_t lst_dyn[];  // [S * 256]: this wave's S * 64
+    __shared__ uint32_t hist_w[4 * kLightKeys];
+    const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
+    uint32_t* lst = lst_dyn + wid * 64u * w.S;
+    uint32_t* hist = hist_w + wid * kLightKeys;
+    const uint32_t p = tile_block() * 256u + threadIdx.x;
+    Counters k{0u, 0u, 0u};
+    if (lane < kLightKeys) hist[lane] = 0u;
+    wave_sync();
+    const uint32_t sm = p < w.P ? w.smask[p] : 0u;
+    const uint32_t m = sm & kSlotBits, key = sm >> 16;
+    const uint32_t pos = m ? atomicAdd(&hist[key], (uint32_t)__popc(m)) : 0u;
+    wave_sync();
+    uint32_t total;
+    const uint32_t ex = wave_prefix(lane < kLightKeys ? hist[lane] : 0u, total);
+    wave_sync();  // every lane has read its bucket count before the offsets replace them
+    if (lane < kLightKeys) hist[lane] = ex;
+    wave_sync();
+    uint32_t at = m ? hist[key] + pos : 0u;
+    for (uint32_t b = m; b; b &= b - 1u) lst[at++] = ((uint32_t)__ffs(b) - 1u) << 27 | p;
+    wave_sync();
+    const vpx_volume* vol = uni_ptr(&sv.volumes[0]);
+    const DevGrid g = sv.grids[vol->grid_id];
+    for (uint32_t i = lane; i < total; i += 64u) {
+        const uint32_t e = lst[i];
+        const uint64_t slot = (uint64_t)(e >> 27) * w.P + (e & 0x07ffffffu);
+        ++k.shadow;
+        bool hit = false;
+        {
+            const float4 so = w.SO[slot], sd = w.SD[slot];
+            ORay o;
+            o.O = xform_pos(mk(so.x, so.y, so.z), vol->inv_matrix);
+            o.D = xform_vec(mk(sd.x, sd.y, sd.z), vol->inv_matrix);
+            o.rD = mk(__fdiv_rn(1.0f, o.D.x), __fdiv_rn(1.0f, o.D.y), __fdiv_rn(1.0f, o.D.z));
+            Dda s;
+            if (dda_setup(*vol, g.n, o, s)) {
+                skip::Walk wk = to_walk(s);
+                hit = walk_wave<16, VPX_SKIPW_SHADOW, VPX_MINC_SHADOW, VPX_RUN_SHADOW>(grid_view(g), wk, so.w, k.cells);
+            }
+        }
+        asm volatile("" ::: "memory");
+        if (hit) w.SD[slot].w = __uint_as_float(__float_as_uint(w.SD[slot].w) | 4u /* occluded */);
+    }
+    flush_counters(k, 0u, ctr, VPX_STAGE_SHADOW);
+}
+
+// VPX_FRAME_WAVE: the frame per wave (each wave its 16x4 strip: primary walks, shade, shadow
+// walks, resolve, finish) with wave-local compaction and no workgroup barrier.  Measured:
+// C1 0.725 vs 0.711 ms, rank 0's share at 8 ranks 0.231 vs 0.228 — the tile's barriers are
+// not what sets the small-launch floor (its longest walk chains are).  Left off.
+#ifndef VPX_FRAME_WAVE
+#define VPX_FRAME_WAVE 0
+#endif
 template <bool ONE, int MODE>
 __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_FRAME : VPX_WPE_MULTI_NEAREST) void k_frame0(
     SceneView sv, FrameArgs f, WaveBufs w, unsigned long long* __restrict__ ctr, float4* __restrict__ accum,
     uint32_t* __restrict__ rgb8, float4* __restrict__ packed) {
-    primary_tile<ONE, true>(sv, f, w, ctr);
-    __syncthreads();
-    shadow_tile<ONE>(sv, w, ctr);
-    __syncthreads();
     const uint32_t p = tile_block() * 256u + threadIdx.x;
+    if (ONE && VPX_FRAME_WAVE) {
+        primary_tile<ONE, true, true>(sv, f, w, ctr);
+        wave_sync();  // the shade's shadow slots, walked by other lanes of the wave
+        shadow_wave(sv, w, ctr);
+        wave_sync();  // the slots' occluded flags
+    } else {
+        primary_tile<ONE, true>(sv, f, w, ctr);
+        __syncthreads();
+        shadow_tile<ONE>(sv, w, ctr);
+        __syncthreads();
+    }
     resolve_path(sv, w, p);
     finish_path<MODE>(f, w, p, accum, rgb8, packed);
 }

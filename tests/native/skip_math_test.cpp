@@ -150,6 +150,17 @@ int fast_check() {
         uint32_t lo1[3] = {lo[0], lo[1], lo[2]}, hi1[3] = {hi[0], hi[1], hi[2]};
         uint32_t c1 = 7, cb1 = 7;
         const int r1 = skip_box_lean(a1, lo1, hi1, bound, c1);
+        {  // the second segment always computed (skip_box_lean<false>) takes the same box the same way
+            Walk a0 = w;
+            uint32_t lo0[3] = {lo[0], lo[1], lo[2]}, hi0[3] = {hi[0], hi[1], hi[2]};
+            uint32_t c0 = 7;
+            const int r0 = skip_box_lean<false>(a0, lo0, hi0, bound, c0);
+            if (r0 != r1 || c0 != c1 || memcmp(lo0, lo1, sizeof lo0) || memcmp(hi0, hi1, sizeof hi0) ||
+                (r0 == 0 && memcmp(&a0, &a1, sizeof(Walk)))) {
+                if (bad < 10) printf("lean<false> / lean<true> mismatch r %d/%d cells %u/%u\n", r0, r1, c0, c1);
+                ++bad;
+            }
+        }
         ++total;
         if (r1 == 2) continue;
         ++handled;
