@@ -605,6 +605,9 @@ int validate_frame(vpx_ctx* c, const vpx_frame_params* p) {
     if (!p) return fail(c, VPX_E_INVALID, "null frame params");
     if (p->width == 0 || p->height == 0 || p->width > 32768 || p->height > 32768)
         return fail(c, VPX_E_INVALID, "frame size out of range");
+    // the shadow lists pack a path index into 27 bits beside the slot number (shadow_tile)
+    if ((uint64_t)((p->width + kTile - 1) / kTile) * ((p->height + kTile - 1) / kTile) * (uint64_t)kTilePix > (1ull << 27))
+        return fail(c, VPX_E_INVALID, "frame larger than 2^27 tile-padded pixels");
     if (p->max_bounces < -1 || p->max_bounces > kMaxLevels - 2)
         return fail(c, VPX_E_INVALID, "max_bounces must be in [-1, 14]");
     if (p->area_samples < 0 || p->area_samples > 15) return fail(c, VPX_E_INVALID, "area_samples must be in [0, 15]");

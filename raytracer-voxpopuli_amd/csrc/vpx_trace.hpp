@@ -441,6 +441,9 @@ constexpr int kStepUnroll = VPX_STEP_UNROLL;  // cell steps per step-phase itera
 #define VPX_BRICK_PREFETCH 0  // 1: a brick run first loads the words (octant plane: the byte) of the brick it will exit into
 // (measured with the planes: C1 0.779 vs 0.705 ms, C2 4.79 vs 4.33, C3 6.15 vs 5.70 — an extra load per run costs more than the latency it hides)
 #endif
+#ifndef VPX_RUN_XOR
+#define VPX_RUN_XOR 0  // 1: a brick run detects the brick change from the step's old and new coordinates
+#endif
 #ifndef VPX_STEP_PREFETCH
 #define VPX_STEP_PREFETCH 0  // 1: both cells of an iteration load their words together (measured slower: C1 0.815 vs 0.773 ms, C3 6.38 vs 6.14)
 #endif
@@ -626,11 +629,15 @@ __device__ __forceinline__ bool walk_wave(const skip::GridView& g, skip::Walk& w
                             const int cap = cls == 1 ? kRun : kRunE;
 #pragma unroll
                             for (int r = 0; r < (kRunMax > 0 ? kRunMax : 1); ++r) {
+                                const uint32_t ox = w.X, oy = w.Y, oz = w.Z;
                                 if (!skip::step1(w, g.n)) {
                                     mode = kMiss;
                                     break;
                                 }
-                                if (r + 1 == cap || ((w.X >> 2) | ((w.Y >> 2) << 10) | ((w.Z >> 2) << 20)) != bk)
+                                // left the brick: this step changed a coordinate above its low two
+                                // bits (VPX_RUN_XOR), i.e. the brick key differs from bk
+                                if (r + 1 == cap || (VPX_RUN_XOR ? ((w.X ^ ox) | (w.Y ^ oy) | (w.Z ^ oz)) > 3u
+                                                                 : ((w.X >> 2) | ((w.Y >> 2) << 10) | ((w.Z >> 2) << 20)) != bk))
                                     break;  // another brick (or the run's cap): the next pass loads
                                 if (!(w.t < bound)) {
                                     mode = kMiss;

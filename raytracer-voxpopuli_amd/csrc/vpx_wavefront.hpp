@@ -207,6 +207,21 @@ __device__ __forceinline__ uint32_t tile_block() {
 }
 
 // ------------------------------------------------------------------- stage 2
+// Slot bookkeeping (VPX_SLOT_SMASK): resolve takes a slot's validity from the path's smask
+// bit (written by every shade for every path) instead of the slot's SD flags, so a rejected
+// area-light sample writes no zero slot, and resolve does not re-zero the SM word (every
+// shade rewrites it for every path before the next resolve reads it).
+#ifndef VPX_SLOT_SMASK
+#define VPX_SLOT_SMASK 1
+#endif
+// Fused tails (VPX_TAIL_LDS): k_shadow_finish / k_frame0 keep the tile's occluded flags in an
+// LDS bitmap (bit s * 256 + pixel-in-tile) instead of setting a bit in each occluded slot's
+// HBM SD word, and hand the last level's light sum from resolve to finish in registers
+// instead of through LB.  Needs VPX_SLOT_SMASK (validity from smask).
+#ifndef VPX_TAIL_LDS
+#define VPX_TAIL_LDS 1
+#endif
+static_assert(!VPX_TAIL_LDS || VPX_SLOT_SMASK, "VPX_TAIL_LDS takes slot validity from smask");
 __device__ __forceinline__ void put_slot(const WaveBufs& w, uint32_t s, uint32_t p, f3 o, f3 d, float tmax, f3 val,
                                          uint32_t fl) {
     const uint64_t i = (uint64_t)s * w.P + p;
@@ -264,8 +279,8 @@ __device__ __forceinline__ uint32_t emit_illumination(const SceneView& sv, const
             const float dst = length(dir);
             const f3 dn = dir * (1.0f / dst);
             const float c = dot(dn, n);
-            if (c <= 0) {
-                put_slot(w, i, p, mk(0.f, 0.f, 0.f), mk(0.f, 0.f, 0.f), 0.f, mk(0.f, 0.f, 0.f), 0u);
+            if (c <= 0) {  // rejected: no shadow ray (VPX_SLOT_SMASK: the smask bit says so, nothing written)
+                if (!VPX_SLOT_SMASK) put_slot(w, i, p, mk(0.f, 0.f, 0.f), mk(0.f, 0.f, 0.f), 0.f, mk(0.f, 0.f, 0.f), 0u);
                 continue;
             }
             f3 li = ld3(l.color) * c;
@@ -518,19 +533,35 @@ __global__ __launch_bounds__(256) void k_shade(SceneView sv, FrameArgs f, WaveBu
 
 // Light sum of a level once its shadow rays are resolved (kSlotOcc set by k_shadow1):
 // the evaluators' accumulation (renderer.cpp:102-207) and Illumination's *lightCount.
-__device__ __forceinline__ void resolve_path(const SceneView& sv, const WaveBufs& w, uint32_t p) {
+// occ (fused tails, VPX_TAIL_LDS): the tile's occluded bits in LDS, bit s * 256 + (p & 255);
+// out: the light sum and its level are returned instead of written to LB (the caller's
+// finish_path takes them), out->lvl = ~0u when the path has none.
+struct LightSum {
+    uint32_t lvl;
+    f3 inc;
+};
+__device__ __forceinline__ void resolve_path(const SceneView& sv, const WaveBufs& w, uint32_t p,
+                                             const uint32_t* occ = nullptr, LightSum* out = nullptr) {
+    if (out) out->lvl = ~0u;
     if (p >= w.P) return;
     const float4 sm = w.SM[p];
     const uint32_t pend = __float_as_uint(sm.w);
     if (!pend) return;
     const uint32_t kind = pend & 7u, count = (pend >> 4) & 15u, lvl = (pend >> 8) & 31u, lc = pend >> 16;
-    w.SM[p] = make_float4(0.f, 0.f, 0.f, __uint_as_float(0u));
+    if (!VPX_SLOT_SMASK) w.SM[p] = make_float4(0.f, 0.f, 0.f, __uint_as_float(0u));
     if (pend & 8u) return;  // discarded probe
+    const uint32_t valid = VPX_SLOT_SMASK ? w.smask[p] : 0u;
     f3 acc = mk(0.f, 0.f, 0.f);
     for (uint32_t s = 0; s < count; ++s) {
         const uint64_t i = (uint64_t)s * w.P + p;
-        const uint32_t fl = __float_as_uint(w.SD[i].w);
-        if (!(fl & kSlotValid) || (fl & 4u /* kSlotOcc */)) continue;
+        if (VPX_SLOT_SMASK) {
+            if (!((valid >> s) & 1u)) continue;
+            const uint32_t b = s * 256u + (p & 255u);
+            if (occ ? (occ[b >> 5] >> (b & 31u)) & 1u : __float_as_uint(w.SD[i].w) & 4u /* kSlotOcc */) continue;
+        } else {
+            const uint32_t fl = __float_as_uint(w.SD[i].w);
+            if (!(fl & kSlotValid) || (fl & 4u /* kSlotOcc */)) continue;
+        }
         const float4 v = w.SL[i];
         if (kind == kLightArea)
             acc = acc + mk(v.x, v.y, v.z);
@@ -541,7 +572,12 @@ __device__ __forceinline__ void resolve_path(const SceneView& sv, const WaveBufs
     if (kind == kLightArea) inc = (acc / (float)sv.area_samples) * mk(sm.x, sm.y, sm.z);
     inc = inc * (float)lc;
     if (pend & kPendZeroAdd) inc = mk(0.f, 0.f, 0.f) + inc;
-    w.LB[(uint64_t)lvl * w.P + p] = make_float4(inc.x, inc.y, inc.z, 0.f);
+    if (out) {
+        out->lvl = lvl;
+        out->inc = inc;
+    } else {
+        w.LB[(uint64_t)lvl * w.P + p] = make_float4(inc.x, inc.y, inc.z, 0.f);
+    }
 }
 
 __global__ __launch_bounds__(256) void k_resolve(SceneView sv, WaveBufs w) {
@@ -1009,9 +1045,24 @@ __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_BOUNCE : VPX_WPE_MULTI_N
 #endif
 // Renderer::IsOccluded for the shadow slots of G tiles (entry = slot << 27 | path); sets
 // the slot's occluded flag.  The light sums are formed in slot order by k_resolve.
+// An occluded slot: its bit in the tile's LDS bitmap (fused tails), else kSlotOcc in its SD word.
+constexpr uint32_t kOccWords = 15u * 256u / 32u;  // area_samples <= 15 slots per path
+__device__ __forceinline__ void mark_occluded(const WaveBufs& w, uint64_t slot, uint32_t e, uint32_t* occ) {
+    if (occ) {
+        const uint32_t b = (e >> 27) * 256u + (e & 255u);
+        atomicOr(&occ[b >> 5], 1u << (b & 31u));
+    } else {
+        w.SD[slot].w = __uint_as_float(__float_as_uint(w.SD[slot].w) | 4u /* kSlotOcc */);
+    }
+}
+
+// occ: the fused tails' LDS bitmap of occluded slots (one tile per workgroup), else nullptr.
 template <bool ONE>
-__device__ __forceinline__ void shadow_tile(const SceneView& sv, const WaveBufs& w, unsigned long long* __restrict__ ctr) {
+__device__ __forceinline__ void shadow_tile(const SceneView& sv, const WaveBufs& w, unsigned long long* __restrict__ ctr,
+                                            uint32_t* occ = nullptr) {
     __shared__ uint32_t sh[4];
+    if (occ)
+        for (uint32_t i = threadIdx.x; i < w.S * 8u; i += 256u) occ[i] = 0u;  // published by the barriers below
     extern __shared__ uint32_t lst_dyn[];  // [S * 256 * G]
     const uint32_t base = tile_block() * 256u * kGroupTiles;
     Counters k{0u, 0u, 0u};
@@ -1100,7 +1151,7 @@ __device__ __forceinline__ void shadow_tile(const SceneView& sv, const WaveBufs&
                 if (open)
                     cont_save(cont + atomicAdd(&ncont, 1u) * kContWords, wk, bound, e);
                 else if (hit)
-                    w.SD[slot].w = __uint_as_float(__float_as_uint(w.SD[slot].w) | 4u /* occluded */);
+                    mark_occluded(w, slot, e, occ);
             }
             __syncthreads();
             if (threadIdx.x < ncont) {
@@ -1109,7 +1160,7 @@ __device__ __forceinline__ void shadow_tile(const SceneView& sv, const WaveBufs&
                 const float bound = cont_load(cont + threadIdx.x * kContWords, wk, e2);
                 const uint64_t slot = (uint64_t)(e2 >> 27) * w.P + (e2 & 0x07ffffffu);
                 if (walk_wave<16, VPX_SKIPW_SHADOW, VPX_MINC_SHADOW, VPX_RUN_SHADOW>(gv, wk, bound, k.cells))
-                    w.SD[slot].w = __uint_as_float(__float_as_uint(w.SD[slot].w) | 4u /* occluded */);
+                    mark_occluded(w, slot, e2, occ);
             }
         }
         flush_counters(k, 0u, ctr, VPX_STAGE_SHADOW);
@@ -1138,7 +1189,7 @@ __device__ __forceinline__ void shadow_tile(const SceneView& sv, const WaveBufs&
                 }
             }
             asm volatile("" ::: "memory");
-            if (hit) w.SD[slot].w = __uint_as_float(__float_as_uint(w.SD[slot].w) | 4u /* occluded */);
+            if (hit) mark_occluded(w, slot, e, occ);
             continue;
         }
         const float4 so = w.SO[slot], sd = w.SD[slot];
@@ -1146,7 +1197,7 @@ __device__ __forceinline__ void shadow_tile(const SceneView& sv, const WaveBufs&
         r.O = mk(so.x, so.y, so.z);
         r.D = mk(sd.x, sd.y, sd.z);
         r.t = so.w;
-        if (shadow(sv, r, k)) w.SD[slot].w = __uint_as_float(__float_as_uint(sd.w) | 4u /* occluded */);
+        if (shadow(sv, r, k)) mark_occluded(w, slot, e, occ);
     }
     flush_counters(k, 0u, ctr, VPX_STAGE_SHADOW);
 }
@@ -1188,7 +1239,8 @@ enum FinishMode : int { kFinishImage = 0, kFinishPackedSample = 1, kFinishPacked
 // Fold the level records bottom-up (the recursion's rounding order), then write per MODE.
 template <int MODE>
 __device__ __forceinline__ void finish_path(const FrameArgs& f, const WaveBufs& w, uint32_t p, float4* __restrict__ accum,
-                                            uint32_t* __restrict__ rgb8, float4* __restrict__ packed) {
+                                            uint32_t* __restrict__ rgb8, float4* __restrict__ packed,
+                                            const LightSum* ls = nullptr) {
     if (p >= w.P) return;
     uint32_t x, y;
     const bool valid = path_pixel(f, p, x, y);
@@ -1204,12 +1256,15 @@ __device__ __forceinline__ void finish_path(const FrameArgs& f, const WaveBufs& 
             const uint64_t li = (uint64_t)i * w.P + p;
             const float4 a4 = w.LA[li];
             const f3 a = mk(a4.x, a4.y, a4.z);
-            if (form == kFormMulAdd) {
-                const float4 b4 = w.LB[li];
-                v = mk(b4.x, b4.y, b4.z) + v * a;
-            } else if (form == kFormAddMul) {
-                const float4 b4 = w.LB[li];
-                v = (v + mk(b4.x, b4.y, b4.z)) * a;
+            if (form == kFormMulAdd || form == kFormAddMul) {
+                f3 b;
+                if (ls && ls->lvl == (uint32_t)i) {
+                    b = ls->inc;  // this launch's resolve (fused tail)
+                } else {
+                    const float4 b4 = w.LB[li];
+                    b = mk(b4.x, b4.y, b4.z);
+                }
+                v = form == kFormMulAdd ? b + v * a : (v + b) * a;
             } else if (form == kFormMul) {
                 v = v * a;
             }
@@ -1255,11 +1310,14 @@ __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_SHADOW : VPX_WPE_MULTI_S
     SceneView sv, FrameArgs f, WaveBufs w, unsigned long long* __restrict__ ctr, float4* __restrict__ accum,
     uint32_t* __restrict__ rgb8, float4* __restrict__ packed) {
     if (!ONE) stage_tlas(sv);
-    shadow_tile<ONE>(sv, w, ctr);
+    __shared__ uint32_t occ_bits[kOccWords];
+    uint32_t* occ = VPX_TAIL_LDS ? occ_bits : nullptr;
+    shadow_tile<ONE>(sv, w, ctr, occ);
     __syncthreads();
     const uint32_t p = tile_block() * 256u + threadIdx.x;
-    resolve_path(sv, w, p);
-    finish_path<MODE>(f, w, p, accum, rgb8, packed);
+    LightSum ls;
+    resolve_path(sv, w, p, occ, VPX_TAIL_LDS ? &ls : nullptr);
+    finish_path<MODE>(f, w, p, accum, rgb8, packed, VPX_TAIL_LDS ? &ls : nullptr);
 }
 
 // The other levels' tail the same way (VPX_FUSE_RESOLVE): the tile's IsOccluded walks, the
@@ -1359,6 +1417,8 @@ __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_FRAME : VPX_WPE_MULTI_NE
     SceneView sv, FrameArgs f, WaveBufs w, unsigned long long* __restrict__ ctr, float4* __restrict__ accum,
     uint32_t* __restrict__ rgb8, float4* __restrict__ packed) {
     const uint32_t p = tile_block() * 256u + threadIdx.x;
+    __shared__ uint32_t occ_bits[kOccWords];
+    uint32_t* occ = VPX_TAIL_LDS && !VPX_FRAME_WAVE ? occ_bits : nullptr;
     if (ONE && VPX_FRAME_WAVE) {
         primary_tile<ONE, true, true>(sv, f, w, ctr);
         wave_sync();  // the shade's shadow slots, walked by other lanes of the wave
@@ -1367,11 +1427,12 @@ __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_FRAME : VPX_WPE_MULTI_NE
     } else {
         primary_tile<ONE, true>(sv, f, w, ctr);
         __syncthreads();
-        shadow_tile<ONE>(sv, w, ctr);
+        shadow_tile<ONE>(sv, w, ctr, occ);
         __syncthreads();
     }
-    resolve_path(sv, w, p);
-    finish_path<MODE>(f, w, p, accum, rgb8, packed);
+    LightSum ls;
+    resolve_path(sv, w, p, occ, VPX_TAIL_LDS ? &ls : nullptr);
+    finish_path<MODE>(f, w, p, accum, rgb8, packed, VPX_TAIL_LDS ? &ls : nullptr);
 }
 
 // ------------------------------------------------------ static-camera reprojection

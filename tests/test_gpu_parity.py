@@ -813,3 +813,15 @@ def test_sky_flag_without_texture_is_refused(pkg):
     with pytest.raises(pkg.abi.VpxError):
         ctx.render(desc.frame_params(0), acc.data_ptr())
     ctx.close()
+
+
+def test_frame_beyond_path_index_range_is_refused(pkg):
+    """The shadow lists hold a path index in 27 bits: frames of more than 2^27 tile-padded
+    pixels are refused before any launch (16384x8192 is exactly 2^27, 16384x8208 one tile row
+    more)."""
+    desc = SCENES["teapot128"](pkg.scene)
+    ctx = make_ctx(pkg, desc)
+    acc = torch.zeros(4, dtype=torch.float32, device="cuda")  # never written: refused before launch
+    with pytest.raises(pkg.abi.VpxError, match="2\\^27"):
+        ctx.render(desc.with_size(16384, 8208).frame_params(0), acc.data_ptr())
+    ctx.close()
