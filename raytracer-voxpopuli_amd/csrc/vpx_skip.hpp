@@ -368,6 +368,24 @@ template <uint32_t MINC = kMinCube>
 VPX_HD int classify_dfp(Walk& w, const GridView& g, const uint8_t* pl) {
     return classify_dfp_byte<MINC>(w, g, load_u8(pl, blk_index(w.X >> 2, w.Y >> 2, w.Z >> 2, g.nb2)));
 }
+// The same class, with the brick's cell mask loaded beside the plane byte when `spec` (the
+// walk's previous brick was occupied, so this one likely is too): an occupied brick then
+// costs one memory round trip instead of two dependent ones; a wrong guess costs a load.
+template <uint32_t MINC = kMinCube>
+VPX_HD int classify_dfp_spec(Walk& w, const GridView& g, const uint8_t* pl, bool spec) {
+    const uint32_t bi = blk_index(w.X >> 2, w.Y >> 2, w.Z >> 2, g.nb2);
+    const uint32_t k = load_u8(pl, bi);
+    uint64_t m = 0ull;
+    if (spec) m = load_mask(g.l1, bi);
+    if (k == 0u) {
+        if (!spec) m = load_mask(g.l1, bi);
+        w.m1 = m;
+        const uint32_t cb = (w.X & 3u) | ((w.Y & 3u) << 2) | ((w.Z & 3u) << 4);
+        return ((m >> cb) & 1ull) ? 0 : 1;
+    }
+    w.m1 = (uint64_t)k << w.osh;
+    return k >= MINC ? 2 : 3;
+}
 
 // The empty box of a class-2 cell: its brick's distance-field cube toward the ray's
 // octant, clipped to the grid.  Only the faces ahead of the ray matter to skip_box, so the
@@ -384,13 +402,8 @@ VPX_HD void df_box(const Walk& w, uint32_t n, uint32_t lo[3], uint32_t hi[3]) {
     }
 }
 
-// One reference step (scene.cpp:773-802), branch-free; false = left the grid.
-VPX_HD bool step1(Walk& w, uint32_t n) {
-    const bool xy = w.tx < w.ty, xz = w.tx < w.tz, yz = w.ty < w.tz;
-    const bool ax = xy && xz;
-    const bool ay = !xy && yz;
-    const bool az = !(ax || ay);
-    w.t = ax ? w.tx : (ay ? w.ty : w.tz);
+// The chosen axis' cell and head advance (shared by both forms of step1).
+VPX_HD bool step1_commit(Walk& w, uint32_t n, bool ax, bool ay, bool az) {
     w.X += ax ? (uint32_t)w.sx : 0u;
     w.Y += ay ? (uint32_t)w.sy : 0u;
     w.Z += az ? (uint32_t)w.sz : 0u;
@@ -399,6 +412,36 @@ VPX_HD bool step1(Walk& w, uint32_t n) {
     w.tz = az ? w.tz + w.dz : w.tz;
     const uint32_t m = w.X > w.Y ? w.X : w.Y;
     return (m > w.Z ? m : w.Z) < n;
+}
+
+// One reference step (scene.cpp:773-802), branch-free; false = left the grid.
+// VPX_STEP_MIN2: the reference's axis choice `x<y ? (x<z ? x : z) : (y<z ? y : z)` read as
+// "a = x<y ? x : y; a<z ? (the axis of a) : z" — the same axis for every input, NaN and ties
+// included (x<y false -> a = y, then y<z; x<y true -> x<z), with two compares and one select
+// instead of three compares and a select chain.
+// The walkers choose per walk kind (bit 18 of their RUN word, vpx_trace.hpp): with the
+// shadow walkers' 72-VGPR budget this form spilled more and measured slower on C3.
+#ifndef VPX_STEP_MIN2
+#define VPX_STEP_MIN2 1
+#endif
+template <bool MIN2 = VPX_STEP_MIN2 != 0>
+VPX_HD bool step1(Walk& w, uint32_t n) {
+  if (MIN2) {
+    const bool xy = w.tx < w.ty;
+    const float a = xy ? w.tx : w.ty;
+    const bool nz = a < w.tz;
+    const bool ax = xy && nz;
+    const bool ay = !xy && nz;
+    const bool az = !nz;
+    w.t = nz ? a : w.tz;
+    return step1_commit(w, n, ax, ay, az);
+  }
+    const bool xy = w.tx < w.ty, xz = w.tx < w.tz, yz = w.ty < w.tz;
+    const bool ax = xy && xz;
+    const bool ay = !xy && yz;
+    const bool az = !(ax || ay);
+    w.t = ax ? w.tx : (ay ? w.ty : w.tz);
+    return step1_commit(w, n, ax, ay, az);
 }
 
 // Cross the empty box [lo, hi] (per axis, inclusive) around the current cell.

@@ -419,6 +419,19 @@ constexpr int kStepUnroll = VPX_STEP_UNROLL;  // cell steps per step-phase itera
 // (skip_box_lean<true>; VPX_S2_*).  Measured (ms, one box): C1 0.713 -> 0.693, C3 5.57 ->
 // 5.34, rank 0's C1 share at 8 ranks 0.234 -> 0.222; bounce walks (rays leaving surfaces,
 // whose boxes cross binades in most waves) C2 4.27 -> 4.34 with it, so off there.
+// bit 18: step1's two-compare axis choice (VPX_STEP_MIN2 form) in the walk's steps.  Measured
+// (ms, three interleaved runs, vs the three-compare form): C1 0.678 vs 0.687; for the shadow
+// walkers (72 VGPRs, 7 waves/SIMD) it spilled two more VGPRs and C3 went 5.26 -> 5.53, so they
+// keep the three-compare form.
+#ifndef VPX_M2_NEAREST
+#define VPX_M2_NEAREST 1
+#endif
+#ifndef VPX_M2_BOUNCE
+#define VPX_M2_BOUNCE 1
+#endif
+#ifndef VPX_M2_SHADOW
+#define VPX_M2_SHADOW 0
+#endif
 #ifndef VPX_S2_NEAREST
 #define VPX_S2_NEAREST 1
 #endif
@@ -429,20 +442,23 @@ constexpr int kStepUnroll = VPX_STEP_UNROLL;  // cell steps per step-phase itera
 #define VPX_S2_SHADOW 1
 #endif
 #ifndef VPX_RUN_NEAREST
-#define VPX_RUN_NEAREST (3 | 2 << 8 | VPX_DFP_NEAREST << 16 | VPX_S2_NEAREST << 17)
+#define VPX_RUN_NEAREST (3 | 2 << 8 | VPX_DFP_NEAREST << 16 | VPX_S2_NEAREST << 17 | VPX_M2_NEAREST << 18)
 #endif
 #ifndef VPX_RUN_BOUNCE
-#define VPX_RUN_BOUNCE (4 | 1 << 8 | VPX_DFP_BOUNCE << 16 | VPX_S2_BOUNCE << 17)
+#define VPX_RUN_BOUNCE (4 | 1 << 8 | VPX_DFP_BOUNCE << 16 | VPX_S2_BOUNCE << 17 | VPX_M2_BOUNCE << 18)
 #endif
 #ifndef VPX_RUN_SHADOW
-#define VPX_RUN_SHADOW (3 | 1 << 8 | VPX_DFP_SHADOW << 16 | VPX_S2_SHADOW << 17)
+#define VPX_RUN_SHADOW (3 | 1 << 8 | VPX_DFP_SHADOW << 16 | VPX_S2_SHADOW << 17 | VPX_M2_SHADOW << 18)
 #endif
 #ifndef VPX_BRICK_PREFETCH
 #define VPX_BRICK_PREFETCH 0  // 1: a brick run first loads the words (octant plane: the byte) of the brick it will exit into
 // (measured with the planes: C1 0.779 vs 0.705 ms, C2 4.79 vs 4.33, C3 6.15 vs 5.70 — an extra load per run costs more than the latency it hides)
 #endif
+#ifndef VPX_SPEC_MASK
+#define VPX_SPEC_MASK 0  // 1: after an occupied brick, the next brick's cell mask loads beside its plane byte
+#endif
 #ifndef VPX_RUN_XOR
-#define VPX_RUN_XOR 0  // 1: a brick run detects the brick change from the step's old and new coordinates
+#define VPX_RUN_XOR 1  // 1: a brick run detects the brick change from the step's old and new coordinates
 #endif
 #ifndef VPX_STEP_PREFETCH
 #define VPX_STEP_PREFETCH 0  // 1: both cells of an iteration load their words together (measured slower: C1 0.815 vs 0.773 ms, C3 6.38 vs 6.14)
@@ -488,9 +504,12 @@ __device__ __forceinline__ bool walk_wave(const skip::GridView& g, skip::Walk& w
     constexpr int kPasses = (RUN >> 8) & 255u ? (int)((RUN >> 8) & 255u) : kStepUnroll;
     constexpr bool kDfp = (RUN >> 16) & 1u;
     constexpr bool kSeg2Branch = (RUN >> 17) & 1u;
+    constexpr bool kMin2 = (RUN >> 18) & 1u;  // step1's two-compare axis choice (vpx_skip.hpp)
     const uint8_t* pl = kDfp ? g.dfp + (uint64_t)(w.osh >> 3) * g.plane : nullptr;  // the ray's octant plane
     (void)pl;
     int mode = kStep;
+    bool spec = false;  // VPX_SPEC_MASK: the last classified brick was occupied
+    (void)spec;
     // brick-exit prefetch (VPX_BRICK_PREFETCH): the level words of brick pkey, loaded while
     // the lane ran through the brick before it (the world is static, so they stay valid)
     uint64_t pm1 = 0ull, pm2 = 0ull;
@@ -526,7 +545,7 @@ __device__ __forceinline__ bool walk_wave(const skip::GridView& g, skip::Walk& w
                     mode = kMiss;
                 } else {
                     skip::Walk w2 = w;
-                    const bool in2 = skip::step1(w2, g.n);
+                    const bool in2 = skip::step1<kMin2>(w2, g.n);
                     const skip::Words a = skip::load_words(w.X, w.Y, w.Z, g);
                     const skip::Words b = skip::load_words(in2 ? w2.X : w.X, in2 ? w2.Y : w.Y, in2 ? w2.Z : w.Z, g);
                     const int cls = skip::classify_words<MINC>(w, a);
@@ -549,7 +568,7 @@ __device__ __forceinline__ bool walk_wave(const skip::GridView& g, skip::Walk& w
                                 mode = kSkip;
                             } else {
                                 ++cells;
-                                if (!skip::step1(w, g.n)) mode = kMiss;
+                                if (!skip::step1<kMin2>(w, g.n)) mode = kMiss;
                             }
                         }
                     }
@@ -564,7 +583,7 @@ __device__ __forceinline__ bool walk_wave(const skip::GridView& g, skip::Walk& w
                 if (mode == kStep) {
                     const int cls = skip::classify<MINC>(w, g);
                     skip::Walk w2 = w;
-                    const bool in = skip::step1(w2, g.n);
+                    const bool in = skip::step1<kMin2>(w2, g.n);
                     const bool live = w.t < bound;        // the reference's `while (s.t < ray.t)`
                     const bool adv = live && (cls & 1);   // classes 1 and 3: an empty cell, step on
                     cells += (live && cls != 2) ? 1u : 0u;  // a visited cell (solid or stepped over)
@@ -591,7 +610,10 @@ __device__ __forceinline__ bool walk_wave(const skip::GridView& g, skip::Walk& w
                         if (VPX_BRICK_PREFETCH && kRun > 0 && bk == pkey)
                             cls = kDfp ? skip::classify_dfp_byte<MINC>(w, g, (uint32_t)pm1)
                                        : skip::classify_words<MINC>(w, skip::Words{pm1, pm2});
-                        else if (kDfp)
+                        else if (kDfp && VPX_SPEC_MASK) {
+                            cls = skip::classify_dfp_spec<MINC>(w, g, pl, spec);
+                            spec = cls <= 1;  // an occupied brick: guess the next one is too
+                        } else if (kDfp)
                             cls = skip::classify_dfp<MINC>(w, g, pl);
                         else
                             cls = skip::classify<MINC>(w, g);
@@ -602,7 +624,7 @@ __device__ __forceinline__ bool walk_wave(const skip::GridView& g, skip::Walk& w
                             mode = kSkip;
                         } else if (kRun == 0) {
                             ++cells;
-                            if (!skip::step1(w, g.n)) mode = kMiss;
+                            if (!skip::step1<kMin2>(w, g.n)) mode = kMiss;
                         } else {
                             const uint64_t solid = cls == 1 ? w.m1 : 0ull;
 #if VPX_BRICK_PREFETCH
@@ -630,7 +652,7 @@ __device__ __forceinline__ bool walk_wave(const skip::GridView& g, skip::Walk& w
 #pragma unroll
                             for (int r = 0; r < (kRunMax > 0 ? kRunMax : 1); ++r) {
                                 const uint32_t ox = w.X, oy = w.Y, oz = w.Z;
-                                if (!skip::step1(w, g.n)) {
+                                if (!skip::step1<kMin2>(w, g.n)) {
                                     mode = kMiss;
                                     break;
                                 }
@@ -678,7 +700,7 @@ __device__ __forceinline__ bool walk_wave(const skip::GridView& g, skip::Walk& w
                 mode = kMiss;
             } else {
                 ++cells;  // visit the landing cell, then take the leaving event
-                mode = skip::step1(w, g.n) ? kStep : kMiss;
+                mode = skip::step1<kMin2>(w, g.n) ? kStep : kMiss;
             }
         }
         VPX_PH(ck += __builtin_amdgcn_s_memtime() - t1;)

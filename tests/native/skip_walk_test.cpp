@@ -164,8 +164,44 @@ static void debug_walk(const GridView& g, Walk w, float bound) {
     }
 }
 
+// step1, both forms (the walkers' branch-free step), against the reference's branches (scene.cpp:773-802)
+// on random heads drawn from a small value set, so ties, zeros, infinities and NaNs are common:
+// the same axis, t, heads and cell.
+static long check_step1(std::mt19937_64& r) {
+    const float vals[] = {0.0f, -0.0f, 1.0f, 1.0f, 0.5f, 2.0f, 1e-30f, 3.4e38f, INFINITY, -INFINITY, NAN, 0.25f};
+    long bad = 0;
+    for (int i = 0; i < 2000000; ++i) {
+        Walk a{};
+        a.X = 5, a.Y = 6, a.Z = 7, a.sx = (r() & 1) ? 1 : -1, a.sy = (r() & 1) ? 1 : -1, a.sz = (r() & 1) ? 1 : -1;
+        float* h[3] = {&a.tx, &a.ty, &a.tz};
+        for (int k = 0; k < 3; ++k) *h[k] = (r() % 4) ? vals[r() % 12] : (float)(r() % 1000) * 0.001f;
+        a.dx = 0.125f, a.dy = 0.25f, a.dz = 0.5f;
+        Walk b = a, c = a;
+        step1<true>(a, 64);
+        step1<false>(c, 64);
+        if (b.tx < b.ty) {
+            if (b.tx < b.tz) b.t = b.tx, b.X += b.sx, b.tx += b.dx;
+            else b.t = b.tz, b.Z += b.sz, b.tz += b.dz;
+        } else {
+            if (b.ty < b.tz) b.t = b.ty, b.Y += b.sy, b.ty += b.dy;
+            else b.t = b.tz, b.Z += b.sz, b.tz += b.dz;
+        }
+        if (std::memcmp(&a, &b, sizeof(Walk)) || std::memcmp(&c, &b, sizeof(Walk))) {
+            if (bad < 5) printf("step1 mismatch: heads %a %a %a\n", b.tx, b.ty, b.tz);
+            ++bad;
+        }
+    }
+    return bad;
+}
+
 int main(int argc, char** argv) {
     _mm_setcsr(_mm_getcsr() | 0x8040u);
+    {
+        std::mt19937_64 r0(12345);
+        const long sb = check_step1(r0);
+        printf("step1 vs reference branches: 2000000 states, step1 bad=%ld\n", sb);
+        if (sb) return 1;
+    }
     const long rays = argc > 1 ? atol(argv[1]) : 20000;
     long bad = 0, total = 0;
     uint64_t cells_all = 0;
