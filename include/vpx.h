@@ -153,7 +153,8 @@ typedef struct vpx_camera {
 
 /* Per-frame parameters (the knobs of Renderer::Update / Trace). */
 typedef struct vpx_frame_params {
-    uint32_t width, height;       /* SCRWIDTH/SCRHEIGHT (compile-time in the reference)     */
+    uint32_t width, height;       /* SCRWIDTH/SCRHEIGHT (compile-time in the reference);    */
+                                  /* each <= 32768, 16x16-tile-padded W*H <= 2^27           */
     int32_t max_bounces;          /* depth handed to Trace (Renderer::maxBounces)           */
     uint32_t frame_index;         /* numRenderedFrames: weight 1/(n+1) and seed stream      */
     uint32_t seed_base;           /* added to the pixel key of the per-pixel seed           */
