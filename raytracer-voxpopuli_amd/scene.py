@@ -6,9 +6,9 @@ Everything here is HOST-side input preparation restating the reference's scene s
     474-475).  The benchmark / test workloads (C0-C4) name the reference's assets
     (teapot, monu3, roomGlass); the .vox files themselves do not travel with this repo,
     so `load_model(name)` decodes `<VPX_ASSETS_DIR>/<name>.vox` when that directory is
-    given and otherwise reads the same decoded data from tests/golden/<name>.npz (the
-    reference's vendored ogt_vox output; tests/test_vox_decode.py checks vpx_vox_decode
-    against it on all 12 reference assets);
+    given and otherwise reads the package's decoded asset store `assets/<name>.npz` (models[0]
+    + palette of all 12 reference assets as ogt_vox returns them; tests/test_vox_decode.py
+    checks vpx_vox_decode against the test fixtures and the store against the fixtures);
   - `load_model_grid`  Scene::LoadModel placement      template/scene.cpp:449-529
   - `palette_materials` LoadModel's palette override    template/scene.cpp:516-520
   - lights / materials / camera defaults                renderer.cpp:93-100,357-443; camera.h
@@ -27,7 +27,7 @@ from . import abi
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
-GOLDEN = os.path.join(REPO, "tests", "golden")
+ASSETS = os.path.join(HERE, "assets")  # decoded models (no test data is read by the product)
 NONE = abi.MAT_NONE
 
 
@@ -50,11 +50,11 @@ def decode_vox(src):
 
 def load_model(name):
     """(size[3], voxels uint8[sx*sy*sz], palette uint8[256,4]) as ogt_vox returns them:
-    decoded from $VPX_ASSETS_DIR/<name>.vox when set, else the decoded fixture."""
+    decoded from $VPX_ASSETS_DIR/<name>.vox when set, else from the package's asset store."""
     d = os.environ.get("VPX_ASSETS_DIR")
     if d:
         return decode_vox(os.path.join(d, name + ".vox"))
-    z = np.load(os.path.join(GOLDEN, name + ".npz"))
+    z = np.load(os.path.join(ASSETS, name + ".npz"))
     return z["size"].astype(np.int64), z["voxels"].astype(np.uint8), z["palette"].astype(np.uint8)
 
 

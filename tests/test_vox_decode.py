@@ -35,6 +35,19 @@ def test_reference_assets_decode_like_ogt_vox(pkg, name):
     assert np.array_equal(pal, z["palette"])
 
 
+@pytest.mark.parametrize("name", MODELS)
+def test_package_asset_store_equals_fixtures(pkg, name):
+    """The product reads its models from raytracer-voxpopuli_amd/assets (never from tests/):
+    each entry is the fixture of the same asset, byte for byte."""
+    size, vox, pal = pkg.scene.load_model(name) if not os.environ.get("VPX_ASSETS_DIR") else (None, None, None)
+    if size is None:
+        pytest.skip("VPX_ASSETS_DIR set: load_model decodes .vox files instead")
+    z = np.load(os.path.join(GOLDEN, name + ".npz"))
+    assert size.tolist() == z["size"].tolist()
+    assert np.array_equal(vox, z["voxels"])
+    assert np.array_equal(pal, z["palette"])
+
+
 # ------------------------------------------------------------------ hand-built files
 def chunk(cid, body=b"", children=b""):
     return cid.encode() + struct.pack("<II", len(body), len(children)) + body + children
