@@ -367,9 +367,10 @@ __device__ __forceinline__ skip::Walk to_walk(const Dda& s) {
 // classify / skip_box / step1 as skip::walk_skip (so results are identical), but the long
 // skip_box is executed in batches — only when few lanes of the wave still want to take
 // plain cell steps — instead of inside every step iteration of the wave.
-// Skip-phase weights (measured on C1 / C3 / C2: FindNearest 2, IsOccluded 4, bounces 2).
+// Skip-phase weights (measured on C1 / C3 / C2: FindNearest 2, IsOccluded 4, bounces 2;
+// with the two-compare step FindNearest 1: C1 0.666 vs 0.671 ms over two three-run A/Bs).
 #ifndef VPX_SKIPW_NEAREST
-#define VPX_SKIPW_NEAREST 2
+#define VPX_SKIPW_NEAREST 1
 #endif
 #ifndef VPX_SKIPW_BOUNCE
 #define VPX_SKIPW_BOUNCE 2
