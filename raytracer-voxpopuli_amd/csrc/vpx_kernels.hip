@@ -690,12 +690,13 @@ int launch_render(vpx_ctx* c, const SceneView& sv, const FrameArgs& f, uint32_t 
     WaveBufs w = c->wave;
     if (rp) w.RD = rp->rd;
     const dim3 grid(tiles), block(kThreads);
-    const size_t slds = sizeof(uint32_t) * S * kThreads * kGroupTiles;
-    const dim3 ggrid((tiles + kGroupTiles - 1) / kGroupTiles);
+    const size_t slds = sizeof(uint32_t) * S * kThreads;
     // single volume, no analytic shapes: the DDA kernels' lean instances
     const bool one = sv.num_volumes == 1 && !(sv.num_spheres | sv.num_triangles);
-    const bool fuse_tail = kFuseTail && !rp && kGroupTiles == 1;
-    if (VPX_FUSE_FRAME && one && kFuseHead && fuse_tail && f.max_bounces == 0 && tiles <= VPX_FUSE_FRAME_TILES) {
+    // the last level's shadow -> resolve -> finish as one launch (k_shadow_finish), except
+    // on the static-camera path, whose tail is the reprojection
+    const bool fuse_tail = !rp;
+    if (one && fuse_tail && f.max_bounces == 0 && tiles <= kFuseFrameTiles) {
         prof_mark(c, VPX_STAGE_FRAME);  // the whole depth-0 frame, one launch (k_frame0)
         hipLaunchKernelGGL((k_frame0<true, MODE>), grid, block, slds, c->stream, sv, f, w, c->d_ctr, accum, rgb8, packed);
         prof_mark(c, -1);
@@ -703,7 +704,7 @@ int launch_render(vpx_ctx* c, const SceneView& sv, const FrameArgs& f, uint32_t 
         return VPX_OK;
     }
     prof_mark(c, VPX_STAGE_PRIMARY);
-    const bool fuse_head = kFuseHead && f.max_bounces >= 0;
+    const bool fuse_head = f.max_bounces >= 0;  // level 0's shade at the end of k_primary
     if (fuse_head)
         hipLaunchKernelGGL((one ? k_primary<true, true> : k_primary<false, true>), grid, block, 0, c->stream, sv, f, w,
                            c->d_ctr);
@@ -725,26 +726,15 @@ int launch_render(vpx_ctx* c, const SceneView& sv, const FrameArgs& f, uint32_t 
             prof_mark(c, -1);
             break;
         }
-#if VPX_FUSE_RESOLVE
-        if (fuse_tail) {  // shadow walks + resolve as one launch (k_shadow_resolve)
-            prof_mark(c, VPX_STAGE_SHADOW);
-            hipLaunchKernelGGL(one ? k_shadow_resolve<true> : k_shadow_resolve<false>, grid, block, slds, c->stream, sv, w,
-                               c->d_ctr);
-            prof_mark(c, -1);
-        } else
-#endif
-        {
-            prof_mark(c, VPX_STAGE_SHADOW);
-            hipLaunchKernelGGL(one ? k_shadow_tile<true> : k_shadow_tile<false>, ggrid, block, slds, c->stream, sv, w,
-                               c->d_ctr);
-            prof_mark(c, -1);
-            prof_mark(c, VPX_STAGE_RESOLVE);
-            hipLaunchKernelGGL(k_resolve, grid, block, 0, c->stream, sv, w);
-            prof_mark(c, -1);
-        }
+        prof_mark(c, VPX_STAGE_SHADOW);
+        hipLaunchKernelGGL(one ? k_shadow_tile<true> : k_shadow_tile<false>, grid, block, slds, c->stream, sv, w, c->d_ctr);
+        prof_mark(c, -1);
+        prof_mark(c, VPX_STAGE_RESOLVE);
+        hipLaunchKernelGGL(k_resolve, grid, block, 0, c->stream, sv, w);
+        prof_mark(c, -1);
         if (level < f.max_bounces) {
             prof_mark(c, VPX_STAGE_BOUNCE);
-            hipLaunchKernelGGL(one ? k_nearest_tile<true> : k_nearest_tile<false>, ggrid, block, 0, c->stream, sv, w, c->d_ctr);
+            hipLaunchKernelGGL(one ? k_nearest_tile<true> : k_nearest_tile<false>, grid, block, 0, c->stream, sv, w, c->d_ctr);
             prof_mark(c, -1);
         }
     }
@@ -757,7 +747,7 @@ int launch_render(vpx_ctx* c, const SceneView& sv, const FrameArgs& f, uint32_t 
     } else {  // Renderer::Tick static branch, second pass (renderer.cpp:2024-2100)
         hipLaunchKernelGGL(k_finish_reproject, grid, block, 0, c->stream, f, w, rp->alb, rp->ill);
         hipLaunchKernelGGL(k_reproject_setup, grid, block, 0, c->stream, f, w, rp->prev);
-        hipLaunchKernelGGL(one ? k_shadow_tile<true> : k_shadow_tile<false>, ggrid, block, slds, c->stream, sv, w, c->d_ctr);
+        hipLaunchKernelGGL(one ? k_shadow_tile<true> : k_shadow_tile<false>, grid, block, slds, c->stream, sv, w, c->d_ctr);
         hipLaunchKernelGGL(k_reproject_resolve, grid, block, 0, c->stream, f, w, rp->alb, rp->ill, rp->hist, rp->temp,
                            rgb8);
         VPX_HIP(c, hipMemcpyAsync(rp->hist, rp->temp, sizeof(float4) * (size_t)f.width * f.height,
@@ -1200,15 +1190,12 @@ struct TlasBuild {
     }
 };
 
-#ifndef VPX_TLAS
-#define VPX_TLAS 1  // -DVPX_TLAS=0: the reference's linear volume loop (A/B builds)
-#endif
 int build_tlas(vpx_ctx* c, const std::vector<float4>& bounds) {
     c->tlas_on = false;
     c->tlas_nodes = 0;
     c->tlas_always = 0;
     const uint32_t count = (uint32_t)bounds.size();
-    if (!VPX_TLAS || count < 2 || count > kTlasMaxVolumes) return VPX_OK;  // one volume / too many: the linear loop
+    if (count < 2 || count > kTlasMaxVolumes) return VPX_OK;  // one volume / too many: the linear loop
     TlasBuild b;
     for (uint32_t i = 1; i < count; ++i) {  // volume 0 is walked first, outside the tree
         const float4 s = bounds[i];

@@ -296,37 +296,14 @@ VPX_HD uint32_t lin_index(uint32_t x, uint32_t y, uint32_t z, uint32_t nb) {
 #endif
 }
 
-#ifndef VPX_MIN_CUBE
-#define VPX_MIN_CUBE 2
-#endif
 // Smallest distance-field cube (in bricks) worth a skip; smaller ones are stepped through.
-constexpr uint32_t kMinCube = VPX_MIN_CUBE;
+constexpr uint32_t kMinCube = 2;
 // 0: solid cell, 1: empty cell of an occupied brick (step), 2: empty brick with a
 // distance-field cube of at least kMinCube bricks (skip it: df_box), 3: empty brick with a
 // smaller cube (step; every cell of the brick is empty).  Both level words are loaded at
 // every call and the class is formed with selects: the loads hit the cache while the
 // brick does not change, and a per-brick key cache with load branches measured 3.5 %
 // slower on C1 (the divergent branches cost more than the loads they avoid).
-// classify split in two: the level words of a cell (loads only) and the class from them,
-// so a walker can issue the loads of a later cell before it needs this one's class.
-struct Words {
-    uint64_t m1, m2;
-};
-VPX_HD Words load_words(uint32_t X, uint32_t Y, uint32_t Z, const GridView& g) {
-    return Words{load_mask(g.l1, blk_index(X >> 2, Y >> 2, Z >> 2, g.nb2)),
-                 load_mask(g.l2, blk_index(X >> 4, Y >> 4, Z >> 4, g.nb3))};
-}
-template <uint32_t MINC = kMinCube>
-VPX_HD int classify_words(Walk& w, const Words& m) {
-    w.m1 = m.m1, w.m2 = m.m2;
-    const uint32_t X = w.X, Y = w.Y, Z = w.Z;
-    const uint32_t bb = ((X >> 2) & 3u) | (((Y >> 2) & 3u) << 2) | (((Z >> 2) & 3u) << 4);
-    const uint32_t cb = (X & 3u) | ((Y & 3u) << 2) | ((Z & 3u) << 4);
-    const int cell = ((w.m1 >> cb) & 1ull) ? 0 : 1;
-    const int brick = ((uint32_t)(w.m1 >> w.osh) & 255u) >= MINC ? 2 : 3;
-    return ((w.m2 >> bb) & 1ull) ? cell : brick;
-}
-
 template <uint32_t MINC = kMinCube>
 VPX_HD int classify(Walk& w, const GridView& g) {
     const uint32_t X = w.X, Y = w.Y, Z = w.Z;
@@ -368,25 +345,6 @@ template <uint32_t MINC = kMinCube>
 VPX_HD int classify_dfp(Walk& w, const GridView& g, const uint8_t* pl) {
     return classify_dfp_byte<MINC>(w, g, load_u8(pl, blk_index(w.X >> 2, w.Y >> 2, w.Z >> 2, g.nb2)));
 }
-// The same class, with the brick's cell mask loaded beside the plane byte when `spec` (the
-// walk's previous brick was occupied, so this one likely is too): an occupied brick then
-// costs one memory round trip instead of two dependent ones; a wrong guess costs a load.
-template <uint32_t MINC = kMinCube>
-VPX_HD int classify_dfp_spec(Walk& w, const GridView& g, const uint8_t* pl, bool spec) {
-    const uint32_t bi = blk_index(w.X >> 2, w.Y >> 2, w.Z >> 2, g.nb2);
-    const uint32_t k = load_u8(pl, bi);
-    uint64_t m = 0ull;
-    if (spec) m = load_mask(g.l1, bi);
-    if (k == 0u) {
-        if (!spec) m = load_mask(g.l1, bi);
-        w.m1 = m;
-        const uint32_t cb = (w.X & 3u) | ((w.Y & 3u) << 2) | ((w.Z & 3u) << 4);
-        return ((m >> cb) & 1ull) ? 0 : 1;
-    }
-    w.m1 = (uint64_t)k << w.osh;
-    return k >= MINC ? 2 : 3;
-}
-
 // The empty box of a class-2 cell: its brick's distance-field cube toward the ray's
 // octant, clipped to the grid.  Only the faces ahead of the ray matter to skip_box, so the
 // faces behind are put at the current cell.
@@ -415,16 +373,13 @@ VPX_HD bool step1_commit(Walk& w, uint32_t n, bool ax, bool ay, bool az) {
 }
 
 // One reference step (scene.cpp:773-802), branch-free; false = left the grid.
-// VPX_STEP_MIN2: the reference's axis choice `x<y ? (x<z ? x : z) : (y<z ? y : z)` read as
+// MIN2: the reference's axis choice `x<y ? (x<z ? x : z) : (y<z ? y : z)` read as
 // "a = x<y ? x : y; a<z ? (the axis of a) : z" — the same axis for every input, NaN and ties
 // included (x<y false -> a = y, then y<z; x<y true -> x<z), with two compares and one select
 // instead of three compares and a select chain.
 // The walkers choose per walk kind (bit 18 of their RUN word, vpx_trace.hpp): with the
 // shadow walkers' 72-VGPR budget this form spilled more and measured slower on C3.
-#ifndef VPX_STEP_MIN2
-#define VPX_STEP_MIN2 1
-#endif
-template <bool MIN2 = VPX_STEP_MIN2 != 0>
+template <bool MIN2 = true>
 VPX_HD bool step1(Walk& w, uint32_t n) {
   if (MIN2) {
     const bool xy = w.tx < w.ty;
@@ -515,9 +470,6 @@ VPX_HD int skip_box(Walk& w, const uint32_t lo[3], const uint32_t hi[3], float b
 }
 
 // ------------------------------------------------------- lean tier
-#ifndef VPX_SEG2_BRANCH
-#define VPX_SEG2_BRANCH 1  // the second closed-form segment only when a lane of the wave needs it
-#endif
 // skip_box in straight-line integer code.  Each axis's sequence is put in closed form as
 // up to two segments (its own binade, then the next one after one plain IEEE step), and
 // the box is first clipped, per axis, to the events those two segments reach.  So every
@@ -694,7 +646,8 @@ VPX_HD uint32_t axis_count(const Axis& a, float h, float T, bool strict, uint32_
 // Cross the empty box [lo, hi] around the current cell, clipped per axis as above (lo / hi
 // receive the clipped box).  0: landed just before the event that leaves the clipped box
 // (cells += skipped visits); 1: the walk ends inside it (cells += visits); 2: refused.
-template <bool SEG2_BRANCH = VPX_SEG2_BRANCH != 0>
+// SEG2_BRANCH: the second closed-form segment only when a lane of the wave needs it.
+template <bool SEG2_BRANCH = true>
 VPX_HD int skip_box_lean(Walk& w, uint32_t lo[3], uint32_t hi[3], float bound, uint32_t& cells) {
     if (!((w.tx > 0.0f) & (w.ty > 0.0f) & (w.tz > 0.0f))) return 2;
     Axis ax, ay, az;

@@ -367,103 +367,35 @@ __device__ __forceinline__ skip::Walk to_walk(const Dda& s) {
 // classify / skip_box / step1 as skip::walk_skip (so results are identical), but the long
 // skip_box is executed in batches — only when few lanes of the wave still want to take
 // plain cell steps — instead of inside every step iteration of the wave.
-// Skip-phase weights (measured on C1 / C3 / C2: FindNearest 2, IsOccluded 4, bounces 2;
-// with the two-compare step FindNearest 1: C1 0.666 vs 0.671 ms over two three-run A/Bs).
-#ifndef VPX_SKIPW_NEAREST
-#define VPX_SKIPW_NEAREST 1
-#endif
-#ifndef VPX_SKIPW_BOUNCE
-#define VPX_SKIPW_BOUNCE 2
-#endif
-#ifndef VPX_SKIPW_SHADOW
-#define VPX_SKIPW_SHADOW 4
-#endif
-#ifndef VPX_STEP_THRESHOLD
-#define VPX_STEP_THRESHOLD 16
-#endif
-constexpr uint32_t kStepThreshold = VPX_STEP_THRESHOLD;
-#ifndef VPX_STEP_UNROLL
-#define VPX_STEP_UNROLL 2
-#endif
+// Skip-phase weights SKIPW per walk kind: keep stepping while steppers x SKIPW >= waiting
+// skippers (measured on C1 / C3 / C2: FindNearest 2, IsOccluded 4, bounces 2; with the
+// two-compare step FindNearest 1: C1 0.666 vs 0.671 ms over two three-run A/Bs).
+constexpr uint32_t kSkipwNearest = 1, kSkipwBounce = 2, kSkipwShadow = 4;
 // Smallest distance-field cube worth a skip per walk kind (C1, ms: FindNearest 0.430 with
 // 2 / 0.435 with 1; IsOccluded 0.383 with 2 / 0.354 with 1).
-#ifndef VPX_MINC_NEAREST
-#define VPX_MINC_NEAREST 2
-#endif
-#ifndef VPX_MINC_BOUNCE
-#define VPX_MINC_BOUNCE 2
-#endif
-#ifndef VPX_MINC_SHADOW
-#define VPX_MINC_SHADOW 1
-#endif
-constexpr int kStepUnroll = VPX_STEP_UNROLL;  // cell steps per step-phase iteration
-#ifndef VPX_STEP_SELECT
-#define VPX_STEP_SELECT 0  // 1: branch-free commit of the step with selects (measured: C1 0.792 vs 0.780 ms, C3 6.20 vs 6.16)
-#endif
-// Brick runs per walk kind: cap | passes << 8 — after its words load, a lane steps up to
-// `cap` cells inside its brick on the register copy; `passes` loads per step-phase iteration
-// (cap 0: one cell per load, VPX_STEP_UNROLL passes).  Measured (ms, one box, base 0 / 2):
-// primary C1 0.432 -> 0.402 with 3|2<<8; shadow C3 4.01 -> 3.82 with 3|1<<8; bounce C2
-// 0.654 -> 0.569 with 4|1<<8.  Caps above 4 spill (the runs are unrolled).
-// Bit 16 of the run word: the walk classifies from its octant plane (skip::classify_dfp)
-// instead of the l1 + l2 words (VPX_DFP_*).
-#ifndef VPX_DFP_NEAREST
-#define VPX_DFP_NEAREST 1
-#endif
-#ifndef VPX_DFP_BOUNCE
-#define VPX_DFP_BOUNCE 1
-#endif
-#ifndef VPX_DFP_SHADOW
-#define VPX_DFP_SHADOW 1
-#endif
-// Bit 17: the skip's second closed-form segment only when a lane of the wave needs it
-// (skip_box_lean<true>; VPX_S2_*).  Measured (ms, one box): C1 0.713 -> 0.693, C3 5.57 ->
-// 5.34, rank 0's C1 share at 8 ranks 0.234 -> 0.222; bounce walks (rays leaving surfaces,
-// whose boxes cross binades in most waves) C2 4.27 -> 4.34 with it, so off there.
-// bit 18: step1's two-compare axis choice (VPX_STEP_MIN2 form) in the walk's steps.  Measured
-// (ms, three interleaved runs, vs the three-compare form): C1 0.678 vs 0.687; for the shadow
-// walkers (72 VGPRs, 7 waves/SIMD) it spilled two more VGPRs and C3 went 5.26 -> 5.53, so they
-// keep the three-compare form.
-#ifndef VPX_M2_NEAREST
-#define VPX_M2_NEAREST 1
-#endif
-#ifndef VPX_M2_BOUNCE
-#define VPX_M2_BOUNCE 1
-#endif
-#ifndef VPX_M2_SHADOW
-#define VPX_M2_SHADOW 0
-#endif
-#ifndef VPX_S2_NEAREST
-#define VPX_S2_NEAREST 1
-#endif
-#ifndef VPX_S2_BOUNCE
-#define VPX_S2_BOUNCE 0
-#endif
-#ifndef VPX_S2_SHADOW
-#define VPX_S2_SHADOW 1
-#endif
-#ifndef VPX_RUN_NEAREST
-#define VPX_RUN_NEAREST (3 | 2 << 8 | VPX_DFP_NEAREST << 16 | VPX_S2_NEAREST << 17 | VPX_M2_NEAREST << 18)
-#endif
-#ifndef VPX_RUN_BOUNCE
-#define VPX_RUN_BOUNCE (4 | 1 << 8 | VPX_DFP_BOUNCE << 16 | VPX_S2_BOUNCE << 17 | VPX_M2_BOUNCE << 18)
-#endif
-#ifndef VPX_RUN_SHADOW
-#define VPX_RUN_SHADOW (3 | 1 << 8 | VPX_DFP_SHADOW << 16 | VPX_S2_SHADOW << 17 | VPX_M2_SHADOW << 18)
-#endif
-#ifndef VPX_BRICK_PREFETCH
-#define VPX_BRICK_PREFETCH 0  // 1: a brick run first loads the words (octant plane: the byte) of the brick it will exit into
-// (measured with the planes: C1 0.779 vs 0.705 ms, C2 4.79 vs 4.33, C3 6.15 vs 5.70 — an extra load per run costs more than the latency it hides)
-#endif
-#ifndef VPX_SPEC_MASK
-#define VPX_SPEC_MASK 0  // 1: after an occupied brick, the next brick's cell mask loads beside its plane byte
-#endif
-#ifndef VPX_RUN_XOR
-#define VPX_RUN_XOR 1  // 1: a brick run detects the brick change from the step's old and new coordinates
-#endif
-#ifndef VPX_STEP_PREFETCH
-#define VPX_STEP_PREFETCH 0  // 1: both cells of an iteration load their words together (measured slower: C1 0.815 vs 0.773 ms, C3 6.38 vs 6.14)
-#endif
+constexpr uint32_t kMincNearest = 2, kMincBounce = 2, kMincShadow = 1;
+// Brick runs per walk kind, the RUN word: cap | passes << 8 | seg2 << 17 | min2 << 18.
+// After its octant-plane byte (and, in an occupied brick, its cell mask) loads, a lane
+// steps up to `cap` cells inside its 4^3 brick on the register copy; `passes` brick loads
+// per step-phase iteration.  Measured (ms, one box): primary C1 0.432 -> 0.402 with 3|2<<8;
+// shadow C3 4.01 -> 3.82 with 3|1<<8; bounce C2 0.654 -> 0.569 with 4|1<<8.  Caps above 4
+// spill (the runs are unrolled); caps 6 / 10 for runs through all-empty bricks: C1 0.751 /
+// 0.765 vs 0.703 ms.
+// seg2 (bit 17): the skip's second closed-form segment only when a lane of the wave needs it
+// (skip_box_lean<true>).  Measured (ms, one box): C1 0.713 -> 0.693, C3 5.57 -> 5.34, rank
+// 0's C1 share at 8 ranks 0.234 -> 0.222; bounce walks (rays leaving surfaces, whose boxes
+// cross binades in most waves) C2 4.27 -> 4.34 with it, so off there.
+// min2 (bit 18): step1's two-compare axis choice (vpx_skip.hpp).  Measured (ms, three
+// interleaved runs, vs the three-compare form): C1 0.678 vs 0.687; the shadow walkers (72
+// VGPRs, 7 waves/SIMD) spilled two more VGPRs with it and C3 went 5.26 -> 5.53, so they keep
+// the three-compare form.
+// Rejected walk variants (DESIGN.md §4 keeps the measurements): classifying from the l1 + l2
+// words instead of the octant plane, a branch-free select-committed step, loading two
+// cells' words per round trip, prefetching the exit brick's byte, speculative cell-mask
+// loads after an occupied brick, walk continuations with a step budget.
+constexpr uint32_t kRunNearest = 3u | 2u << 8 | 1u << 17 | 1u << 18;
+constexpr uint32_t kRunBounce = 4u | 1u << 8 | 0u << 17 | 1u << 18;
+constexpr uint32_t kRunShadow = 3u | 1u << 8 | 1u << 17 | 0u << 18;
 #ifdef VPX_ASM_MARKS  // analysis builds only: label the walk phases in the ISA listing
 #define VPX_MARK(s) asm volatile("; MARK " s)
 #else
@@ -484,184 +416,57 @@ __device__ unsigned long long g_phase[32];
 // Phases are wave-uniform: cell steps while enough lanes want one (see SKIPW), then the
 // waiting lanes skip together.  Each lane runs exactly skip::walk_skip's sequence (the
 // reference's cells with the reference's floats).
-//
-// BUDGET > 0: the wave stops after BUDGET step iterations + skip phases (wave-uniform) and
-// *open tells which lanes are unfinished: their state is a walk to be continued (mode kStep
-// at an unclassified cell, or kSkip at a classified one — classify is idempotent, so
-// resuming both as kStep repeats no count).  The caller repacks the open walks of its tile
-// into fewer waves and continues them with another walk_wave call.
-// iters (optional): += the step iterations and skip phases this lane took part in.
-template <int PHK = 0, uint32_t SKIPW = 0, uint32_t MINC = skip::kMinCube, uint32_t RUN = 0, uint32_t BUDGET = 0>
-__device__ __forceinline__ bool walk_wave(const skip::GridView& g, skip::Walk& w, float bound, uint32_t& cells,
-                                          bool* open = nullptr, uint32_t* iters = nullptr) {
+template <int PHK, uint32_t SKIPW, uint32_t MINC, uint32_t RUN>
+__device__ __forceinline__ bool walk_wave(const skip::GridView& g, skip::Walk& w, float bound, uint32_t& cells) {
     enum : int { kStep = 0, kSkip = 1, kMiss = 2, kHit = 3 };
     constexpr int kRun = (int)(RUN & 255u);
-    // bits 24..31: the cap for runs through an all-empty brick (class 3), which read no
-    // cell bits (0: kRun as well).  Measured with caps 6 / 10 for every walk kind: C1 0.751 /
-    // 0.765 vs 0.703 ms, C2 4.60 / 4.66 vs 4.33, C3 5.92 / 5.98 vs 5.73 — the longer unrolled
-    // run costs more issue than the loads it saves.
-    constexpr int kRunE = (RUN >> 24) ? (int)(RUN >> 24) : kRun;
-    constexpr int kRunMax = kRunE > kRun ? kRunE : kRun;
-    constexpr int kPasses = (RUN >> 8) & 255u ? (int)((RUN >> 8) & 255u) : kStepUnroll;
-    constexpr bool kDfp = (RUN >> 16) & 1u;
+    constexpr int kPasses = (int)((RUN >> 8) & 255u);
     constexpr bool kSeg2Branch = (RUN >> 17) & 1u;
     constexpr bool kMin2 = (RUN >> 18) & 1u;  // step1's two-compare axis choice (vpx_skip.hpp)
-    const uint8_t* pl = kDfp ? g.dfp + (uint64_t)(w.osh >> 3) * g.plane : nullptr;  // the ray's octant plane
-    (void)pl;
+    static_assert(SKIPW > 0 && kRun > 0 && kPasses > 0, "walk_wave: skip weight, run cap and passes");
+    const uint8_t* pl = g.dfp + (uint64_t)(w.osh >> 3) * g.plane;  // the ray's octant plane
     int mode = kStep;
-    bool spec = false;  // VPX_SPEC_MASK: the last classified brick was occupied
-    (void)spec;
-    // brick-exit prefetch (VPX_BRICK_PREFETCH): the level words of brick pkey, loaded while
-    // the lane ran through the brick before it (the world is static, so they stay valid)
-    uint64_t pm1 = 0ull, pm2 = 0ull;
-    uint32_t pkey = ~0u;
-    (void)pm1, (void)pm2, (void)pkey;
     VPX_PH(uint64_t cs = 0, ck = 0, ns = 0, nk = 0, ls = 0, lk = 0, fb = 0, cf = 0;)
-    uint32_t spent = 0;  // BUDGET: step iterations + skip phases so far (wave-uniform)
-    bool over = false;
     for (;;) {
         VPX_PH(uint64_t t0 = __builtin_amdgcn_s_memtime();)
         for (;;) {
             const uint64_t stepping = __ballot(mode == kStep);
             if (!stepping) break;
-            if (BUDGET && ++spent > BUDGET) {
-                over = true;
-                break;
-            }
-            if (iters && mode == kStep) ++*iters;
             // cost-weighted: a skip phase costs several step phases, so keep stepping while
-            // steppers x SKIPW >= waiting skippers (SKIPW = 0: while >= kStepThreshold step)
-            if (SKIPW ? (uint32_t)__popcll(stepping) * SKIPW < (uint32_t)__popcll(__ballot(mode == kSkip))
-                      : ((uint32_t)__popcll(stepping) < kStepThreshold && __ballot(mode == kSkip)))
-                break;
+            // steppers x SKIPW >= waiting skippers
+            if ((uint32_t)__popcll(stepping) * SKIPW < (uint32_t)__popcll(__ballot(mode == kSkip))) break;
             VPX_PH(++ns; ls += __popcll(stepping); cf += __popcll(__ballot(mode >= kMiss));)  // cf: finished lanes per step iteration
             VPX_MARK("step body");
-#if VPX_STEP_PREFETCH
-            // Two reference steps per memory round trip: the cell the reference visits next
-            // if this one is empty is known before this one's class (step1 needs only the
-            // float heads), so both cells' level words are loaded together; the second cell's
-            // words are simply unused when this one is solid, starts a skip or ends the walk.
-            if (mode == kStep) {
-                if (!(w.t < bound)) {
-                    mode = kMiss;
-                } else {
-                    skip::Walk w2 = w;
-                    const bool in2 = skip::step1<kMin2>(w2, g.n);
-                    const skip::Words a = skip::load_words(w.X, w.Y, w.Z, g);
-                    const skip::Words b = skip::load_words(in2 ? w2.X : w.X, in2 ? w2.Y : w.Y, in2 ? w2.Z : w.Z, g);
-                    const int cls = skip::classify_words<MINC>(w, a);
-                    if (cls == 0) {
-                        ++cells;
-                        mode = kHit;
-                    } else if (cls == 2) {
-                        mode = kSkip;
-                    } else {
-                        ++cells;
-                        w.X = w2.X, w.Y = w2.Y, w.Z = w2.Z, w.t = w2.t, w.tx = w2.tx, w.ty = w2.ty, w.tz = w2.tz;
-                        if (!in2 || !(w.t < bound)) {
-                            mode = kMiss;
-                        } else {
-                            const int cls2 = skip::classify_words<MINC>(w, b);
-                            if (cls2 == 0) {
-                                ++cells;
-                                mode = kHit;
-                            } else if (cls2 == 2) {
-                                mode = kSkip;
-                            } else {
-                                ++cells;
-                                if (!skip::step1<kMin2>(w, g.n)) mode = kMiss;
-                            }
-                        }
-                    }
-                }
-            }
-#elif VPX_STEP_SELECT
-            // Branch-free step: the class and the stepped state are both formed and the state
-            // is committed with selects, so the step body has one exec region and no phi
-            // copies of the walk state (the if/else form compiled to ~50 v_mov per iteration).
-#pragma unroll
-            for (int u = 0; u < kStepUnroll; ++u) {
-                if (mode == kStep) {
-                    const int cls = skip::classify<MINC>(w, g);
-                    skip::Walk w2 = w;
-                    const bool in = skip::step1<kMin2>(w2, g.n);
-                    const bool live = w.t < bound;        // the reference's `while (s.t < ray.t)`
-                    const bool adv = live && (cls & 1);   // classes 1 and 3: an empty cell, step on
-                    cells += (live && cls != 2) ? 1u : 0u;  // a visited cell (solid or stepped over)
-                    w.X = adv ? w2.X : w.X, w.Y = adv ? w2.Y : w.Y, w.Z = adv ? w2.Z : w.Z;
-                    w.t = adv ? w2.t : w.t;
-                    w.tx = adv ? w2.tx : w.tx, w.ty = adv ? w2.ty : w.ty, w.tz = adv ? w2.tz : w.tz;
-                    mode = !live ? kMiss : cls == 0 ? kHit : cls == 2 ? kSkip : in ? kStep : kMiss;
-                }
-            }
-#else
-            // Brick runs: the class of a cell is a function of its brick's two words only, so
-            // once they are loaded a lane keeps stepping on the register copy while it stays
-            // in that brick — the cell mask (class 1) or "all empty" (class 3) decides each
-            // cell exactly as classify would — and reloads only when it crosses into another
-            // brick (or after kRun cells): fewer dependent memory round trips per cell.
+            // Brick runs: the class of a cell is a function of its brick's plane byte and cell
+            // mask only, so once they are loaded a lane keeps stepping on the register copy
+            // while it stays in that brick — the cell mask (class 1) or "all empty" (class 3)
+            // decides each cell exactly as classify would — and reloads only when it crosses
+            // into another brick (or after kRun cells): fewer dependent memory round trips.
 #pragma unroll
             for (int u = 0; u < kPasses; ++u) {
                 if (mode == kStep) {
                     if (!(w.t < bound)) {
                         mode = kMiss;
                     } else {
-                        const uint32_t bk = (w.X >> 2) | ((w.Y >> 2) << 10) | ((w.Z >> 2) << 20);
-                        int cls;
-                        if (VPX_BRICK_PREFETCH && kRun > 0 && bk == pkey)
-                            cls = kDfp ? skip::classify_dfp_byte<MINC>(w, g, (uint32_t)pm1)
-                                       : skip::classify_words<MINC>(w, skip::Words{pm1, pm2});
-                        else if (kDfp && VPX_SPEC_MASK) {
-                            cls = skip::classify_dfp_spec<MINC>(w, g, pl, spec);
-                            spec = cls <= 1;  // an occupied brick: guess the next one is too
-                        } else if (kDfp)
-                            cls = skip::classify_dfp<MINC>(w, g, pl);
-                        else
-                            cls = skip::classify<MINC>(w, g);
+                        const int cls = skip::classify_dfp<MINC>(w, g, pl);
                         if (cls == 0) {
                             ++cells;
                             mode = kHit;
                         } else if (cls == 2) {
                             mode = kSkip;
-                        } else if (kRun == 0) {
-                            ++cells;
-                            if (!skip::step1<kMin2>(w, g.n)) mode = kMiss;
                         } else {
                             const uint64_t solid = cls == 1 ? w.m1 : 0ull;
-#if VPX_BRICK_PREFETCH
-                            {  // the brick this run will most likely exit into: first boundary crossing
-                                const float ex = w.tx + (float)(w.sx > 0 ? 3u - (w.X & 3u) : (w.X & 3u)) * w.dx;
-                                const float ey = w.ty + (float)(w.sy > 0 ? 3u - (w.Y & 3u) : (w.Y & 3u)) * w.dy;
-                                const float ez = w.tz + (float)(w.sz > 0 ? 3u - (w.Z & 3u) : (w.Z & 3u)) * w.dz;
-                                uint32_t nx = w.X >> 2, ny = w.Y >> 2, nz = w.Z >> 2;
-                                if (ex <= ey && ex <= ez) nx += (uint32_t)w.sx;
-                                else if (ey <= ez) ny += (uint32_t)w.sy;
-                                else nz += (uint32_t)w.sz;
-                                if ((nx << 2) < g.n && (ny << 2) < g.n && (nz << 2) < g.n && nx < 1024u && ny < 1024u && nz < 1024u) {
-                                    if (kDfp) {  // the exit brick's plane byte only
-                                        pm1 = skip::load_u8(pl, skip::blk_index(nx, ny, nz, g.nb2));
-                                    } else {
-                                        pm1 = skip::load_mask(g.l1, skip::blk_index(nx, ny, nz, g.nb2));
-                                        pm2 = skip::load_mask(g.l2, skip::blk_index(nx >> 2, ny >> 2, nz >> 2, g.nb3));
-                                    }
-                                    pkey = nx | (ny << 10) | (nz << 20);
-                                }
-                            }
-#endif
                             ++cells;
-                            const int cap = cls == 1 ? kRun : kRunE;
 #pragma unroll
-                            for (int r = 0; r < (kRunMax > 0 ? kRunMax : 1); ++r) {
+                            for (int r = 0; r < kRun; ++r) {
                                 const uint32_t ox = w.X, oy = w.Y, oz = w.Z;
                                 if (!skip::step1<kMin2>(w, g.n)) {
                                     mode = kMiss;
                                     break;
                                 }
-                                // left the brick: this step changed a coordinate above its low two
-                                // bits (VPX_RUN_XOR), i.e. the brick key differs from bk
-                                if (r + 1 == cap || (VPX_RUN_XOR ? ((w.X ^ ox) | (w.Y ^ oy) | (w.Z ^ oz)) > 3u
-                                                                 : ((w.X >> 2) | ((w.Y >> 2) << 10) | ((w.Z >> 2) << 20)) != bk))
-                                    break;  // another brick (or the run's cap): the next pass loads
+                                // left the brick: this step changed a coordinate above its low
+                                // two bits (or the run reached its cap): the next pass loads
+                                if (r + 1 == kRun || ((w.X ^ ox) | (w.Y ^ oy) | (w.Z ^ oz)) > 3u) break;
                                 if (!(w.t < bound)) {
                                     mode = kMiss;
                                     break;
@@ -676,11 +481,9 @@ __device__ __forceinline__ bool walk_wave(const skip::GridView& g, skip::Walk& w
                     }
                 }
             }
-#endif
         }
         VPX_MARK("step phase end");
         VPX_PH(uint64_t t1 = __builtin_amdgcn_s_memtime(); cs += t1 - t0;)
-        if (BUDGET && over) break;
         const uint64_t skipping = __ballot(mode == kSkip);
         if (!skipping) {
             if (!__ballot(mode == kStep)) break;
@@ -688,9 +491,6 @@ __device__ __forceinline__ bool walk_wave(const skip::GridView& g, skip::Walk& w
         }
         VPX_PH(++nk; lk += __popcll(skipping);)
         VPX_MARK("skip phase");
-        if (BUDGET) ++spent;
-        if (iters && mode == kSkip) ++*iters;
-        pkey = ~0u;  // the prefetch does not live across a skip phase (its registers are free there)
         if (mode == kSkip) {
             uint32_t lo[3], hi[3];
             skip::df_box(w, g.n, lo, hi);
@@ -719,7 +519,6 @@ __device__ __forceinline__ bool walk_wave(const skip::GridView& g, skip::Walk& w
         atomicAdd(&g_phase[PHK + 8], cf);
     }
 #endif
-    if (BUDGET && open) *open = over && (mode == kStep || mode == kSkip);
     return mode == kHit;
 }
 
@@ -876,11 +675,7 @@ struct Counters {
 // of Setup3DDDA (Cube::Contains / Cube::Intersect, scene.cpp:166-210) fails too, so the
 // reference reads no cell of that volume and skipping it changes nothing.  The margin
 // (vpx_kernels.hip volume_bounds) dwarfs the float rounding of both tests.
-#ifndef VPX_VOLUME_CULL
-#define VPX_VOLUME_CULL 1
-#endif
 __device__ __forceinline__ bool misses_volume(const float4 b, f3 o, f3 d) {
-    if (!VPX_VOLUME_CULL) return false;
     const f3 oc = mk(b.x, b.y, b.z) - o;
     const float oc2 = dot(oc, oc), bb = dot(oc, d), dd = dot(d, d);
     const bool outside = oc2 > b.w;
@@ -953,7 +748,7 @@ __device__ __forceinline__ void for_volumes(const SceneView& sv, f3 o, f3 d, con
 // The winner's normal and material are formed once after the loop (the reference forms
 // them at every improving hit; the last one is the winner's, from the same object-space
 // ray and t), so only t and the hit cell are carried through the walks.
-template <uint32_t SKIPW = VPX_SKIPW_NEAREST, uint32_t MINC = VPX_MINC_NEAREST, uint32_t RUN = VPX_RUN_NEAREST>
+template <uint32_t SKIPW = kSkipwNearest, uint32_t MINC = kMincNearest, uint32_t RUN = kRunNearest>
 __device__ __forceinline__ int32_t find_nearest(const SceneView& sv, Ray& r, Counters& k) {
     int32_t vox = -2;
     ++k.nearest;
@@ -1009,10 +804,9 @@ __device__ __forceinline__ int32_t find_nearest(const SceneView& sv, Ray& r, Cou
     return vox;
 }
 
-#ifndef VPX_TLAS_SHADOW
-#define VPX_TLAS_SHADOW 0  // measured C4 IsOccluded: 2.67 ms through the TLAS vs 2.57 linear
-#endif
-// Renderer::IsOccluded, renderer.cpp:209-243 (scalar transforms, exact 1/D).
+// Renderer::IsOccluded, renderer.cpp:209-243 (scalar transforms, exact 1/D).  The linear
+// volume loop: through the instance TLAS it measured slower (C4 IsOccluded 2.67 vs 2.57 ms:
+// most shadow rays end in the world volume, the rest cross the instance lattice).
 __device__ __forceinline__ bool is_occluded(const SceneView& sv, const Ray& r, Counters& k) {
     bool occ = false;
     auto visit = [&](uint32_t i) {
@@ -1027,13 +821,10 @@ __device__ __forceinline__ bool is_occluded(const SceneView& sv, const Ray& r, C
         if (!dda_setup(vol, g.n, o, s)) return true;
         skip::Walk w = to_walk(s);
         // first solid cell with t < bound: occluded, the reference returns (no later volume)
-        occ = walk_wave<16, VPX_SKIPW_SHADOW, VPX_MINC_SHADOW, VPX_RUN_SHADOW>(grid_view(g), w, r.t, k.cells);
+        occ = walk_wave<16, kSkipwShadow, kMincShadow, kRunShadow>(grid_view(g), w, r.t, k.cells);
         return !occ;
     };
-    if (VPX_TLAS_SHADOW && sv.tlas_on)
-        for_volumes(sv, r.O, r.D, r.t, visit);
-    else
-        for (uint32_t i = 0; i < sv.num_volumes && !occ; ++i) visit(i);
+    for (uint32_t i = 0; i < sv.num_volumes && !occ; ++i) visit(i);
     if (occ) return true;
     for (uint32_t i = 0; i < sv.num_spheres; ++i)
         if (sphere_is_hit(sv.spheres[i], r)) return true;

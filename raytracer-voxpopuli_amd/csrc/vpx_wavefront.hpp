@@ -171,57 +171,33 @@ __device__ __forceinline__ void flush_counters(const Counters& k, uint32_t prima
 
 // The tile (logical block) a workgroup of the walking kernels takes.  Workgroups are dealt
 // round-robin to the 8 XCDs (blocks b and b + 8 share one, MI355X_MICROARCH.md "Workgroup
-// dispatch"), so consecutive tiles land in 8 different L2s.  With VPX_XCD_RUN = R > 0, runs
-// of R consecutive tiles go to one XCD and the runs are dealt round-robin: block b = 8k + x
-// takes tile ((k / R) * 8 + x) * R + k % R (the last partial round keeps t = b).  Contiguous
-// bands per XCD were measured and rejected: the image's cost is spatially uneven, and a
-// band per XCD left most XCDs idle (C1 primary 0.46 -> 0.80 ms).  A permutation of the
-// tiles — any kernel may use it or not; the fused tail uses it for its walks and finish.
-// Launches of more than VPX_XCD_BIG_TILES tiles (C3 / C4 at 3840x2160: 32400) use runs of
-// VPX_XCD_RUN_BIG: 8-tile strips per XCD measured C3 5.61 -> 5.52 ms (runs of 4: 5.62, of
-// 30 — a column band per XCD — 10.1); C1-sized launches keep t = b (runs of 8: 0.705 ->
-// 0.716 ms).
-#ifndef VPX_XCD_RUN
-#define VPX_XCD_RUN 0
-#endif
-#ifndef VPX_XCD_RUN_BIG
-#define VPX_XCD_RUN_BIG 8
-#endif
-#ifndef VPX_XCD_BIG_TILES
-#define VPX_XCD_BIG_TILES 16384
-#endif
+// dispatch"), so consecutive tiles land in 8 different L2s.  Launches of more than
+// kXcdBigTiles tiles (C3 / C4 at 3840x2160: 32400) deal runs of kXcdRunBig consecutive tiles
+// to each XCD, the runs round-robin: block b = 8k + x takes tile ((k / R) * 8 + x) * R + k % R
+// (the last partial round keeps t = b).  8-tile strips per XCD measured C3 5.61 -> 5.52 ms
+// (runs of 4: 5.62, of 30 — a column band per XCD — 10.1).  C1-sized launches keep t = b
+// (runs of 8: 0.705 -> 0.716 ms; runs of 2 / 4 within noise; a contiguous band per XCD:
+// primary 0.46 -> 0.80 ms — the image's cost is spatially uneven, most XCDs idled).
+// A permutation of the tiles: any kernel may use it or not.
+constexpr uint32_t kXcdRunBig = 8;
+constexpr uint32_t kXcdBigTiles = 16384;
 __device__ __forceinline__ uint32_t tile_block() {
-    if (VPX_XCD_RUN_BIG && gridDim.x > VPX_XCD_BIG_TILES) {
-        constexpr uint32_t R = VPX_XCD_RUN_BIG;
+    if (gridDim.x > kXcdBigTiles) {
+        constexpr uint32_t R = kXcdRunBig;
         const uint32_t b = blockIdx.x, full = (gridDim.x / (8u * R)) * 8u * R;
         if (b >= full) return b;
         const uint32_t x = b & 7u, k = b >> 3;
         return ((k / R) * 8u + x) * R + k % R;
     }
-    if (VPX_XCD_RUN == 0) return blockIdx.x;
-    constexpr uint32_t R = VPX_XCD_RUN > 0 ? VPX_XCD_RUN : 1;
-    const uint32_t b = blockIdx.x, full = (gridDim.x / (8u * R)) * 8u * R;
-    if (b >= full) return b;
-    const uint32_t x = b & 7u, k = b >> 3;
-    return ((k / R) * 8u + x) * R + k % R;
+    return blockIdx.x;
 }
 
 // ------------------------------------------------------------------- stage 2
-// Slot bookkeeping (VPX_SLOT_SMASK): resolve takes a slot's validity from the path's smask
-// bit (written by every shade for every path) instead of the slot's SD flags, so a rejected
-// area-light sample writes no zero slot, and resolve does not re-zero the SM word (every
-// shade rewrites it for every path before the next resolve reads it).
-#ifndef VPX_SLOT_SMASK
-#define VPX_SLOT_SMASK 1
-#endif
-// Fused tails (VPX_TAIL_LDS): k_shadow_finish / k_frame0 keep the tile's occluded flags in an
-// LDS bitmap (bit s * 256 + pixel-in-tile) instead of setting a bit in each occluded slot's
-// HBM SD word, and hand the last level's light sum from resolve to finish in registers
-// instead of through LB.  Needs VPX_SLOT_SMASK (validity from smask).
-#ifndef VPX_TAIL_LDS
-#define VPX_TAIL_LDS 1
-#endif
-static_assert(!VPX_TAIL_LDS || VPX_SLOT_SMASK, "VPX_TAIL_LDS takes slot validity from smask");
+// Slot bookkeeping: a shadow slot's validity is the path's smask bit (written by every shade
+// for every path), so a rejected area-light sample writes no slot and resolve does not
+// re-zero the SM word (every shade rewrites it before the next resolve reads it).  The fused
+// tails (k_shadow_finish, k_frame0) keep the tile's occluded flags in an LDS bitmap and hand
+// the last level's light sum from resolve to finish in registers.
 __device__ __forceinline__ void put_slot(const WaveBufs& w, uint32_t s, uint32_t p, f3 o, f3 d, float tmax, f3 val,
                                          uint32_t fl) {
     const uint64_t i = (uint64_t)s * w.P + p;
@@ -279,10 +255,7 @@ __device__ __forceinline__ uint32_t emit_illumination(const SceneView& sv, const
             const float dst = length(dir);
             const f3 dn = dir * (1.0f / dst);
             const float c = dot(dn, n);
-            if (c <= 0) {  // rejected: no shadow ray (VPX_SLOT_SMASK: the smask bit says so, nothing written)
-                if (!VPX_SLOT_SMASK) put_slot(w, i, p, mk(0.f, 0.f, 0.f), mk(0.f, 0.f, 0.f), 0.f, mk(0.f, 0.f, 0.f), 0u);
-                continue;
-            }
+            if (c <= 0) continue;  // rejected: no shadow ray (its smask bit stays clear, nothing written)
             f3 li = ld3(l.color) * c;
             li = li * l.color_multiplier;
             li = li * (radius * radius);
@@ -533,7 +506,7 @@ __global__ __launch_bounds__(256) void k_shade(SceneView sv, FrameArgs f, WaveBu
 
 // Light sum of a level once its shadow rays are resolved (kSlotOcc set by k_shadow1):
 // the evaluators' accumulation (renderer.cpp:102-207) and Illumination's *lightCount.
-// occ (fused tails, VPX_TAIL_LDS): the tile's occluded bits in LDS, bit s * 256 + (p & 255);
+// occ (fused tails): the tile's occluded bits in LDS, bit s * 256 + (p & 255);
 // out: the light sum and its level are returned instead of written to LB (the caller's
 // finish_path takes them), out->lvl = ~0u when the path has none.
 struct LightSum {
@@ -548,20 +521,14 @@ __device__ __forceinline__ void resolve_path(const SceneView& sv, const WaveBufs
     const uint32_t pend = __float_as_uint(sm.w);
     if (!pend) return;
     const uint32_t kind = pend & 7u, count = (pend >> 4) & 15u, lvl = (pend >> 8) & 31u, lc = pend >> 16;
-    if (!VPX_SLOT_SMASK) w.SM[p] = make_float4(0.f, 0.f, 0.f, __uint_as_float(0u));
     if (pend & 8u) return;  // discarded probe
-    const uint32_t valid = VPX_SLOT_SMASK ? w.smask[p] : 0u;
+    const uint32_t valid = w.smask[p];
     f3 acc = mk(0.f, 0.f, 0.f);
     for (uint32_t s = 0; s < count; ++s) {
         const uint64_t i = (uint64_t)s * w.P + p;
-        if (VPX_SLOT_SMASK) {
-            if (!((valid >> s) & 1u)) continue;
-            const uint32_t b = s * 256u + (p & 255u);
-            if (occ ? (occ[b >> 5] >> (b & 31u)) & 1u : __float_as_uint(w.SD[i].w) & 4u /* kSlotOcc */) continue;
-        } else {
-            const uint32_t fl = __float_as_uint(w.SD[i].w);
-            if (!(fl & kSlotValid) || (fl & 4u /* kSlotOcc */)) continue;
-        }
+        if (!((valid >> s) & 1u)) continue;
+        const uint32_t b = s * 256u + (p & 255u);
+        if (occ ? (occ[b >> 5] >> (b & 31u)) & 1u : __float_as_uint(w.SD[i].w) & 4u /* kSlotOcc */) continue;
         const float4 v = w.SL[i];
         if (kind == kLightArea)
             acc = acc + mk(v.x, v.y, v.z);
@@ -612,21 +579,9 @@ __global__ __launch_bounds__(256) void k_resolve(SceneView sv, WaveBufs w) {
 
 #define VPX_WPE(n) __attribute__((amdgpu_waves_per_eu(n)))
 
-// The multi-volume kernels read the instance TLAS (vpx_trace.hpp TlasNode) from LDS: one
-// copy per workgroup (<= 2.5 KiB); the wave-uniform traversal then broadcasts each node
-// from LDS to its lanes.  Called by every thread.
-#ifndef VPX_TLAS_LDS
-#define VPX_TLAS_LDS 0  // measured: C4 FindNearest 1.70 ms from LDS vs 1.68 with scalar loads; IsOccluded 2.81 vs 2.68
-#endif
-__device__ __forceinline__ void stage_tlas(SceneView& sv) {
-    __shared__ TlasNode s_nodes[kTlasMaxNodes];
-    if (!VPX_TLAS_LDS || !sv.tlas_on) return;  // kernel argument: uniform
-    const uint32_t words = sv.tlas_nodes * (uint32_t)(sizeof(TlasNode) / 4);
-    for (uint32_t i = threadIdx.x; i < words; i += blockDim.x)
-        reinterpret_cast<uint32_t*>(s_nodes)[i] = reinterpret_cast<const uint32_t*>(sv.tlas)[i];
-    __syncthreads();
-    sv.tlas = s_nodes;
-}
+// The multi-volume kernels read the instance TLAS nodes with scalar loads (the traversal is
+// wave-uniform); staging them in LDS measured slower (C4 FindNearest 1.70 vs 1.68 ms,
+// IsOccluded 2.81 vs 2.68).
 
 // One 256-thread workgroup per 16x16 tile.  Work is compacted inside the tile through LDS
 // (no global atomics), so a DDA wave only carries rays that will actually march, and the
@@ -651,7 +606,7 @@ __device__ __forceinline__ uint32_t block_scan(uint32_t cnt, uint32_t& total, ui
     return base + off;
 }
 
-template <uint32_t SKIPW = VPX_SKIPW_NEAREST, uint32_t MINC = VPX_MINC_NEAREST, uint32_t RUN = VPX_RUN_NEAREST>
+template <uint32_t SKIPW = kSkipwNearest, uint32_t MINC = kMincNearest, uint32_t RUN = kRunNearest>
 __device__ __forceinline__ void nearest_record(SceneView sv, const PathRay& pr, uint32_t p, Ray& r, Counters& k) {
     r.t = kBig;
     r.mat = kNone;
@@ -691,7 +646,7 @@ __device__ __forceinline__ bool nearest_begin_1v(const SceneView& sv, const Path
 __device__ __forceinline__ void nearest_end_1v(const SceneView& sv, const PathRay& w, uint32_t p, const skip::Walk& wk,
                                                bool hit);
 
-template <uint32_t SKIPW = VPX_SKIPW_NEAREST, uint32_t MINC = VPX_MINC_NEAREST, uint32_t RUN = VPX_RUN_NEAREST>
+template <uint32_t SKIPW = kSkipwNearest, uint32_t MINC = kMincNearest, uint32_t RUN = kRunNearest>
 __device__ __forceinline__ void nearest_record_1v(const SceneView& sv, const PathRay& w, uint32_t p, Counters& k) {
     bool hit = false;
     skip::Walk wk;
@@ -718,40 +673,24 @@ __device__ __forceinline__ void nearest_end_1v(const SceneView& sv, const PathRa
     w.HM[w.at(p)] = mat | (2u << 8) | inside;  // vox 0
 }
 
-#ifndef VPX_HEAD_LDS
-#define VPX_HEAD_LDS 1
-#endif
-// Primary walkers ordered by the previous frame's walk length of their pixel (w.cost):
-// 16 buckets of 2^VPX_COST_SHIFT iterations.  The CPU wave-cost model (tools/wavecost.py)
-// gives 0.81-0.83 of the pixel-order wave cost; measured (one box, ms): C1 0.697-0.704 vs
-// 0.712-0.715, C3 5.43 vs 5.54 — the lanes a wave wastes are not what sets a tile's time
-// (its longest walk is), and a per-pixel history is a frame-to-frame dependency the path
-// otherwise does not have.  Left off.
-#ifndef VPX_COST_SORT
-#define VPX_COST_SORT 0
-#endif
-#ifndef VPX_COST_SHIFT
-#define VPX_COST_SHIFT 2
-#endif
 // Primary rays + Renderer::FindNearest.  Every path's ray / RNG state is written; rays
 // that cannot hit a voxel or shape (one volume, no shapes, Setup3DDDA fails: the
 // reference returns before reading a cell) get their miss record directly.
-// WAVE: every wave of the tile runs its own 64 pixels (a 16x4 strip) through the head
-// with wave-local compaction and no workgroup barrier (k_frame0<.., WAVE>).
-template <bool ONE, bool SHADE, bool WAVE = false>
-__device__ __forceinline__ void primary_tile(SceneView& sv, const FrameArgs& f, const WaveBufs& w,
+// SHADE: the fused head keeps the tile's rays and hit records in LDS (its walkers and its
+// level-0 shade are the only readers).  Ordering the tile's walkers by their pixel's walk
+// length in the previous frame measured faster per wave but not per tile (C1 0.697-0.704 vs
+// 0.712-0.715 ms with, C3 5.43 vs 5.54 — a tile costs its longest walk) and adds a
+// frame-to-frame dependency, so walkers run in pixel order.
+template <bool ONE, bool SHADE>
+__device__ __forceinline__ void primary_tile(const SceneView& sv, const FrameArgs& f, const WaveBufs& w,
                                              unsigned long long* __restrict__ ctr) {
     __shared__ uint32_t sh[4];
     __shared__ uint32_t lst[256];
-    // the fused head keeps the tile's rays and hit records in LDS: its walkers and its
-    // level-0 shade are the only readers (VPX_HEAD_LDS=0: the global path buffers)
-    __shared__ float4 s_ray[SHADE && VPX_HEAD_LDS ? 3 * 256 : 1];
-    __shared__ uint32_t s_hm[SHADE && VPX_HEAD_LDS ? 256 : 1];
-    if (!ONE) stage_tlas(sv);
+    __shared__ float4 s_ray[SHADE ? 3 * 256 : 1];
+    __shared__ uint32_t s_hm[SHADE ? 256 : 1];
     const uint32_t tb = tile_block() * 256u;
     const uint32_t p = tb + threadIdx.x;
-    const bool lds = SHADE && VPX_HEAD_LDS;
-    const PathRay pr = lds ? PathRay{s_ray, s_ray + 256, s_ray + 512, s_hm, tb} : PathRay{w.O, w.D, w.H, w.HM, 0u};
+    const PathRay pr = SHADE ? PathRay{s_ray, s_ray + 256, s_ray + 512, s_hm, tb} : PathRay{w.O, w.D, w.H, w.HM, 0u};
     Counters k{0u, 0u, 0u};
     uint32_t prim = 0;
     bool walk = false;
@@ -779,7 +718,7 @@ __device__ __forceinline__ void primary_tile(SceneView& sv, const FrameArgs& f, 
         pr.O[pr.at(p)] = make_float4(r.O.x, r.O.y, r.O.z, __uint_as_float(rng));
         pr.D[pr.at(p)] = make_float4(r.D.x, r.D.y, r.D.z, __uint_as_float(flags));
         // an inactive path (no pixel) must read as such in the later levels' kernels
-        if (lds && !flags && f.max_bounces > 0) w.D[p] = make_float4(0.f, 0.f, 0.f, __uint_as_float(0u));
+        if (SHADE && !flags && f.max_bounces > 0) w.D[p] = make_float4(0.f, 0.f, 0.f, __uint_as_float(0u));
         if (go) {
             walk = true;
             if (ONE) {
@@ -799,55 +738,12 @@ __device__ __forceinline__ void primary_tile(SceneView& sv, const FrameArgs& f, 
         }
     }
     uint32_t total;
-    const uint32_t lbase = WAVE ? threadIdx.x & ~63u : 0u;  // this wave's part of lst
-    const uint32_t li = WAVE ? threadIdx.x & 63u : threadIdx.x;
-    if (WAVE) {
-        const uint32_t at = wave_prefix(walk ? 1u : 0u, total);
-        if (walk) lst[lbase + at] = p;
-        wave_sync();
-    } else {
-#if VPX_COST_SORT
-    // the tile's walkers counting-sorted by their pixel's walk length in the previous frame
-    // (longest first), so a wave's lanes finish together: an LDS histogram of 16 buckets,
-    // one wave's prefix sum, the scatter (any order gives the same per-ray results)
-    __shared__ uint32_t hist[16];
-    if (threadIdx.x < 16) hist[threadIdx.x] = 0u;
-    __syncthreads();
-    uint32_t key = 0, pos = 0;
-    if (walk) {
-        const uint32_t c = w.cost[p] >> VPX_COST_SHIFT;
-        key = 15u - (c < 15u ? c : 15u);
-        pos = atomicAdd(&hist[key], 1u);
-    }
-    __syncthreads();
-    if (threadIdx.x < 64) {
-        uint32_t t;
-        const uint32_t v = threadIdx.x < 16 ? hist[threadIdx.x] : 0u;
-        const uint32_t ex = wave_prefix(v, t);
-        if (threadIdx.x < 16) hist[threadIdx.x] = ex;
-        if (threadIdx.x == 0) sh[0] = t;
-    }
-    __syncthreads();
-    total = sh[0];
-    if (walk) lst[hist[key] + pos] = p;
-#else
     const uint32_t at = block_scan(walk ? 1u : 0u, total, sh);  // (its barrier orders the LDS writes)
     if (walk) lst[at] = p;
-#endif
     __syncthreads();
-    }
-    if (li < total) {
-        const uint32_t q = lst[lbase + li];
-        if (ONE && VPX_COST_SORT && !WAVE) {
-            skip::Walk wk;
-            bool hit = false;
-            uint32_t it = 0;
-            if (nearest_begin_1v(sv, pr, q, k, wk))
-                hit = walk_wave<0, VPX_SKIPW_NEAREST, VPX_MINC_NEAREST, VPX_RUN_NEAREST>(
-                    grid_view(sv.grids[uni_ptr(&sv.volumes[0])->grid_id]), wk, kBig, k.cells, nullptr, &it);
-            w.cost[q] = (uint8_t)(it < 255u ? it : 255u);
-            nearest_end_1v(sv, pr, q, wk, hit);
-        } else if (ONE) {
+    if (threadIdx.x < total) {
+        const uint32_t q = lst[threadIdx.x];
+        if (ONE) {
             nearest_record_1v(sv, pr, q, k);
         } else {
             const float4 o = pr.O[pr.at(q)], d = pr.D[pr.at(q)];
@@ -860,10 +756,7 @@ __device__ __forceinline__ void primary_tile(SceneView& sv, const FrameArgs& f, 
     }
     flush_counters(k, prim, ctr, VPX_STAGE_PRIMARY);
     if (SHADE) {  // level 0's material switch for this thread's own path (k_primary_shade)
-        if (WAVE)
-            wave_sync();  // the wave's hit records, written by its compacted walkers
-        else
-            __syncthreads();  // the tile's hit records, written by the compacted walkers
+        __syncthreads();  // the tile's hit records, written by the compacted walkers
         Counters ks{0u, 0u, 0u};
         shade_path<true>(sv, f, w, pr, p, 0, ks);
         flush_counters(ks, 0u, ctr, VPX_STAGE_SHADE);
@@ -876,175 +769,43 @@ __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_NEAREST : VPX_WPE_MULTI_
     primary_tile<ONE, SHADE>(sv, f, w, ctr);
 }
 
-// Walk continuations (bounce and shadow walks of one-volume scenes): a tile's walks first
-// run for at most VPX_CONT_* step iterations + skip phases; the unfinished ones are saved
-// to LDS, repacked densely after a workgroup barrier and continued by the first threads,
-// so the long walks of a tile share waves instead of each keeping a mostly finished wave
-// stepping (0: one unbounded pass).  Measured (one box, ms/step, base C1 0.706 / C2 4.28 /
-// C3 5.71): bounce budgets 12 / 24 -> C2 4.37 / 4.23 (noise); shadow budgets 12 / 24 / 40 ->
-// C3 6.14 / 5.95 / 5.86, C1 0.740 / 0.723 / 0.723 — the tile's longest walks set its time
-// either way, and the repack adds a barrier and LDS round trips.  Left off.
-#ifndef VPX_CONT_BOUNCE
-#define VPX_CONT_BOUNCE 0
-#endif
-#ifndef VPX_CONT_SHADOW
-#define VPX_CONT_SHADOW 0
-#endif
-constexpr uint32_t kContWords = 13;  // per open walk: t, heads, deltas, bound, X, Y, Z, signs, id
-__device__ __forceinline__ void cont_save(uint32_t* c, const skip::Walk& w, float bound, uint32_t id) {
-    c[0] = __float_as_uint(w.t), c[1] = __float_as_uint(w.tx), c[2] = __float_as_uint(w.ty), c[3] = __float_as_uint(w.tz);
-    c[4] = __float_as_uint(w.dx), c[5] = __float_as_uint(w.dy), c[6] = __float_as_uint(w.dz), c[7] = __float_as_uint(bound);
-    c[8] = w.X, c[9] = w.Y, c[10] = w.Z;
-    c[11] = (w.sx < 0 ? 1u : 0u) | (w.sy < 0 ? 2u : 0u) | (w.sz < 0 ? 4u : 0u);
-    c[12] = id;
-}
-__device__ __forceinline__ float cont_load(const uint32_t* c, skip::Walk& w, uint32_t& id) {
-    w.t = __uint_as_float(c[0]), w.tx = __uint_as_float(c[1]), w.ty = __uint_as_float(c[2]), w.tz = __uint_as_float(c[3]);
-    w.dx = __uint_as_float(c[4]), w.dy = __uint_as_float(c[5]), w.dz = __uint_as_float(c[6]);
-    w.X = c[8], w.Y = c[9], w.Z = c[10];
-    const uint32_t sg = c[11];
-    w.sx = sg & 1u ? -1 : 1, w.sy = sg & 2u ? -1 : 1, w.sz = sg & 4u ? -1 : 1;
-    skip::walk_begin(w);
-    id = c[12];
-    return __uint_as_float(c[7]);
-}
-
-#ifndef VPX_BOUNCE_BUCKETS
-#define VPX_BOUNCE_BUCKETS 0  // 1: bounce walks grouped by direction octant (measured C2: 4.88 vs 4.82 ms, no gain)
-#endif
-// Sparse stages (bounce FindNearest, IsOccluded) can gather the work of G tiles per
-// workgroup (entries stay in tile order).  Measured on C1: G = 1, 2, 4, 8 -> 2.70, 2.87,
-// 3.22, 4.36 ms/frame.  Walk lengths are heavy-tailed (mean ~60 iterations, max ~400),
-// so a wave costs about its longest ray: packing more rays per wave raises every wave's
-// maximum more than it saves in partially filled waves.  G = 1.
-#ifndef VPX_GROUP_TILES
-#define VPX_GROUP_TILES 1
-#endif
-constexpr uint32_t kGroupTiles = VPX_GROUP_TILES;
-
-// Run the last level's IsOccluded, light resolve and finish as one launch (k_shadow_finish;
-// needs one tile per workgroup).  -DVPX_FUSE_TAIL=0 restores the three launches.
-#ifndef VPX_FUSE_TAIL
-#define VPX_FUSE_TAIL 1
-#endif
-constexpr bool kFuseTail = VPX_FUSE_TAIL != 0;
-// Run level 0's material switch at the end of the primary-ray kernel (k_primary<.., true>).
-#ifndef VPX_FUSE_HEAD
-#define VPX_FUSE_HEAD 1
-#endif
-constexpr bool kFuseHead = VPX_FUSE_HEAD != 0;
-
-// Prefix scan over the G*256 paths of a workgroup (each thread scans G paths).
-template <uint32_t G>
-__device__ __forceinline__ uint32_t group_scan(const uint32_t (&cnt)[G], uint32_t& total, uint32_t* sh) {
-    uint32_t mine = 0;
-#pragma unroll
-    for (uint32_t g = 0; g < G; ++g) mine += cnt[g];
-    return block_scan(mine, total, sh);
-}
-
-// Renderer::FindNearest for the active paths of G tiles (bounce levels).
+// Renderer::FindNearest for the active paths of a tile (bounce levels).  Rejected (DESIGN.md
+// §4): grouping a tile's walks by direction octant (C2 4.88 vs 4.82 ms), gathering 2 / 4 / 8
+// tiles per workgroup (C1 2.87 / 3.22 / 4.36 vs 2.70 ms: walk lengths are heavy-tailed, a
+// wave costs its longest ray), continuing a tile's unfinished walks in repacked waves after a
+// step budget (C2 4.23-4.37 vs 4.28 ms).
 template <bool ONE>
 __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_BOUNCE : VPX_WPE_MULTI_NEAREST) void k_nearest_tile(SceneView sv, WaveBufs w, unsigned long long* __restrict__ ctr) {
-    if (!ONE) stage_tlas(sv);
     __shared__ uint32_t sh[4];
-    __shared__ uint32_t lst[256 * kGroupTiles];
-    const uint32_t base = tile_block() * 256u * kGroupTiles;
+    __shared__ uint32_t lst[256];
+    const uint32_t base = tile_block() * 256u;
     Counters k{0u, 0u, 0u};
     uint32_t total;
-#if VPX_BOUNCE_BUCKETS
-    // bounce rays leave surfaces in scattered directions: the tile's walks are grouped by the
-    // octant of their direction (LDS histogram + one wave's prefix sum, as the shadow lists),
-    // so a wave's lanes head the same way (the distance-field byte they read, their steps)
-    static_assert(kGroupTiles == 1, "octant buckets assume one tile per workgroup");
-    __shared__ uint32_t hist[8];
-    if (threadIdx.x < 8) hist[threadIdx.x] = 0u;
-    __syncthreads();
     const uint32_t p = base + threadIdx.x;
-    bool act = false;
-    uint32_t key = 0, pos = 0;
-    if (p < w.P) {
-        const float4 d = w.D[p];
-        act = (__float_as_uint(d.w) & kActive) != 0u;
-        key = (__float_as_uint(d.x) >> 31) | ((__float_as_uint(d.y) >> 31) << 1) | ((__float_as_uint(d.z) >> 31) << 2);
-        if (act) pos = atomicAdd(&hist[key], 1u);
-    }
+    const uint32_t cnt = (p < w.P && (__float_as_uint(w.D[p].w) & kActive)) ? 1u : 0u;
+    const uint32_t at = block_scan(cnt, total, sh);
+    if (cnt) lst[at] = p;
     __syncthreads();
-    if (threadIdx.x < 64) {
-        uint32_t t;
-        const uint32_t v = threadIdx.x < 8 ? hist[threadIdx.x] : 0u;
-        const uint32_t ex = wave_prefix(v, t);
-        if (threadIdx.x < 8) hist[threadIdx.x] = ex;
-        if (threadIdx.x == 0) sh[0] = t;
-    }
-    __syncthreads();
-    total = sh[0];
-    if (act) lst[hist[key] + pos] = p;
-    __syncthreads();
-#else
-    uint32_t cnt[kGroupTiles];
-#pragma unroll
-    for (uint32_t g = 0; g < kGroupTiles; ++g) {  // thread t scans paths base + t*G + g
-        const uint32_t p = base + threadIdx.x * kGroupTiles + g;
-        cnt[g] = (p < w.P && (__float_as_uint(w.D[p].w) & kActive)) ? 1u : 0u;
-    }
-    uint32_t at = group_scan<kGroupTiles>(cnt, total, sh);
-#pragma unroll
-    for (uint32_t g = 0; g < kGroupTiles; ++g)
-        if (cnt[g]) lst[at++] = base + threadIdx.x * kGroupTiles + g;
-    __syncthreads();
-#endif
-    if (ONE && VPX_CONT_BOUNCE) {
-        static_assert(kGroupTiles == 1, "continuations assume one tile per workgroup");
-        __shared__ uint32_t cont[256 * kContWords];
-        __shared__ uint32_t ncont;
-        const PathRay pr{w.O, w.D, w.H, w.HM, 0u};
-        const skip::GridView gv = grid_view(sv.grids[uni_ptr(&sv.volumes[0])->grid_id]);
-        if (threadIdx.x == 0) ncont = 0u;
-        __syncthreads();
-        if (threadIdx.x < total) {
-            const uint32_t q = lst[threadIdx.x];
-            skip::Walk wk;
-            bool hit = false, open = false;
-            if (nearest_begin_1v(sv, pr, q, k, wk))
-                hit = walk_wave<0, VPX_SKIPW_BOUNCE, VPX_MINC_BOUNCE, VPX_RUN_BOUNCE, VPX_CONT_BOUNCE>(gv, wk, kBig, k.cells, &open);
-            if (open)
-                cont_save(cont + atomicAdd(&ncont, 1u) * kContWords, wk, kBig, q);
-            else
-                nearest_end_1v(sv, pr, q, wk, hit);
-        }
-        __syncthreads();
-        if (threadIdx.x < ncont) {
-            skip::Walk wk;
-            uint32_t q;
-            cont_load(cont + threadIdx.x * kContWords, wk, q);
-            const bool hit = walk_wave<0, VPX_SKIPW_BOUNCE, VPX_MINC_BOUNCE, VPX_RUN_BOUNCE>(gv, wk, kBig, k.cells);
-            nearest_end_1v(sv, pr, q, wk, hit);
-        }
-        flush_counters(k, 0u, ctr, VPX_STAGE_BOUNCE);
-        return;
-    }
     for (uint32_t i = threadIdx.x; i < total; i += 256u) {
         const uint32_t q = lst[i];
         if (ONE) {
-            nearest_record_1v<VPX_SKIPW_BOUNCE, VPX_MINC_BOUNCE, VPX_RUN_BOUNCE>(sv, PathRay{w.O, w.D, w.H, w.HM, 0u}, q, k);
-            continue;
+            nearest_record_1v<kSkipwBounce, kMincBounce, kRunBounce>(sv, PathRay{w.O, w.D, w.H, w.HM, 0u}, q, k);
+        } else {
+            const float4 o = w.O[q], d = w.D[q];
+            Ray r;
+            r.O = mk(o.x, o.y, o.z);
+            r.D = mk(d.x, d.y, d.z);
+            r.inside = (__float_as_uint(d.w) & kInside) != 0u;
+            nearest_record<kSkipwBounce, kMincBounce, kRunBounce>(sv, PathRay{w.O, w.D, w.H, w.HM, 0u}, q, r, k);
         }
-        const float4 o = w.O[q], d = w.D[q];
-        Ray r;
-        r.O = mk(o.x, o.y, o.z);
-        r.D = mk(d.x, d.y, d.z);
-        r.inside = (__float_as_uint(d.w) & kInside) != 0u;
-        nearest_record<VPX_SKIPW_BOUNCE, VPX_MINC_BOUNCE, VPX_RUN_BOUNCE>(sv, PathRay{w.O, w.D, w.H, w.HM, 0u}, q, r, k);
     }
     flush_counters(k, 0u, ctr, VPX_STAGE_BOUNCE);
 }
 
-#ifndef VPX_SHADOW_BUCKETS
-#define VPX_SHADOW_BUCKETS 1
-#endif
-// Renderer::IsOccluded for the shadow slots of G tiles (entry = slot << 27 | path); sets
-// the slot's occluded flag.  The light sums are formed in slot order by k_resolve.
+// Renderer::IsOccluded for the shadow slots of a tile (entry = slot << 27 | path).  The
+// tile's slots are counting-sorted by the light they go to (LDS histogram, one wave's prefix
+// sum, the scatter), so a wave's lanes walk toward the same light and read the same
+// distance-field words (C3, 4 area lights x 3 samples: 6.69 -> 6.24 ms/frame).
 // An occluded slot: its bit in the tile's LDS bitmap (fused tails), else kSlotOcc in its SD word.
 constexpr uint32_t kOccWords = 15u * 256u / 32u;  // area_samples <= 15 slots per path
 __device__ __forceinline__ void mark_occluded(const WaveBufs& w, uint64_t slot, uint32_t e, uint32_t* occ) {
@@ -1063,25 +824,19 @@ __device__ __forceinline__ void shadow_tile(const SceneView& sv, const WaveBufs&
     __shared__ uint32_t sh[4];
     if (occ)
         for (uint32_t i = threadIdx.x; i < w.S * 8u; i += 256u) occ[i] = 0u;  // published by the barriers below
-    extern __shared__ uint32_t lst_dyn[];  // [S * 256 * G]
-    const uint32_t base = tile_block() * 256u * kGroupTiles;
+    extern __shared__ uint32_t lst_dyn[];  // [S * 256]
+    const uint32_t base = tile_block() * 256u;
     Counters k{0u, 0u, 0u};
-#if VPX_SHADOW_BUCKETS
     // counting sort of the tile's slots by light key: LDS histogram (the order inside a
     // bucket is whatever the atomics give — it only orders independent walks), bucket
     // offsets from one wave's prefix sum, then the scatter
     __shared__ uint32_t hist[kLightKeys];
     if (threadIdx.x < kLightKeys) hist[threadIdx.x] = 0u;
     __syncthreads();
-    uint32_t m[kGroupTiles], key[kGroupTiles], pos[kGroupTiles];
-#pragma unroll
-    for (uint32_t g = 0; g < kGroupTiles; ++g) {
-        const uint32_t p = base + threadIdx.x * kGroupTiles + g;
-        const uint32_t sm = p < w.P ? w.smask[p] : 0u;
-        m[g] = sm & kSlotBits;
-        key[g] = sm >> 16;
-        pos[g] = m[g] ? atomicAdd(&hist[key[g]], (uint32_t)__popc(m[g])) : 0u;
-    }
+    const uint32_t p = base + threadIdx.x;
+    const uint32_t sm = p < w.P ? w.smask[p] : 0u;
+    const uint32_t m = sm & kSlotBits, key = sm >> 16;
+    const uint32_t pos = m ? atomicAdd(&hist[key], (uint32_t)__popc(m)) : 0u;
     __syncthreads();
     uint32_t total = 0;
     if (threadIdx.x < 64) {
@@ -1093,79 +848,11 @@ __device__ __forceinline__ void shadow_tile(const SceneView& sv, const WaveBufs&
     }
     __syncthreads();
     total = sh[0];
-#pragma unroll
-    for (uint32_t g = 0; g < kGroupTiles; ++g) {
-        const uint32_t p = base + threadIdx.x * kGroupTiles + g;
-        uint32_t at = m[g] ? hist[key[g]] + pos[g] : 0u;
-        for (uint32_t b = m[g]; b; b &= b - 1u) lst_dyn[at++] = ((uint32_t)__ffs(b) - 1u) << 27 | p;
+    {
+        uint32_t at = m ? hist[key] + pos : 0u;
+        for (uint32_t b = m; b; b &= b - 1u) lst_dyn[at++] = ((uint32_t)__ffs(b) - 1u) << 27 | p;
     }
     __syncthreads();
-#else
-    uint32_t m[kGroupTiles], cnt[kGroupTiles];
-#pragma unroll
-    for (uint32_t g = 0; g < kGroupTiles; ++g) {
-        const uint32_t p = base + threadIdx.x * kGroupTiles + g;
-        m[g] = p < w.P ? w.smask[p] & kSlotBits : 0u;
-        cnt[g] = (uint32_t)__popc(m[g]);
-    }
-    uint32_t total;
-    uint32_t at = group_scan<kGroupTiles>(cnt, total, sh);
-#pragma unroll
-    for (uint32_t g = 0; g < kGroupTiles; ++g) {
-        const uint32_t p = base + threadIdx.x * kGroupTiles + g;
-        for (uint32_t b = m[g]; b; b &= b - 1u) lst_dyn[at++] = ((uint32_t)__ffs(b) - 1u) << 27 | p;
-    }
-    __syncthreads();
-#endif
-    if (ONE && VPX_CONT_SHADOW) {  // continuations: first pass over up to 256 slots per round
-        __shared__ uint32_t cont[256 * kContWords];
-        __shared__ uint32_t ncont;
-        const vpx_volume* vol = uni_ptr(&sv.volumes[0]);
-        const skip::GridView gv = grid_view(sv.grids[vol->grid_id]);
-        for (uint32_t base = 0; base < total; base += 256u) {
-            if (base) __syncthreads();  // the previous round's readers of cont / ncont are done
-            if (threadIdx.x == 0) ncont = 0u;
-            __syncthreads();
-            const uint32_t i = base + threadIdx.x;
-            if (i < total) {
-                const uint32_t e = lst_dyn[i];
-                const uint64_t slot = (uint64_t)(e >> 27) * w.P + (e & 0x07ffffffu);
-                ++k.shadow;
-                bool hit = false, open = false;
-                skip::Walk wk;
-                float bound = 0.f;
-                {
-                    const float4 so = w.SO[slot], sd = w.SD[slot];
-                    ORay o;
-                    o.O = xform_pos(mk(so.x, so.y, so.z), vol->inv_matrix);
-                    o.D = xform_vec(mk(sd.x, sd.y, sd.z), vol->inv_matrix);
-                    o.rD = mk(__fdiv_rn(1.0f, o.D.x), __fdiv_rn(1.0f, o.D.y), __fdiv_rn(1.0f, o.D.z));
-                    Dda s;
-                    bound = so.w;
-                    if (dda_setup(*vol, gv.n, o, s)) {
-                        wk = to_walk(s);
-                        hit = walk_wave<16, VPX_SKIPW_SHADOW, VPX_MINC_SHADOW, VPX_RUN_SHADOW, VPX_CONT_SHADOW>(gv, wk, bound, k.cells, &open);
-                    }
-                }
-                asm volatile("" ::: "memory");
-                if (open)
-                    cont_save(cont + atomicAdd(&ncont, 1u) * kContWords, wk, bound, e);
-                else if (hit)
-                    mark_occluded(w, slot, e, occ);
-            }
-            __syncthreads();
-            if (threadIdx.x < ncont) {
-                skip::Walk wk;
-                uint32_t e2;
-                const float bound = cont_load(cont + threadIdx.x * kContWords, wk, e2);
-                const uint64_t slot = (uint64_t)(e2 >> 27) * w.P + (e2 & 0x07ffffffu);
-                if (walk_wave<16, VPX_SKIPW_SHADOW, VPX_MINC_SHADOW, VPX_RUN_SHADOW>(gv, wk, bound, k.cells))
-                    mark_occluded(w, slot, e2, occ);
-            }
-        }
-        flush_counters(k, 0u, ctr, VPX_STAGE_SHADOW);
-        return;
-    }
     for (uint32_t i = threadIdx.x; i < total; i += 256u) {
         const uint32_t e = lst_dyn[i];
         const uint64_t slot = (uint64_t)(e >> 27) * w.P + (e & 0x07ffffffu);
@@ -1185,7 +872,7 @@ __device__ __forceinline__ void shadow_tile(const SceneView& sv, const WaveBufs&
                 Dda s;
                 if (dda_setup(*vol, g.n, o, s)) {
                     skip::Walk wk = to_walk(s);
-                    hit = walk_wave<16, VPX_SKIPW_SHADOW, VPX_MINC_SHADOW, VPX_RUN_SHADOW>(grid_view(g), wk, so.w, k.cells);
+                    hit = walk_wave<16, kSkipwShadow, kMincShadow, kRunShadow>(grid_view(g), wk, so.w, k.cells);
                 }
             }
             asm volatile("" ::: "memory");
@@ -1204,7 +891,6 @@ __device__ __forceinline__ void shadow_tile(const SceneView& sv, const WaveBufs&
 
 template <bool ONE>
 __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_SHADOW : VPX_WPE_MULTI_SHADOW) void k_shadow_tile(SceneView sv, WaveBufs w, unsigned long long* __restrict__ ctr) {
-    if (!ONE) stage_tlas(sv);
     shadow_tile<ONE>(sv, w, ctr);
 }
 
@@ -1309,130 +995,49 @@ template <bool ONE, int MODE>
 __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_SHADOW : VPX_WPE_MULTI_SHADOW) void k_shadow_finish(
     SceneView sv, FrameArgs f, WaveBufs w, unsigned long long* __restrict__ ctr, float4* __restrict__ accum,
     uint32_t* __restrict__ rgb8, float4* __restrict__ packed) {
-    if (!ONE) stage_tlas(sv);
-    __shared__ uint32_t occ_bits[kOccWords];
-    uint32_t* occ = VPX_TAIL_LDS ? occ_bits : nullptr;
+    __shared__ uint32_t occ[kOccWords];
     shadow_tile<ONE>(sv, w, ctr, occ);
     __syncthreads();
     const uint32_t p = tile_block() * 256u + threadIdx.x;
     LightSum ls;
-    resolve_path(sv, w, p, occ, VPX_TAIL_LDS ? &ls : nullptr);
-    finish_path<MODE>(f, w, p, accum, rgb8, packed, VPX_TAIL_LDS ? &ls : nullptr);
+    resolve_path(sv, w, p, occ, &ls);
+    finish_path<MODE>(f, w, p, accum, rgb8, packed, &ls);
 }
 
-// The other levels' tail the same way (VPX_FUSE_RESOLVE): the tile's IsOccluded walks, the
-// barrier, then each thread's light resolve — k_shadow_tile -> k_resolve as one launch, so
-// the resolve's loads and stores of finished tiles overlap other tiles' walks.  Measured on
-// C2 (three runs each): 4.32-4.34 vs 4.30-4.31 ms with the two launches — the barrier holds
-// the tile's finished waves longer than the separate 14-µs resolve costs.  Left off.
-#ifndef VPX_FUSE_RESOLVE
-#define VPX_FUSE_RESOLVE 0
-#endif
-template <bool ONE>
-__global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_SHADOW : VPX_WPE_MULTI_SHADOW) void k_shadow_resolve(
-    SceneView sv, WaveBufs w, unsigned long long* __restrict__ ctr) {
-    if (!ONE) stage_tlas(sv);
-    shadow_tile<ONE>(sv, w, ctr);
-    __syncthreads();
-    resolve_path(sv, w, tile_block() * 256u + threadIdx.x);
-}
-
-// A Trace-depth-0 frame in one launch (VPX_FUSE_FRAME): the fused head (primary walk +
-// level-0 shade) and the fused tail (the tile's shadow walks, resolve, finish) of the same
-// tile, one barrier apart — the shade's slots are read back by the workgroup that wrote them
-// (as k_shadow_finish reads its own occluded flags), and a tile's shadow walks overlap other
+// The other levels' tail is NOT fused the same way (IsOccluded walks + barrier + resolve as
+// one launch measured 4.32-4.34 vs 4.30-4.31 ms on C2: the barrier holds the tile's finished
+// waves longer than the separate 14-us resolve costs).
+//
+// A Trace-depth-0 frame in one launch (k_frame0): the fused head (primary walk + level-0
+// shade) and the fused tail (the tile's shadow walks, resolve, finish) of the same tile, one
+// barrier apart — the shade's slots are read back by the workgroup that wrote them (as
+// k_shadow_finish reads its own occluded flags), and a tile's shadow walks overlap other
 // tiles' primary walks instead of waiting for the slowest primary wave of the frame.
-// Used for single-volume launches of at most VPX_FUSE_FRAME_TILES tiles, where the walkers'
+// Used for single-volume launches of at most kFuseFrameTiles tiles, where the walkers'
 // drain tails dominate (one MI355X, ms, two launches -> one, VPX_WPE_FRAME 5: C1 0.723 ->
 // 0.713; rank 0's share of C1 at 8 ranks 0.297 -> 0.228; C1 at 64x64 0.234 -> 0.198).  On
 // the big launches the two kernels stay apart (C3 5.84 vs 6.14; C4, 65 volumes, 59.3 vs
-// 64.5): there the separate kernels' 6 waves/SIMD pay more than the shared drain.
-#ifndef VPX_FUSE_FRAME
-#define VPX_FUSE_FRAME 1
-#endif
-#ifndef VPX_FUSE_FRAME_TILES
-#define VPX_FUSE_FRAME_TILES 12288
-#endif
+// 64.5): there the separate kernels' 6 waves/SIMD pay more than the shared drain.  Running
+// each wave's 16x4 strip through the whole frame with wave-local compaction and no
+// workgroup barrier measured C1 0.725 vs 0.711 ms (the tile's barriers are not what sets the
+// small-launch floor; its longest walk chains are).
+constexpr uint32_t kFuseFrameTiles = 12288;
 #ifndef VPX_WPE_FRAME
 #define VPX_WPE_FRAME 5  // 6: 272 spilled VGPRs; 5: 9; 4: none but slower
-#endif
-// shadow_tile for one wave's 64 paths (single volume): the slots counting-sorted by light
-// key in a wave-local histogram, walked by the wave's lanes, no workgroup barrier.
-__device__ __forceinline__ void shadow_wave(const SceneView& sv, const WaveBufs& w, unsigned long long* __restrict__ ctr) {
-    extern __shared__ uint32_t lst_dyn[];  // [S * 256]: this wave's S * 64
-    __shared__ uint32_t hist_w[4 * kLightKeys];
-    const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
-    uint32_t* lst = lst_dyn + wid * 64u * w.S;
-    uint32_t* hist = hist_w + wid * kLightKeys;
-    const uint32_t p = tile_block() * 256u + threadIdx.x;
-    Counters k{0u, 0u, 0u};
-    if (lane < kLightKeys) hist[lane] = 0u;
-    wave_sync();
-    const uint32_t sm = p < w.P ? w.smask[p] : 0u;
-    const uint32_t m = sm & kSlotBits, key = sm >> 16;
-    const uint32_t pos = m ? atomicAdd(&hist[key], (uint32_t)__popc(m)) : 0u;
-    wave_sync();
-    uint32_t total;
-    const uint32_t ex = wave_prefix(lane < kLightKeys ? hist[lane] : 0u, total);
-    wave_sync();  // every lane has read its bucket count before the offsets replace them
-    if (lane < kLightKeys) hist[lane] = ex;
-    wave_sync();
-    uint32_t at = m ? hist[key] + pos : 0u;
-    for (uint32_t b = m; b; b &= b - 1u) lst[at++] = ((uint32_t)__ffs(b) - 1u) << 27 | p;
-    wave_sync();
-    const vpx_volume* vol = uni_ptr(&sv.volumes[0]);
-    const DevGrid g = sv.grids[vol->grid_id];
-    for (uint32_t i = lane; i < total; i += 64u) {
-        const uint32_t e = lst[i];
-        const uint64_t slot = (uint64_t)(e >> 27) * w.P + (e & 0x07ffffffu);
-        ++k.shadow;
-        bool hit = false;
-        {
-            const float4 so = w.SO[slot], sd = w.SD[slot];
-            ORay o;
-            o.O = xform_pos(mk(so.x, so.y, so.z), vol->inv_matrix);
-            o.D = xform_vec(mk(sd.x, sd.y, sd.z), vol->inv_matrix);
-            o.rD = mk(__fdiv_rn(1.0f, o.D.x), __fdiv_rn(1.0f, o.D.y), __fdiv_rn(1.0f, o.D.z));
-            Dda s;
-            if (dda_setup(*vol, g.n, o, s)) {
-                skip::Walk wk = to_walk(s);
-                hit = walk_wave<16, VPX_SKIPW_SHADOW, VPX_MINC_SHADOW, VPX_RUN_SHADOW>(grid_view(g), wk, so.w, k.cells);
-            }
-        }
-        asm volatile("" ::: "memory");
-        if (hit) w.SD[slot].w = __uint_as_float(__float_as_uint(w.SD[slot].w) | 4u /* occluded */);
-    }
-    flush_counters(k, 0u, ctr, VPX_STAGE_SHADOW);
-}
-
-// VPX_FRAME_WAVE: the frame per wave (each wave its 16x4 strip: primary walks, shade, shadow
-// walks, resolve, finish) with wave-local compaction and no workgroup barrier.  Measured:
-// C1 0.725 vs 0.711 ms, rank 0's share at 8 ranks 0.231 vs 0.228 — the tile's barriers are
-// not what sets the small-launch floor (its longest walk chains are).  Left off.
-#ifndef VPX_FRAME_WAVE
-#define VPX_FRAME_WAVE 0
 #endif
 template <bool ONE, int MODE>
 __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_FRAME : VPX_WPE_MULTI_NEAREST) void k_frame0(
     SceneView sv, FrameArgs f, WaveBufs w, unsigned long long* __restrict__ ctr, float4* __restrict__ accum,
     uint32_t* __restrict__ rgb8, float4* __restrict__ packed) {
     const uint32_t p = tile_block() * 256u + threadIdx.x;
-    __shared__ uint32_t occ_bits[kOccWords];
-    uint32_t* occ = VPX_TAIL_LDS && !VPX_FRAME_WAVE ? occ_bits : nullptr;
-    if (ONE && VPX_FRAME_WAVE) {
-        primary_tile<ONE, true, true>(sv, f, w, ctr);
-        wave_sync();  // the shade's shadow slots, walked by other lanes of the wave
-        shadow_wave(sv, w, ctr);
-        wave_sync();  // the slots' occluded flags
-    } else {
-        primary_tile<ONE, true>(sv, f, w, ctr);
-        __syncthreads();
-        shadow_tile<ONE>(sv, w, ctr, occ);
-        __syncthreads();
-    }
+    __shared__ uint32_t occ[kOccWords];
+    primary_tile<ONE, true>(sv, f, w, ctr);
+    __syncthreads();
+    shadow_tile<ONE>(sv, w, ctr, occ);
+    __syncthreads();
     LightSum ls;
-    resolve_path(sv, w, p, occ, VPX_TAIL_LDS ? &ls : nullptr);
-    finish_path<MODE>(f, w, p, accum, rgb8, packed, VPX_TAIL_LDS ? &ls : nullptr);
+    resolve_path(sv, w, p, occ, &ls);
+    finish_path<MODE>(f, w, p, accum, rgb8, packed, &ls);
 }
 
 // ------------------------------------------------------ static-camera reprojection

@@ -228,7 +228,7 @@ def test_sharded_accumulator_equals_monolithic(pkg, orc):
 
 
 def test_fused_frame_equals_two_launch_frame(pkg):
-    """The depth-0 frame runs as one launch (k_frame0) up to VPX_FUSE_FRAME_TILES (12288)
+    """The depth-0 frame runs as one launch (k_frame0) up to kFuseFrameTiles (12288)
     tiles and as k_primary + k_shadow_finish above.  The same 2048x1600 frame (12800 tiles)
     rendered whole (two launches) and as two ranks' halves (6400 tiles each: fused) must
     agree bit for bit over 2 AA frames with area lights; the profile names the stage each
