@@ -9,7 +9,8 @@ DESIGN.md §4).  The headline line is C1 (BASELINE.json configs[1]): 1920x1080, 
 (monu3.vox tiled), 1 spp, depth 0.  Inputs (world, tables, accumulator)
 are resident in HBM before timing.
 
-N > 1 (torchrun, one rank per GPU): STRONG scaling — the configured frame (C1: 1920x1080
+N > 1 (one rank process per GPU: under torchrun, or started by this script itself as a
+torch.distributed.run child when run as plain `python bench.py --gpus N`): STRONG scaling — the configured frame (C1: 1920x1080
 at every N; C3/C4: 3840x2160) is cut into 16x16 tiles dealt round-robin to the ranks; each
 rank accumulates and tonemaps its own tiles (the accumulator is sharded with them) and an
 RCCL gather (torch.distributed, backend nccl) brings the packed RGB8 of the step's last
@@ -333,6 +334,27 @@ def cpu_baseline(pkg, desc, budget_s=12.0):
     return out
 
 
+def free_port():
+    """A TCP port on 127.0.0.1 that was free a moment ago (the ranks' rendezvous)."""
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_command(argv, n, port):
+    """The child command that runs this bench as N ranks, one process per GPU (the
+    driver's own form: torch.distributed.run, rendezvous on 127.0.0.1)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+
+
+def needs_launch(n, environ=os.environ):
+    """--gpus N > 1 started as a plain process (no WORLD_SIZE from a launcher): this process
+    must start the N rank processes itself."""
+    return n > 1 and "WORLD_SIZE" not in environ
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -343,6 +365,18 @@ def main():
     ap.add_argument("--no-extra", action="store_true", help="skip extra_configs / weak_scaling")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     args = ap.parse_args()
+    if needs_launch(args.gpus):
+        # `python bench.py --gpus N` without torchrun: start the N ranks as child processes
+        # before this process touches the GPU (no HIP call has been made yet), relay their
+        # output (rank 0 prints the JSON line) and exit with their status
+        import subprocess
+        cmd = launch_command(sys.argv[1:], args.gpus, free_port())
+        print("bench.py: launching", args.gpus, "ranks:", " ".join(cmd), file=sys.stderr, flush=True)
+        sys.exit(subprocess.run(cmd).returncode)
+    if os.environ.get("VPX_BENCH_LAUNCH_PROBE") == "1":  # tests/test_bench_launch.py: the ranks' view, no GPU work
+        print(json.dumps({"rank": int(os.environ.get("RANK", "0")), "world": int(os.environ.get("WORLD_SIZE", "1")),
+                          "local_rank": int(os.environ.get("LOCAL_RANK", "0")), "argv": sys.argv[1:]}), flush=True)
+        return
     pkg = entry.load_package()
     env = Env(args.gpus)
     sha = lib_sha256(pkg)

@@ -206,7 +206,13 @@ int vpx_create(int device, vpx_ctx** out);
    device; with accum == NULL each member keeps the running average of its own tiles and
    only RGB8 travels into rgb8.  vpx_set_stream sets devices[0]'s stream; unit entries,
    profiles, vpx_render_reproject and the rank-level entries (vpx_render_tiles*,
-   vpx_composite_*) run on devices[0]; vpx_get_counters sums the members. */
+   vpx_composite_*) run on devices[0]; vpx_get_counters sums the members.  Every call on a
+   set restores the caller's current HIP device before it returns; stats (vpx_render) read
+   the members' counters outside the launches, so the members still overlap.
+   Verification status: sets that repeat a device (the device-copy gather) are tested bit
+   for bit on one GPU; the distinct-device RCCL gather has its test
+   (test_device_set_equals_single_device[devices3]) but runs only on a node with >= 2 GPUs
+   and has not yet executed on hardware. */
 int vpx_create_multi(const int* devices, int ndev, vpx_ctx** out);
 int vpx_destroy(vpx_ctx* ctx);
 const char* vpx_last_error(const vpx_ctx* ctx);

@@ -18,6 +18,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <array>
 #include <vector>
 
 #include "vpx_wavefront.hpp"
@@ -468,10 +469,24 @@ int fail(vpx_ctx* c, int code, const std::string& msg) {
     return code;
 }
 
+// The caller's current HIP device, restored when the scope ends: a device-set call sets each
+// member's device in turn and must not leave the caller on the last one (torch tensors or
+// buffers the caller allocates afterwards belong on devices[0]).
+struct DeviceGuard {
+    int dev = -1;
+    DeviceGuard() {
+        if (hipGetDevice(&dev) != hipSuccess) dev = -1;
+    }
+    ~DeviceGuard() {
+        if (dev >= 0) (void)hipSetDevice(dev);
+    }
+};
+
 // Device-set contexts forward to their members: every member (uploads / state) or member 0
 // (unit entries, profiles, the single-image static-camera path, the rank-level primitives).
 template <class F>
 int group_all(vpx_ctx* c, F f) {
+    DeviceGuard keep;
     for (vpx_ctx* m : c->members) {
         if (hipSetDevice(m->device) != hipSuccess) return fail(c, VPX_E_DEVICE, "hipSetDevice");
         const int rc = f(m);
@@ -481,6 +496,7 @@ int group_all(vpx_ctx* c, F f) {
 }
 template <class F>
 int group_first(vpx_ctx* c, F f) {
+    DeviceGuard keep;
     vpx_ctx* m = c->members[0];
     if (hipSetDevice(m->device) != hipSuccess) return fail(c, VPX_E_DEVICE, "hipSetDevice");
     const int rc = f(m);
@@ -622,7 +638,7 @@ int validate_frame(vpx_ctx* c, const vpx_frame_params* p) {
 int ensure_wave(vpx_ctx* c, uint32_t P, uint32_t L, uint32_t S) {
     const size_t f4 = sizeof(float4);
     const size_t bytes = (size_t)P * (f4 * (5 + 2 * (size_t)L + 3 * (size_t)S + 1) + 3 * sizeof(uint32_t)) +
-                         sizeof(uint32_t) * (size_t)P + (size_t)P + 17 * 256;
+                         sizeof(uint32_t) * (size_t)P + 16 * 256;
     if (bytes > c->wave_bytes) {
         if (c->d_wave) {
             VPX_HIP(c, hipStreamSynchronize(c->stream));
@@ -642,7 +658,6 @@ int ensure_wave(vpx_ctx* c, uint32_t P, uint32_t L, uint32_t S) {
     WaveBufs& w = c->wave;
     w.P = P;
     w.S = S;
-    w.cost = (uint8_t*)take(P);  // first: its address survives L / S changes (a scheduling hint only)
     w.O = (float4*)take(f4 * P);
     w.D = (float4*)take(f4 * P);
     w.H = (float4*)take(f4 * P);
@@ -810,8 +825,16 @@ int vpx_create(int device, vpx_ctx** out) {
 
 int vpx_destroy(vpx_ctx* c) {
     if (!c) return VPX_E_INVALID;
-    if (c->gl_res) (void)vpx_gl_register_buffer(c, 0u);
+    if (c->gl_res) {  // a context destroyed while its GL buffer is mapped: unmap, then unregister
+        vpx_ctx* h = c->members.empty() ? c : c->members[0];
+        (void)hipSetDevice(h->device);
+        if (c->gl_mapped) (void)hipGraphicsUnmapResources(1, &c->gl_res, h->stream);
+        (void)hipGraphicsUnregisterResource(c->gl_res);
+        c->gl_res = nullptr;
+        c->gl_mapped = false;
+    }
     if (!c->members.empty()) {  // device set: its buffers, communicators and members
+        DeviceGuard keep;
         for (size_t r = 0; r < c->members.size(); ++r) {
             vpx_ctx* m = c->members[r];
             (void)hipSetDevice(m->device);
@@ -1656,6 +1679,7 @@ uint32_t vpx_pixel_seed(uint32_t base, uint32_t frame, uint32_t w, uint32_t h, u
 //     accumulator, reset by frame_index 0) and only packed RGB8 (4 B/pixel) travels ->
 //     vpx_composite_rgb8 into the screen.
 static int group_render(vpx_ctx* c, const vpx_frame_params* p, float* accum, uint32_t* rgb8, vpx_stats* stats) {
+    DeviceGuard keep;
     if (!p) return fail(c, VPX_E_INVALID, "null params");
     if (!accum && !rgb8) return fail(c, VPX_E_INVALID, "accum or rgb8 (device pointers on the first device) required");
     const uint32_t n = (uint32_t)c->members.size();
@@ -1685,22 +1709,27 @@ static int group_render(vpx_ctx* c, const vpx_frame_params* p, float* accum, uin
     }
     vpx_ctx* m0 = c->members[0];
     if (stats) std::memset(stats, 0, sizeof(*stats));
+    // stats: every member's counters are read BEFORE any member launches and after the whole
+    // set is done, and each member's render is bracketed by events on its own stream, so
+    // taking stats does not serialise the members (their launches still overlap)
+    std::vector<std::array<unsigned long long, kCtrWords>> before(stats ? n : 0);
+    if (stats)
+        for (uint32_t r = 0; r < n; ++r) {
+            VPX_HIP(c, hipSetDevice(c->members[r]->device));
+            if ((rc = snapshot_counters(c->members[r], before[r].data()))) return fail(c, rc, c->members[r]->err);
+        }
     // 1. every member renders its tiles (launches are asynchronous: the devices overlap)
     for (uint32_t r = 0; r < n; ++r) {
         vpx_ctx* m = c->members[r];
         VPX_HIP(c, hipSetDevice(m->device));
         if (c->comms.empty())  // copy path: the previous frame's copy of this buffer is done
             VPX_HIP(c, hipStreamWaitEvent(m->stream, c->g_copied, 0));
-        vpx_stats one;
-        rc = samples ? vpx_render_tiles(m, p, kTile, kTile, r, n, (float*)c->g_packed[r], stats ? &one : nullptr)
+        if (stats) VPX_HIP(c, hipEventRecord(m->ev0, m->stream));
+        rc = samples ? vpx_render_tiles(m, p, kTile, kTile, r, n, (float*)c->g_packed[r], nullptr)
                      : vpx_render_tiles_accum(m, p, kTile, kTile, r, n, c->g_accum[r], (uint32_t*)c->g_packed[r],
-                                              stats ? &one : nullptr);
+                                              nullptr);
         if (rc) return fail(c, rc, "device " + std::to_string(m->device) + ": " + m->err);
-        if (stats) {
-            stats->primary_rays += one.primary_rays, stats->shadow_rays += one.shadow_rays;
-            stats->bounce_rays += one.bounce_rays, stats->dda_cells += one.dda_cells;
-            stats->kernel_ms = std::max(stats->kernel_ms, one.kernel_ms);
-        }
+        if (stats) VPX_HIP(c, hipEventRecord(m->ev1, m->stream));
         if (c->comms.empty()) VPX_HIP(c, hipEventRecord(c->g_ev[r], m->stream));
     }
     // 2. gather the packed buffers to member 0
@@ -1731,7 +1760,28 @@ static int group_render(vpx_ctx* c, const vpx_frame_params* p, float* accum, uin
     rc = samples ? vpx_composite_tiles(m0, p, kTile, kTile, n, (const float*)dst, accum, rgb8)
                  : vpx_composite_rgb8(m0, p, kTile, kTile, n, (const uint32_t*)dst, rgb8);
     if (rc) return fail(c, rc, m0->err);
-    if (stats) stats->total_ms = stats->kernel_ms;
+    if (stats) {  // kernel_ms: the slowest member's render; total_ms: member 0's start to the composite's end
+        VPX_HIP(c, hipSetDevice(m0->device));
+        VPX_HIP(c, hipEventRecord(m0->ev2, m0->stream));
+        for (uint32_t r = 0; r < n; ++r) {
+            vpx_ctx* m = c->members[r];
+            VPX_HIP(c, hipSetDevice(m->device));
+            unsigned long long after[kCtrWords];
+            if ((rc = snapshot_counters(m, after))) return fail(c, rc, m->err);  // synchronises m's stream
+            vpx_stats one;
+            std::memset(&one, 0, sizeof(one));
+            fill_stats(&one, before[r].data(), after);
+            stats->primary_rays += one.primary_rays, stats->shadow_rays += one.shadow_rays;
+            stats->bounce_rays += one.bounce_rays, stats->dda_cells += one.dda_cells;
+            float ms = 0.f;
+            VPX_HIP(c, hipEventElapsedTime(&ms, m->ev0, m->ev1));
+            stats->kernel_ms = std::max(stats->kernel_ms, ms);
+        }
+        VPX_HIP(c, hipSetDevice(m0->device));
+        float tot = 0.f;
+        VPX_HIP(c, hipEventElapsedTime(&tot, m0->ev0, m0->ev2));
+        stats->total_ms = std::max(tot, stats->kernel_ms);
+    }
     return VPX_OK;
 }
 
@@ -1739,6 +1789,7 @@ int vpx_create_multi(const int* devices, int ndev, vpx_ctx** out) {
     if (!out) return VPX_E_INVALID;
     *out = nullptr;
     if (!devices || ndev < 1 || ndev > 64) return VPX_E_INVALID;
+    DeviceGuard keep;
     vpx_ctx* c = new (std::nothrow) vpx_ctx();
     if (!c) return VPX_E_NOMEM;
     c->device = devices[0];

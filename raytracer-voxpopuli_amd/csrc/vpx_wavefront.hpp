@@ -94,8 +94,6 @@ struct WaveBufs {
     float4* SM;    // [P] pending light: xyz = kd (area), w = bits(kind | discard<<3 | count<<4 | level<<8 | lc<<16)
     uint32_t* smask;  // [P] shadow slots emitted this level (bit s = slot s, s < 15) | light key << 16
     float4* RD;    // [W*H] reprojection: level-0 intersection point, w = material bits (image order)
-    uint8_t* cost; // [P] the path's last primary walk length (iterations, capped): the order of the
-                   // tile's primary walkers in the next frame (VPX_COST_SORT), never a result
     uint32_t P;    // paths (pixels) this call
     uint32_t S;    // shadow slots per path
 };

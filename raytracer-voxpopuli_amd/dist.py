@@ -156,6 +156,9 @@ class ShardedAccumFrame:
         self.host = host_gather
         if not host_gather:
             cur = torch.cuda.current_stream(device).cuda_stream
+            if not cur:  # the library never launches on the null stream (vpx_set_stream(0) = its own)
+                raise ValueError("ShardedAccumFrame: torch's current stream is the default (null) stream; "
+                                 "make a torch.cuda.Stream() current (torch.cuda.set_stream) and render on it")
             if ctx.stream_handle != cur:
                 raise ValueError("ShardedAccumFrame: the vpx context must render on torch's current stream "
                                  "(ctx.set_stream(torch.cuda.current_stream().cuda_stream))")

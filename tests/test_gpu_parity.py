@@ -266,7 +266,19 @@ def test_fused_frame_equals_two_launch_frame(pkg):
     ctx.close()
 
 
-@pytest.mark.parametrize("devices", [[0], [0, 0], [0, 0, 0, 0]])
+def _hip_current_device():
+    import ctypes as C
+    d = C.c_int(-1)
+    assert C.CDLL("libamdhip64.so").hipGetDevice(C.byref(d)) == 0
+    return d.value
+
+
+# [0, 1]: distinct devices take the in-library RCCL path (ncclCommInitAll, grouped
+# ncclSend / ncclRecv into device 0); it runs only where a node has two GPUs (the one-GPU
+# test box skips it and exercises the repeated-device copy path).
+@pytest.mark.parametrize("devices", [[0], [0, 0], [0, 0, 0, 0],
+                                     pytest.param([0, 1], marks=pytest.mark.skipif(
+                                         torch.cuda.device_count() < 2, reason="distinct-device RCCL path needs 2 GPUs"))])
 def test_device_set_equals_single_device(pkg, orc, devices):
     """vpx_create_multi: the frame's tiles dealt over the members, gathered to devices[0]
     and composited there.  With an accumulator (float4 samples travel) the accumulator and
@@ -277,8 +289,11 @@ def test_device_set_equals_single_device(pkg, orc, devices):
     desc = sc.city_scene("monu3", 128, 100, 70, 1, areas=sc.C3_AREAS[:2])
     desc.flags = pkg.abi.VPX_FLAG_AA
     acc_ref, rgb_ref, st_ref = render_gpu(pkg, desc, frames=3)
+    torch.cuda.set_device(0)
     ctx = pkg.context.Context(devices=devices)
     ctx.load_scene(desc)
+    # every forwarded call restores the caller's device (the buffers below belong on devices[0])
+    assert _hip_current_device() == 0
     W, H = desc.width, desc.height
     acc = torch.zeros(W * H * 4, dtype=torch.float32, device="cuda")
     rgb = torch.zeros(W * H, dtype=torch.int32, device="cuda")
@@ -299,6 +314,7 @@ def test_device_set_equals_single_device(pkg, orc, devices):
     assert np.array_equal(rgb2.cpu().numpy().view(np.uint32), rgb_ref)
     tot = ctx.counters()
     assert tot.primary_rays == 6 * W * H
+    assert _hip_current_device() == 0
     ctx.close()
 
 
