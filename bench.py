@@ -125,7 +125,7 @@ class Env:
         return f"tile-shard x{self.n}, accumulator sharded, RCCL gather of RGB8 to rank 0 (overlapped)"
 
 
-def run_config(pkg, env, cfg, steps, warmup, weak=False, sha=None):
+def run_config(pkg, env, cfg, steps, warmup, weak=False, sha=None, pipeline=0):
     """Load `cfg` on this rank, run warmup + `steps` timed steps, return the result dict
     (rank 0; None elsewhere).  Frees the world before returning."""
     desc = pkg.scene.CONFIGS[cfg]()
@@ -135,6 +135,7 @@ def run_config(pkg, env, cfg, steps, warmup, weak=False, sha=None):
     ctx = pkg.context.Context(env.dev)
     ctx.set_stream(env.stream.cuda_stream)
     ctx.load_scene(desc)
+    ctx.set_pipeline(pipeline)
     torch.cuda.synchronize()
     acc = rgb = sharded = None
     if env.n == 1:
@@ -364,6 +365,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip extra_configs / weak_scaling")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--pipeline", type=int, default=int(os.environ.get("VPX_PIPELINE", "0")),
+                    help="frames in flight per GPU (vpx_set_pipeline lanes; 0 = serial frames)")
     args = ap.parse_args()
     if needs_launch(args.gpus):
         # `python bench.py --gpus N` without torchrun: start the N ranks as child processes
@@ -380,17 +383,17 @@ def main():
     pkg = entry.load_package()
     env = Env(args.gpus)
     sha = lib_sha256(pkg)
-    head = run_config(pkg, env, args.config, args.steps, args.warmup, sha=sha)
+    head = run_config(pkg, env, args.config, args.steps, args.warmup, sha=sha, pipeline=args.pipeline)
     extra, weak = {}, None
     if not args.no_extra:
         xs = max(3, args.steps // 4)
         for cfg in EXTRA_CONFIGS:
             if cfg != args.config:
-                r = run_config(pkg, env, cfg, xs, min(args.warmup, 2), sha=sha)
+                r = run_config(pkg, env, cfg, xs, min(args.warmup, 2), sha=sha, pipeline=args.pipeline)
                 if r is not None:
                     extra[cfg] = r
         if env.n > 1:
-            weak = run_config(pkg, env, args.config, xs, min(args.warmup, 2), weak=True, sha=sha)
+            weak = run_config(pkg, env, args.config, xs, min(args.warmup, 2), weak=True, sha=sha, pipeline=args.pipeline)
     if env.rank == 0:
         out = {"metric": METRIC, "value": head["value"], "unit": "Mray/s", "n_gpus": env.n, "steps": args.steps,
                "warmup": args.warmup, "ms_per_step": head["ms_per_step"], "higher_is_better": True,

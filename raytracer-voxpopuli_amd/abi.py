@@ -137,6 +137,7 @@ SIGNATURES = {
     "vpx_abi_version": (C.c_int, []),
     "vpx_set_stream": (C.c_int, [C.c_void_p, C.c_void_p]),
     "vpx_synchronize": (C.c_int, [C.c_void_p]),
+    "vpx_set_pipeline": (C.c_int, [C.c_void_p, C.c_uint32]),
     "vpx_gl_register_buffer": (C.c_int, [C.c_void_p, C.c_uint]),
     "vpx_gl_map": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]),
     "vpx_gl_unmap": (C.c_int, [C.c_void_p]),

@@ -56,6 +56,10 @@ class Context:
     def synchronize(self):
         self._chk(self.lib.vpx_synchronize(self.h), "vpx_synchronize")
 
+    def set_pipeline(self, depth):
+        """Frames in flight (vpx_set_pipeline): 0 / 1 off, 2..4 lanes."""
+        self._chk(self.lib.vpx_set_pipeline(self.h, int(depth)), "vpx_set_pipeline")
+
     # ------------------------------------------------------------------- scene
     def load_scene(self, desc, upload_grids=True):
         if upload_grids:

@@ -45,6 +45,24 @@ __global__ __launch_bounds__(kThreads) void composite_tiles(FrameArgs f, const f
     if (rgb8) rgb8[p] = tonemap_pack(a);
 }
 
+// A rank's packed frame folded into its packed accumulator + RGB8 (the frames-in-flight form
+// of k_finish<kFinishPackedAccum>: the same blend and tonemap of the same sample, in frame order).
+__global__ __launch_bounds__(kThreads) void blend_packed(FrameArgs f, const float4* __restrict__ sample,
+                                                         float4* __restrict__ accum, uint32_t* __restrict__ rgb8, uint32_t P) {
+    const uint32_t p = blockIdx.x * kThreads + threadIdx.x;
+    if (p >= P) return;
+    uint32_t x, y;
+    if (path_pixel(f, p, x, y)) {
+        const float4 s = sample[p];
+        const float4 a = blend(accum[p], mk(s.x, s.y, s.z), f.weight, f.inv_weight);
+        accum[p] = a;
+        rgb8[p] = tonemap_pack(a);
+    } else {
+        accum[p] = make_float4(0.f, 0.f, 0.f, 0.f);
+        rgb8[p] = 0u;
+    }
+}
+
 // Rank-0 scatter of the gathered packed RGB8 tiles (sharded-accumulator flow).
 __global__ __launch_bounds__(kThreads) void composite_rgb8(FrameArgs f, const uint32_t* __restrict__ gathered,
                                                            uint32_t* __restrict__ rgb8) {
@@ -439,13 +457,31 @@ struct vpx_ctx {
     void* d_scratch = nullptr;
     size_t scratch_bytes = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
-    // wavefront path state (vpx_wavefront.hpp), grown on demand
-    void* d_wave = nullptr;
+    // wavefront path state (vpx_wavefront.hpp), grown on demand: one store per stream that
+    // renders (the caller's stream, and each pipeline lane)
+    struct WaveStore {
+        void* d = nullptr;
+        size_t bytes = 0;
+        WaveBufs w{};
+    };
+    WaveStore wave;
+    // frames in flight (vpx_set_pipeline): each lane renders a whole frame on its own library
+    // stream into its own path state and packed sample buffer; the caller's stream only runs
+    // the frames' composites, in frame order (each waits for its lane's render), so frame f+1's
+    // walks fill the GPU while frame f's last tiles drain.  Empty: frames render on the stream.
+    struct Lane {
+        hipStream_t s = nullptr;
+        WaveStore ws;
+        float4* packed = nullptr;  // the lane's frame: one float4 sample per path (tile order)
+        size_t packed_len = 0;
+        hipEvent_t rendered = nullptr, consumed = nullptr;
+        bool used = false;
+    };
+    std::vector<Lane> lanes;
+    uint32_t lane_next = 0;
     // static-camera path images (float4[W*H] each): albedo, illumination, ray data, temp
     float4* rp_buf = nullptr;
     size_t rp_pixels = 0;
-    size_t wave_bytes = 0;
-    WaveBufs wave{};
     // device set (vpx_create_multi): one member context per device; this context only
     // forwards (VPX_GROUP_*) and runs the tile-sharded vpx_render (group_render)
     std::vector<vpx_ctx*> members;
@@ -467,6 +503,17 @@ namespace {
 int fail(vpx_ctx* c, int code, const std::string& msg) {
     if (c) c->err = msg;
     return code;
+}
+
+// Wait for everything the context has queued: its stream and its pipeline lanes (frames in
+// flight read the world, tables and path buffers that later calls may replace).
+hipError_t sync_all(vpx_ctx* c) {
+    for (const auto& l : c->lanes)
+        if (l.s) {
+            const hipError_t e = hipStreamSynchronize(l.s);
+            if (e != hipSuccess) return e;
+        }
+    return hipStreamSynchronize(c->stream);
 }
 
 // The caller's current HIP device, restored when the scope ends: a device-set call sets each
@@ -635,27 +682,27 @@ int validate_frame(vpx_ctx* c, const vpx_frame_params* p) {
 
 // Carve the wavefront buffers for P paths, L levels and S shadow slots out of one
 // device allocation (grown on demand; never inside a capture).
-int ensure_wave(vpx_ctx* c, uint32_t P, uint32_t L, uint32_t S) {
+int ensure_wave(vpx_ctx* c, vpx_ctx::WaveStore& ws, uint32_t P, uint32_t L, uint32_t S) {
     const size_t f4 = sizeof(float4);
     const size_t bytes = (size_t)P * (f4 * (5 + 2 * (size_t)L + 3 * (size_t)S + 1) + 3 * sizeof(uint32_t)) +
                          sizeof(uint32_t) * (size_t)P + 16 * 256;
-    if (bytes > c->wave_bytes) {
-        if (c->d_wave) {
-            VPX_HIP(c, hipStreamSynchronize(c->stream));
-            (void)hipFree(c->d_wave);
+    if (bytes > ws.bytes) {
+        if (ws.d) {
+            VPX_HIP(c, sync_all(c));
+            (void)hipFree(ws.d);
         }
-        c->d_wave = nullptr;
-        c->wave_bytes = 0;
-        VPX_HIP(c, hipMalloc(&c->d_wave, bytes));
-        c->wave_bytes = bytes;
+        ws.d = nullptr;
+        ws.bytes = 0;
+        VPX_HIP(c, hipMalloc(&ws.d, bytes));
+        ws.bytes = bytes;
     }
-    char* q = (char*)c->d_wave;
+    char* q = (char*)ws.d;
     auto take = [&](size_t n) {
         char* r = q;
         q += (n + 255) & ~(size_t)255;
         return (void*)r;
     };
-    WaveBufs& w = c->wave;
+    WaveBufs& w = ws.w;
     w.P = P;
     w.S = S;
     w.O = (float4*)take(f4 * P);
@@ -677,12 +724,12 @@ int ensure_wave(vpx_ctx* c, uint32_t P, uint32_t L, uint32_t S) {
 
 // Profile marks: a stage's start (stage >= 0) or end (-1) event on the stream, while the
 // event pool lasts; a start without room for its end is not recorded.
-static void prof_mark(vpx_ctx* c, int stage) {
+static void prof_mark(vpx_ctx* c, hipStream_t s, int stage) {
     if (!c->prof_cap) return;
     if (stage >= 0 && !((c->prof_mask >> stage) & 1u)) return;  // not selected (its end is dropped too)
     if (stage >= 0 && c->prof_used + 2 > c->prof_cap) return;
     if (stage < 0 && (c->prof_used & 1u) == 0) return;  // its start was dropped
-    if (hipEventRecord(c->prof_ev[c->prof_used], c->stream) != hipSuccess) return;
+    if (hipEventRecord(c->prof_ev[c->prof_used], s) != hipSuccess) return;
     c->prof_stage[c->prof_used] = stage;
     ++c->prof_used;
 }
@@ -695,14 +742,14 @@ struct Reproj {  // the static-camera tail (vpx_render_reproject)
 };
 
 template <int MODE>
-int launch_render(vpx_ctx* c, const SceneView& sv, const FrameArgs& f, uint32_t tiles, float4* accum, uint32_t* rgb8,
-                  float4* packed, const Reproj* rp = nullptr) {
+int launch_render(vpx_ctx* c, hipStream_t s, vpx_ctx::WaveStore& ws, const SceneView& sv, const FrameArgs& f,
+                  uint32_t tiles, float4* accum, uint32_t* rgb8, float4* packed, const Reproj* rp = nullptr) {
     const uint32_t P = tiles * (uint32_t)kTilePix;
     const uint32_t L = (uint32_t)std::max(1, f.max_bounces + 1);
     const uint32_t S = (uint32_t)std::max(1, sv.area_samples);
-    int rc = ensure_wave(c, P, L, S);
+    int rc = ensure_wave(c, ws, P, L, S);
     if (rc) return rc;
-    WaveBufs w = c->wave;
+    WaveBufs w = ws.w;
     if (rp) w.RD = rp->rd;
     const dim3 grid(tiles), block(kThreads);
     const size_t slds = sizeof(uint32_t) * S * kThreads;
@@ -712,71 +759,115 @@ int launch_render(vpx_ctx* c, const SceneView& sv, const FrameArgs& f, uint32_t 
     // on the static-camera path, whose tail is the reprojection
     const bool fuse_tail = !rp;
     if (one && fuse_tail && f.max_bounces == 0 && tiles <= kFuseFrameTiles) {
-        prof_mark(c, VPX_STAGE_FRAME);  // the whole depth-0 frame, one launch (k_frame0)
-        hipLaunchKernelGGL((k_frame0<true, MODE>), grid, block, slds, c->stream, sv, f, w, c->d_ctr, accum, rgb8, packed);
-        prof_mark(c, -1);
+        prof_mark(c, s, VPX_STAGE_FRAME);  // the whole depth-0 frame, one launch (k_frame0)
+        hipLaunchKernelGGL((k_frame0<true, MODE>), grid, block, slds, s, sv, f, w, c->d_ctr, accum, rgb8, packed);
+        prof_mark(c, s, -1);
         VPX_HIP(c, hipGetLastError());
         return VPX_OK;
     }
-    prof_mark(c, VPX_STAGE_PRIMARY);
+    prof_mark(c, s, VPX_STAGE_PRIMARY);
     const bool fuse_head = f.max_bounces >= 0;  // level 0's shade at the end of k_primary
     if (fuse_head)
-        hipLaunchKernelGGL((one ? k_primary<true, true> : k_primary<false, true>), grid, block, 0, c->stream, sv, f, w,
+        hipLaunchKernelGGL((one ? k_primary<true, true> : k_primary<false, true>), grid, block, 0, s, sv, f, w,
                            c->d_ctr);
     else
-        hipLaunchKernelGGL((one ? k_primary<true, false> : k_primary<false, false>), grid, block, 0, c->stream, sv, f,
+        hipLaunchKernelGGL((one ? k_primary<true, false> : k_primary<false, false>), grid, block, 0, s, sv, f,
                            w, c->d_ctr);
-    prof_mark(c, -1);
+    prof_mark(c, s, -1);
     // the last level's shadow -> resolve -> finish as one launch (k_shadow_finish)
     for (int level = 0; level <= f.max_bounces; ++level) {
         if (!(fuse_head && level == 0)) {
-            prof_mark(c, VPX_STAGE_SHADE);
-            hipLaunchKernelGGL(k_shade, grid, block, 0, c->stream, sv, f, w, level, c->d_ctr);
-            prof_mark(c, -1);
+            prof_mark(c, s, VPX_STAGE_SHADE);
+            hipLaunchKernelGGL(k_shade, grid, block, 0, s, sv, f, w, level, c->d_ctr);
+            prof_mark(c, s, -1);
         }
         if (fuse_tail && level == f.max_bounces) {
-            prof_mark(c, VPX_STAGE_SHADOW);
+            prof_mark(c, s, VPX_STAGE_SHADOW);
             hipLaunchKernelGGL((one ? k_shadow_finish<true, MODE> : k_shadow_finish<false, MODE>), grid, block, slds,
-                               c->stream, sv, f, w, c->d_ctr, accum, rgb8, packed);
-            prof_mark(c, -1);
+                               s, sv, f, w, c->d_ctr, accum, rgb8, packed);
+            prof_mark(c, s, -1);
             break;
         }
-        prof_mark(c, VPX_STAGE_SHADOW);
-        hipLaunchKernelGGL(one ? k_shadow_tile<true> : k_shadow_tile<false>, grid, block, slds, c->stream, sv, w, c->d_ctr);
-        prof_mark(c, -1);
-        prof_mark(c, VPX_STAGE_RESOLVE);
-        hipLaunchKernelGGL(k_resolve, grid, block, 0, c->stream, sv, w);
-        prof_mark(c, -1);
+        prof_mark(c, s, VPX_STAGE_SHADOW);
+        hipLaunchKernelGGL(one ? k_shadow_tile<true> : k_shadow_tile<false>, grid, block, slds, s, sv, w, c->d_ctr);
+        prof_mark(c, s, -1);
+        prof_mark(c, s, VPX_STAGE_RESOLVE);
+        hipLaunchKernelGGL(k_resolve, grid, block, 0, s, sv, w);
+        prof_mark(c, s, -1);
         if (level < f.max_bounces) {
-            prof_mark(c, VPX_STAGE_BOUNCE);
-            hipLaunchKernelGGL(one ? k_nearest_tile<true> : k_nearest_tile<false>, grid, block, 0, c->stream, sv, w, c->d_ctr);
-            prof_mark(c, -1);
+            prof_mark(c, s, VPX_STAGE_BOUNCE);
+            hipLaunchKernelGGL(one ? k_nearest_tile<true> : k_nearest_tile<false>, grid, block, 0, s, sv, w, c->d_ctr);
+            prof_mark(c, s, -1);
         }
     }
     // (fused tail: k_shadow_finish already finished the frame; max_bounces = -1 runs no
     // level, so the finish folds the zero leaf here)
     const bool finished = fuse_tail && f.max_bounces >= 0;
-    if (!finished) prof_mark(c, VPX_STAGE_FINISH);
+    if (!finished) prof_mark(c, s, VPX_STAGE_FINISH);
     if (!rp) {
-        if (!finished) hipLaunchKernelGGL((k_finish<MODE>), grid, block, 0, c->stream, f, w, accum, rgb8, packed);
+        if (!finished) hipLaunchKernelGGL((k_finish<MODE>), grid, block, 0, s, f, w, accum, rgb8, packed);
     } else {  // Renderer::Tick static branch, second pass (renderer.cpp:2024-2100)
-        hipLaunchKernelGGL(k_finish_reproject, grid, block, 0, c->stream, f, w, rp->alb, rp->ill);
-        hipLaunchKernelGGL(k_reproject_setup, grid, block, 0, c->stream, f, w, rp->prev);
-        hipLaunchKernelGGL(one ? k_shadow_tile<true> : k_shadow_tile<false>, grid, block, slds, c->stream, sv, w, c->d_ctr);
-        hipLaunchKernelGGL(k_reproject_resolve, grid, block, 0, c->stream, f, w, rp->alb, rp->ill, rp->hist, rp->temp,
+        hipLaunchKernelGGL(k_finish_reproject, grid, block, 0, s, f, w, rp->alb, rp->ill);
+        hipLaunchKernelGGL(k_reproject_setup, grid, block, 0, s, f, w, rp->prev);
+        hipLaunchKernelGGL(one ? k_shadow_tile<true> : k_shadow_tile<false>, grid, block, slds, s, sv, w, c->d_ctr);
+        hipLaunchKernelGGL(k_reproject_resolve, grid, block, 0, s, f, w, rp->alb, rp->ill, rp->hist, rp->temp,
                            rgb8);
         VPX_HIP(c, hipMemcpyAsync(rp->hist, rp->temp, sizeof(float4) * (size_t)f.width * f.height,
-                                  hipMemcpyDeviceToDevice, c->stream));  // history = temp
+                                  hipMemcpyDeviceToDevice, s));  // history = temp
     }
-    if (!finished) prof_mark(c, -1);
+    if (!finished) prof_mark(c, s, -1);
     VPX_HIP(c, hipGetLastError());
     return VPX_OK;
+}
+
+// Frames in flight: render `tiles` tiles of frame f as packed float4 samples (into `out`, or
+// the lane's own buffer when null) on the next lane's stream, in that lane's path state; the
+// caller's stream waits for the render.  The caller then queues the frame's composite on
+// s and records the lane's `consumed` event after it.
+int lane_render(vpx_ctx* c, const SceneView& sv, const FrameArgs& f, uint32_t tiles, float4* out, vpx_ctx::Lane*& lane) {
+    vpx_ctx::Lane& L = c->lanes[c->lane_next];
+    c->lane_next = (c->lane_next + 1u) % (uint32_t)c->lanes.size();
+    float4* dst = out;
+    if (!dst) {
+        const size_t need = (size_t)tiles * kTilePix;
+        if (L.packed_len < need) {
+            VPX_HIP(c, sync_all(c));
+            if (L.packed) (void)hipFree(L.packed);
+            L.packed = nullptr;
+            L.packed_len = 0;
+            VPX_HIP(c, hipMalloc(&L.packed, sizeof(float4) * need));
+            L.packed_len = need;
+        }
+        dst = L.packed;
+    }
+    // the lane's samples / path state are reused: the composite of its previous frame is done
+    if (L.used) VPX_HIP(c, hipStreamWaitEvent(L.s, L.consumed, 0));
+    int rc = launch_render<kFinishPackedSample>(c, L.s, L.ws, sv, f, tiles, nullptr, nullptr, dst);
+    if (rc) return rc;
+    VPX_HIP(c, hipEventRecord(L.rendered, L.s));
+    VPX_HIP(c, hipStreamWaitEvent(c->stream, L.rendered, 0));
+    L.used = true;
+    lane = &L;
+    return VPX_OK;
+}
+
+void free_lanes(vpx_ctx* c) {
+    for (auto& L : c->lanes) {
+        if (L.s) (void)hipStreamSynchronize(L.s);
+        if (L.ws.d) (void)hipFree(L.ws.d);
+        if (L.packed) (void)hipFree(L.packed);
+        if (L.rendered) (void)hipEventDestroy(L.rendered);
+        if (L.consumed) (void)hipEventDestroy(L.consumed);
+        if (L.s) (void)hipStreamDestroy(L.s);
+    }
+    c->lanes.clear();
+    c->lane_next = 0;
 }
 
 int snapshot_counters(vpx_ctx* c, unsigned long long out[kCtrWords]) {
     unsigned long long all[kCtrWords * kCtrStripes];
     VPX_HIP(c, hipMemcpyAsync(all, c->d_ctr, sizeof(all), hipMemcpyDeviceToHost, c->stream));
-    VPX_HIP(c, hipStreamSynchronize(c->stream));
+    VPX_HIP(c, sync_all(c));
     for (uint32_t i = 0; i < kCtrWords; ++i) {
         out[i] = 0;
         for (uint32_t s = 0; s < kCtrStripes; ++s) out[i] += all[kCtrWords * s + i];
@@ -853,7 +944,8 @@ int vpx_destroy(vpx_ctx* c) {
         return VPX_OK;
     }
     (void)hipSetDevice(c->device);
-    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->stream) (void)sync_all(c);
+    free_lanes(c);
     for (auto& g : c->grids) {
         if (g.ptr) (void)hipFree(g.ptr);
         if (g.l1) (void)hipFree(g.l1);
@@ -861,7 +953,7 @@ int vpx_destroy(vpx_ctx* c) {
         if (g.dfp) (void)hipFree(g.dfp);
     }
     void* ptrs[] = {c->d_grids, c->d_volumes, c->d_vbounds, c->d_tlas, c->d_bvh, c->d_materials, c->d_points, c->d_spots, c->d_areas,
-                    c->d_spheres, c->d_triangles, c->d_ctr, c->d_sum, c->d_scratch, c->d_wave, c->d_sky};
+                    c->d_spheres, c->d_triangles, c->d_ctr, c->d_sum, c->d_scratch, c->wave.d, c->d_sky};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (hipEvent_t e : c->prof_ev) (void)hipEventDestroy(e);
@@ -880,6 +972,26 @@ int vpx_set_stream(vpx_ctx* c, void* s) {
     if (!c) return VPX_E_INVALID;
     if (!c->members.empty()) return vpx_set_stream(c->members[0], s);  // a stream of the first device
     c->stream = s ? (hipStream_t)s : c->own_stream;
+    return VPX_OK;
+}
+
+int vpx_set_pipeline(vpx_ctx* c, uint32_t depth) {
+    VPX_GROUP_ALL(c, vpx_set_pipeline(m_, depth));
+    if (!c) return VPX_E_INVALID;
+    if (depth > 4) return fail(c, VPX_E_INVALID, "pipeline depth must be in [0, 4]");
+    VPX_HIP(c, hipSetDevice(c->device));
+    VPX_HIP(c, sync_all(c));
+    free_lanes(c);
+    if (depth < 2) return VPX_OK;
+    c->lanes.resize(depth);
+    for (auto& L : c->lanes) {
+        if (hipStreamCreateWithFlags(&L.s, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&L.rendered, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&L.consumed, hipEventDisableTiming) != hipSuccess) {
+            free_lanes(c);
+            return fail(c, VPX_E_DEVICE, "pipeline lane stream / events");
+        }
+    }
     return VPX_OK;
 }
 
@@ -943,7 +1055,7 @@ int vpx_gl_unmap(vpx_ctx* c) {
 int vpx_synchronize(vpx_ctx* c) {
     VPX_GROUP_ALL(c, vpx_synchronize(m_));
     if (!c) return VPX_E_INVALID;
-    VPX_HIP(c, hipStreamSynchronize(c->stream));
+    VPX_HIP(c, sync_all(c));
     return VPX_OK;
 }
 
@@ -955,7 +1067,7 @@ static int alloc_grid(vpx_ctx* c, uint32_t id, uint32_t n) {
     auto& g = c->grids[id];
     const size_t bytes = (size_t)n * n * n;
     if (g.ptr && g.n != n) {
-        VPX_HIP(c, hipStreamSynchronize(c->stream));
+        VPX_HIP(c, sync_all(c));
         (void)hipFree(g.ptr);
         (void)hipFree(g.l1);
         (void)hipFree(g.l2);
@@ -998,7 +1110,7 @@ static int build_masks(vpx_ctx* c, uint32_t id) {
     hipLaunchKernelGGL(build_up_k, dim3(512), dim3(256), 0, c->stream, g.l1, g.nb2, g.nb3, g.l2);
     VPX_HIP(c, hipGetLastError());
     if (int r = build_df(c, g)) return r;
-    VPX_HIP(c, hipStreamSynchronize(c->stream));
+    VPX_HIP(c, sync_all(c));
     return VPX_OK;
 }
 
@@ -1023,7 +1135,7 @@ static int build_masks_box(vpx_ctx* c, uint32_t id, uint32_t x0, uint32_t y0, ui
                        hi[2] - lo[2] + 1);
     VPX_HIP(c, hipGetLastError());
     if (int r = build_df(c, g)) return r;
-    VPX_HIP(c, hipStreamSynchronize(c->stream));
+    VPX_HIP(c, sync_all(c));
     return VPX_OK;
 }
 
@@ -1032,6 +1144,7 @@ int vpx_grid_fill(vpx_ctx* c, uint32_t id, uint8_t value) {
     if (!c) return VPX_E_INVALID;
     if (id >= c->grids.size() || !c->grids[id].ptr) return fail(c, VPX_E_INVALID, "unknown grid");
     auto& g = c->grids[id];
+    VPX_HIP(c, sync_all(c));  // frames in flight still read the grid
     VPX_HIP(c, hipMemsetAsync(g.ptr, value, (size_t)g.n * g.n * g.n, c->stream));
     return build_masks(c, id);
 }
@@ -1047,6 +1160,7 @@ int vpx_grid_write_box(vpx_ctx* c, uint32_t id, const uint8_t* src, uint32_t x0,
     const size_t bytes = (size_t)dx * dy * dz;
     if (!bytes) return VPX_OK;
     uint8_t* d = nullptr;
+    VPX_HIP(c, sync_all(c));  // frames in flight still read the grid
     VPX_HIP(c, hipMalloc(&d, bytes));
     if (hipMemcpyAsync(d, src, bytes, hipMemcpyHostToDevice, c->stream) != hipSuccess) {
         (void)hipFree(d);
@@ -1054,7 +1168,7 @@ int vpx_grid_write_box(vpx_ctx* c, uint32_t id, const uint8_t* src, uint32_t x0,
     }
     hipLaunchKernelGGL(write_box_k, dim3((unsigned)std::min<size_t>(4096, (bytes + 255) / 256)), dim3(256), 0, c->stream,
                        g.ptr, g.n, d, x0, y0, z0, dx, dy, dz);
-    const hipError_t e = hipStreamSynchronize(c->stream);
+    const hipError_t e = sync_all(c);
     (void)hipFree(d);
     if (e != hipSuccess) return fail(c, VPX_E_DEVICE, hipGetErrorString(e));
     return build_masks_box(c, id, x0, y0, z0, x0 + dx, y0 + dy, z0 + dz);
@@ -1072,6 +1186,7 @@ int vpx_grid_emissive_sphere(vpx_ctx* c, uint32_t id, uint8_t mat, float radius)
     const int64_t b = std::min<int64_t>((int64_t)g.n - 1, (int64_t)std::ceil(cc + r) + 1);
     if (b < a) return VPX_OK;
     const uint32_t x0 = (uint32_t)a, cnt = (uint32_t)(b - a + 1);
+    VPX_HIP(c, sync_all(c));  // frames in flight still read the grid
     hipLaunchKernelGGL(emissive_sphere_k, dim3((unsigned)std::min<uint64_t>(4096, ((uint64_t)cnt * cnt * cnt + 255) / 256)),
                        dim3(256), 0, c->stream, g.ptr, g.n, mat, radius, x0, cnt);
     VPX_HIP(c, hipGetLastError());
@@ -1081,6 +1196,7 @@ int vpx_grid_emissive_sphere(vpx_ctx* c, uint32_t id, uint8_t mat, float radius)
 int vpx_upload_grid(vpx_ctx* c, uint32_t id, const uint8_t* cells, uint32_t n) {
     VPX_GROUP_ALL(c, vpx_upload_grid(m_, id, cells, n));
     if (!c || !cells) return fail(c, VPX_E_INVALID, "null argument");
+    VPX_HIP(c, sync_all(c));  // frames in flight still read the grid
     int rc = alloc_grid(c, id, n);
     if (rc) return rc;
     VPX_HIP(c, hipMemcpy(c->grids[id].ptr, cells, (size_t)n * n * n, hipMemcpyHostToDevice));
@@ -1092,6 +1208,7 @@ int vpx_generate_tiled_grid(vpx_ctx* c, uint32_t id, uint32_t n, const uint8_t* 
     VPX_GROUP_ALL(c, vpx_generate_tiled_grid(m_, id, n, model, mx, my, mz, px, py, pz, ground));
     if (!c || !model) return fail(c, VPX_E_INVALID, "null argument");
     if (!mx || !my || !mz || !px || !py || !pz) return fail(c, VPX_E_INVALID, "zero model size or period");
+    VPX_HIP(c, sync_all(c));  // frames in flight still read the grid
     int rc = alloc_grid(c, id, n);
     if (rc) return rc;
     const size_t mbytes = (size_t)mx * my * mz;
@@ -1101,7 +1218,7 @@ int vpx_generate_tiled_grid(vpx_ctx* c, uint32_t id, uint32_t n, const uint8_t* 
     hipLaunchKernelGGL(tiled_world_k, dim3(4096), dim3(256), 0, c->stream, c->grids[id].ptr, n, dm, mx, my, mz, px,
                        py, pz, ground);
     VPX_HIP(c, hipGetLastError());
-    VPX_HIP(c, hipStreamSynchronize(c->stream));
+    VPX_HIP(c, sync_all(c));
     (void)hipFree(dm);
     return build_masks(c, id);
 }
@@ -1116,7 +1233,7 @@ int vpx_grid_checksum(vpx_ctx* c, uint32_t id, uint64_t* out) {
     VPX_HIP(c, hipGetLastError());
     unsigned long long h = 0;
     VPX_HIP(c, hipMemcpyAsync(&h, c->d_sum, sizeof(h), hipMemcpyDeviceToHost, c->stream));
-    VPX_HIP(c, hipStreamSynchronize(c->stream));
+    VPX_HIP(c, sync_all(c));
     *out = (uint64_t)h;
     return VPX_OK;
 }
@@ -1247,7 +1364,7 @@ int vpx_set_volumes(vpx_ctx* c, const vpx_volume* v, uint32_t count) {
     VPX_GROUP_ALL(c, vpx_set_volumes(m_, v, count));
     if (!c || (!v && count)) return fail(c, VPX_E_INVALID, "null argument");
     if (count > 65536) return fail(c, VPX_E_INVALID, "too many volumes");
-    VPX_HIP(c, hipStreamSynchronize(c->stream));
+    VPX_HIP(c, sync_all(c));
     if (count > c->d_volumes_cap) {
         if (c->d_volumes) (void)hipFree(c->d_volumes);
         if (c->d_vbounds) (void)hipFree(c->d_vbounds);
@@ -1275,10 +1392,10 @@ int vpx_set_materials(vpx_ctx* c, const vpx_material* m, uint32_t count) {
     // entries past `count` behave like MaterialSetUp's padding: white, roughness 1
     for (auto& e : full) e = vpx_material{{1, 1, 1}, 1.0f, 0.0f, 1.5f, {0, 0}};
     std::memcpy(full, m, sizeof(vpx_material) * count);
-    VPX_HIP(c, hipStreamSynchronize(c->stream));
+    VPX_HIP(c, sync_all(c));
     int rc = upload_table(c, c->d_materials, full, VPX_NUM_MATERIALS);
     if (rc) return rc;
-    VPX_HIP(c, hipStreamSynchronize(c->stream));
+    VPX_HIP(c, sync_all(c));
     c->have_materials = true;
     return VPX_OK;
 }
@@ -1287,12 +1404,12 @@ int vpx_set_lights(vpx_ctx* c, const vpx_point_light* p, uint32_t np, const vpx_
                    const vpx_area_light* a, uint32_t na, const vpx_dir_light* d) {
     VPX_GROUP_ALL(c, vpx_set_lights(m_, p, np, s, ns, a, na, d));
     if (!c) return VPX_E_INVALID;
-    VPX_HIP(c, hipStreamSynchronize(c->stream));
+    VPX_HIP(c, sync_all(c));
     int rc;
     if ((rc = upload_table(c, c->d_points, p, np))) return rc;
     if ((rc = upload_table(c, c->d_spots, s, ns))) return rc;
     if ((rc = upload_table(c, c->d_areas, a, na))) return rc;
-    VPX_HIP(c, hipStreamSynchronize(c->stream));
+    VPX_HIP(c, sync_all(c));
     c->n_points = np, c->n_spots = ns, c->n_areas = na;
     if (d) c->dir = *d;
     return VPX_OK;
@@ -1301,11 +1418,11 @@ int vpx_set_lights(vpx_ctx* c, const vpx_point_light* p, uint32_t np, const vpx_
 int vpx_set_shapes(vpx_ctx* c, const vpx_sphere* s, uint32_t ns, const vpx_triangle* t, uint32_t nt) {
     VPX_GROUP_ALL(c, vpx_set_shapes(m_, s, ns, t, nt));
     if (!c) return VPX_E_INVALID;
-    VPX_HIP(c, hipStreamSynchronize(c->stream));
+    VPX_HIP(c, sync_all(c));
     int rc;
     if ((rc = upload_table(c, c->d_spheres, s, ns))) return rc;
     if ((rc = upload_table(c, c->d_triangles, t, nt))) return rc;
-    VPX_HIP(c, hipStreamSynchronize(c->stream));
+    VPX_HIP(c, sync_all(c));
     c->n_spheres = ns, c->n_triangles = nt;
     return VPX_OK;
 }
@@ -1316,7 +1433,7 @@ int vpx_set_sky(vpx_ctx* c, const float* rgb, uint32_t width, uint32_t height, f
     VPX_HIP(c, hipSetDevice(c->device));
     if (!rgb || !width || !height) {  // remove the texture (misses use the constant sky)
         if (c->d_sky) {
-            VPX_HIP(c, hipStreamSynchronize(c->stream));
+            VPX_HIP(c, sync_all(c));
             (void)hipFree(c->d_sky);
         }
         c->d_sky = nullptr;
@@ -1326,14 +1443,15 @@ int vpx_set_sky(vpx_ctx* c, const float* rgb, uint32_t width, uint32_t height, f
     if ((uint64_t)width * height > (1ull << 28)) return fail(c, VPX_E_INVALID, "sky texture too large");
     const size_t bytes = sizeof(float) * 3 * (size_t)width * height;
     if ((size_t)c->sky_w * c->sky_h != (size_t)width * height) {
-        VPX_HIP(c, hipStreamSynchronize(c->stream));
+        VPX_HIP(c, sync_all(c));
         if (c->d_sky) (void)hipFree(c->d_sky);
         c->d_sky = nullptr;
         c->sky_w = c->sky_h = 0;
         VPX_HIP(c, hipMalloc(&c->d_sky, bytes));
     }
+    VPX_HIP(c, sync_all(c));  // frames in flight still read the texture
     VPX_HIP(c, hipMemcpyAsync(c->d_sky, rgb, bytes, hipMemcpyHostToDevice, c->stream));
-    VPX_HIP(c, hipStreamSynchronize(c->stream));
+    VPX_HIP(c, sync_all(c));
     c->sky_w = width, c->sky_h = height;
     c->sky_hdr = hdr_contribution;
     return VPX_OK;
@@ -1356,12 +1474,25 @@ int vpx_render(vpx_ctx* c, const vpx_frame_params* p, float* accum, uint32_t* rg
     if (rc) return rc;
     if (!accum) return fail(c, VPX_E_INVALID, "accum (device float4[W*H]) is required");
     VPX_HIP(c, hipSetDevice(c->device));
-    unsigned long long before[kCtrWords] = {};
-    if (stats && (rc = snapshot_counters(c, before))) return rc;
     const SceneView sv = view_of(c, p->sky, p->area_samples, (p->flags & VPX_FLAG_SKY) != 0);
     const FrameArgs f = frame_of(c, p, 0, 1);
+    if (!c->lanes.empty() && !stats && !(p->flags & VPX_FLAG_NO_TONEMAP)) {
+        // frames in flight: the frame renders on a lane; its accumulate / tonemap runs on the
+        // caller's stream after the previous frame's (the same blend of the same sample)
+        vpx_ctx::Lane* L = nullptr;
+        if ((rc = lane_render(c, sv, f, f.num_tiles, nullptr, L))) return rc;
+        hipLaunchKernelGGL(composite_tiles, dim3(f.num_tiles), dim3(kThreads), 0, c->stream, f, L->packed,
+                           reinterpret_cast<float4*>(accum), rgb8);
+        VPX_HIP(c, hipGetLastError());
+        VPX_HIP(c, hipEventRecord(L->consumed, c->stream));
+        return VPX_OK;
+    }
+    unsigned long long before[kCtrWords] = {};
+    if (stats && (rc = snapshot_counters(c, before))) return rc;
     if (stats) VPX_HIP(c, hipEventRecord(c->ev0, c->stream));
-    if ((rc = launch_render<kFinishImage>(c, sv, f, f.num_tiles, reinterpret_cast<float4*>(accum), rgb8, nullptr))) return rc;
+    if ((rc = launch_render<kFinishImage>(c, c->stream, c->wave, sv, f, f.num_tiles, reinterpret_cast<float4*>(accum), rgb8,
+                                          nullptr)))
+        return rc;
     if (stats) {
         VPX_HIP(c, hipEventRecord(c->ev1, c->stream));
         unsigned long long after[kCtrWords];
@@ -1386,7 +1517,7 @@ int vpx_render_reproject(vpx_ctx* c, const vpx_frame_params* p, const vpx_prev_c
     VPX_HIP(c, hipSetDevice(c->device));
     const size_t pix = (size_t)p->width * p->height;
     if (pix > c->rp_pixels) {
-        VPX_HIP(c, hipStreamSynchronize(c->stream));
+        VPX_HIP(c, sync_all(c));
         if (c->rp_buf) (void)hipFree(c->rp_buf);
         c->rp_buf = nullptr;
         c->rp_pixels = 0;
@@ -1405,7 +1536,7 @@ int vpx_render_reproject(vpx_ctx* c, const vpx_frame_params* p, const vpx_prev_c
     FrameArgs f = frame_of(c, p, 0, 1);
     f.flags = (f.flags & ~(VPX_FLAG_AA | VPX_FLAG_DOF)) | kFlagReproject;  // GetPrimaryRayNoDOF
     if (stats) VPX_HIP(c, hipEventRecord(c->ev0, c->stream));
-    if ((rc = launch_render<kFinishImage>(c, sv, f, f.num_tiles, nullptr, rgb8, nullptr, &rp))) return rc;
+    if ((rc = launch_render<kFinishImage>(c, c->stream, c->wave, sv, f, f.num_tiles, nullptr, rgb8, nullptr, &rp))) return rc;
     if (stats) {
         VPX_HIP(c, hipEventRecord(c->ev1, c->stream));
         unsigned long long after[kCtrWords];
@@ -1439,13 +1570,26 @@ static int render_tiles_impl(int MODE, vpx_ctx* c, const vpx_frame_params* p, ui
     if (MODE == kFinishPackedSample ? !packed : (!accum || !rgb8))
         return fail(c, VPX_E_INVALID, "null packed buffer");
     VPX_HIP(c, hipSetDevice(c->device));
-    unsigned long long before[kCtrWords] = {};
-    if (stats && (rc = snapshot_counters(c, before))) return rc;
     const SceneView sv = view_of(c, p->sky, p->area_samples, (p->flags & VPX_FLAG_SKY) != 0);
     const FrameArgs f = frame_of(c, p, rank, n_ranks);
+    if (!c->lanes.empty() && !stats) {  // frames in flight (vpx_set_pipeline)
+        vpx_ctx::Lane* L = nullptr;
+        if ((rc = lane_render(c, sv, f, f.tiles_per_rank, MODE == kFinishPackedSample ? packed : nullptr, L))) return rc;
+        if (MODE == kFinishPackedAccum) {  // this rank's running average, in frame order on the caller's stream
+            const uint32_t P = f.tiles_per_rank * (uint32_t)kTilePix;
+            hipLaunchKernelGGL(blend_packed, dim3(f.tiles_per_rank), dim3(kThreads), 0, c->stream, f, L->packed, accum,
+                               rgb8, P);
+            VPX_HIP(c, hipGetLastError());
+        }
+        VPX_HIP(c, hipEventRecord(L->consumed, c->stream));
+        return VPX_OK;
+    }
+    unsigned long long before[kCtrWords] = {};
+    if (stats && (rc = snapshot_counters(c, before))) return rc;
     if (stats) VPX_HIP(c, hipEventRecord(c->ev0, c->stream));
-    rc = MODE == kFinishPackedSample ? launch_render<kFinishPackedSample>(c, sv, f, f.tiles_per_rank, accum, rgb8, packed)
-                                     : launch_render<kFinishPackedAccum>(c, sv, f, f.tiles_per_rank, accum, rgb8, packed);
+    rc = MODE == kFinishPackedSample
+             ? launch_render<kFinishPackedSample>(c, c->stream, c->wave, sv, f, f.tiles_per_rank, accum, rgb8, packed)
+             : launch_render<kFinishPackedAccum>(c, c->stream, c->wave, sv, f, f.tiles_per_rank, accum, rgb8, packed);
     if (rc) return rc;
     if (stats) {
         VPX_HIP(c, hipEventRecord(c->ev1, c->stream));
@@ -1522,7 +1666,7 @@ int vpx_get_counters(vpx_ctx* c, vpx_stats* out, int reset) {
     fill_stats(out, zero, now);
     if (reset) {
         VPX_HIP(c, hipMemsetAsync(c->d_ctr, 0, kCtrWords * kCtrStripes * sizeof(unsigned long long), c->stream));
-        VPX_HIP(c, hipStreamSynchronize(c->stream));
+        VPX_HIP(c, sync_all(c));
     }
     return VPX_OK;
 }
@@ -1542,7 +1686,7 @@ int vpx_find_nearest(vpx_ctx* c, const vpx_ray* rays, uint32_t n, vpx_hit* hits)
     hipLaunchKernelGGL(find_nearest_k, dim3((n + 255) / 256), dim3(256), 0, c->stream, view_of(c, sky, 3), dr, n, dh);
     VPX_HIP(c, hipGetLastError());
     VPX_HIP(c, hipMemcpyAsync(hits, dh, hb, hipMemcpyDeviceToHost, c->stream));
-    VPX_HIP(c, hipStreamSynchronize(c->stream));
+    VPX_HIP(c, sync_all(c));
     return VPX_OK;
 }
 
@@ -1561,7 +1705,7 @@ int vpx_is_occluded(vpx_ctx* c, const vpx_ray* rays, uint32_t n, uint8_t* occ) {
     hipLaunchKernelGGL(is_occluded_k, dim3((n + 255) / 256), dim3(256), 0, c->stream, view_of(c, sky, 3), dr, n, doc);
     VPX_HIP(c, hipGetLastError());
     VPX_HIP(c, hipMemcpyAsync(occ, doc, n, hipMemcpyDeviceToHost, c->stream));
-    VPX_HIP(c, hipStreamSynchronize(c->stream));
+    VPX_HIP(c, sync_all(c));
     return VPX_OK;
 }
 
@@ -1592,7 +1736,7 @@ int vpx_trace(vpx_ctx* c, const vpx_ray* rays, const uint32_t* seeds, uint32_t n
         hipLaunchKernelGGL(trace_k<kMaxLevels>, g, b, 0, c->stream, sv, dr, ds, n, depth, dout);
     VPX_HIP(c, hipGetLastError());
     VPX_HIP(c, hipMemcpyAsync(radiance, dout, ob, hipMemcpyDeviceToHost, c->stream));
-    VPX_HIP(c, hipStreamSynchronize(c->stream));
+    VPX_HIP(c, sync_all(c));
     return VPX_OK;
 }
 
@@ -1600,7 +1744,7 @@ int vpx_bvh_set(vpx_ctx* c, const vpx_bvh_tri* tris, uint32_t n) {
     VPX_GROUP_ALL(c, vpx_bvh_set(m_, tris, n));
     if (!c || (n && !tris)) return fail(c, VPX_E_INVALID, "null argument");
     if (n > VPX_BVH_MAX_TRIS) return fail(c, VPX_E_INVALID, "more triangles than VPX_BVH_MAX_TRIS");
-    VPX_HIP(c, hipStreamSynchronize(c->stream));
+    VPX_HIP(c, sync_all(c));
     if (c->d_bvh) (void)hipFree(c->d_bvh);
     c->d_bvh = nullptr;
     c->bvh_nodes = c->bvh_tris = 0;
@@ -1639,7 +1783,7 @@ int vpx_bvh_intersect(vpx_ctx* c, const vpx_ray* rays, uint32_t n, float* t_out)
                        c->bvh_nodes, c->bvh_tris, dr, n, dt);
     VPX_HIP(c, hipGetLastError());
     VPX_HIP(c, hipMemcpyAsync(t_out, dt, tb, hipMemcpyDeviceToHost, c->stream));
-    VPX_HIP(c, hipStreamSynchronize(c->stream));
+    VPX_HIP(c, sync_all(c));
     return VPX_OK;
 }
 
@@ -1657,7 +1801,7 @@ int vpx_focus_distance(vpx_ctx* c, uint32_t width, uint32_t height, float* fd) {
                        (float*)c->d_scratch);
     VPX_HIP(c, hipGetLastError());
     VPX_HIP(c, hipMemcpyAsync(fd, c->d_scratch, sizeof(float), hipMemcpyDeviceToHost, c->stream));
-    VPX_HIP(c, hipStreamSynchronize(c->stream));
+    VPX_HIP(c, sync_all(c));
     return VPX_OK;
 }
 
@@ -1840,7 +1984,7 @@ extern "C" int vpx_profile_select(vpx_ctx* c, uint32_t stage_mask) {
 extern "C" int vpx_profile_enable(vpx_ctx* c, uint32_t max_launches) {
     VPX_GROUP_FIRST(c, vpx_profile_enable(m_, max_launches));
     if (!c) return VPX_E_INVALID;
-    VPX_HIP(c, hipStreamSynchronize(c->stream));
+    VPX_HIP(c, sync_all(c));
     for (hipEvent_t e : c->prof_ev) (void)hipEventDestroy(e);
     c->prof_ev.clear();
     c->prof_stage.clear();

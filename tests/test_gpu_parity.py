@@ -841,3 +841,79 @@ def test_frame_beyond_path_index_range_is_refused(pkg):
     with pytest.raises(pkg.abi.VpxError, match="2\\^27"):
         ctx.render(desc.with_size(16384, 8208).frame_params(0), acc.data_ptr())
     ctx.close()
+
+
+@pytest.mark.parametrize("lanes", [2, 3])
+@pytest.mark.parametrize("depth", [0, 2])
+def test_frames_in_flight_equal_serial_frames(pkg, lanes, depth):
+    """vpx_set_pipeline: frames rendered on `lanes` library streams with only their
+    accumulate / tonemap on the context's stream give the serial frames' accumulator and
+    screen bit for bit (AA jitter, 5 frames, point + area lights at depth 2), counters
+    included; a world edit between frames is seen by exactly the frames after it."""
+    sc = pkg.scene
+    desc = sc.city_scene("monu3", 128, 96, 80, depth, areas=sc.C3_AREAS[:1] if depth else ())
+    desc.flags = pkg.abi.VPX_FLAG_AA
+    W, H = desc.width, desc.height
+    box = np.full((6, 6, 6), 1, np.uint8)  # NON_METAL_RED cells
+
+    def run(pipe):
+        ctx = pkg.context.Context(0)
+        s = torch.cuda.Stream()
+        ctx.set_stream(s.cuda_stream)
+        ctx.load_scene(desc)
+        ctx.set_pipeline(pipe)
+        acc = torch.zeros(W * H * 4, dtype=torch.float32, device="cuda")
+        rgb = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+        torch.cuda.synchronize()
+        ctx.counters(reset=True)
+        shots = []
+        with torch.cuda.stream(s):
+            for f in range(5):
+                if f == 3:  # a prop edit (LoadModelPartial) between frames
+                    ctx.lib.vpx_grid_write_box(ctx.h, 0, box.ctypes.data_as(C.c_void_p), 60, 40, 60, 6, 6, 6)
+                ctx.render(desc.frame_params(f), acc.data_ptr(), rgb.data_ptr())
+                shots.append(rgb.clone())
+        ctx.synchronize()
+        st = ctx.counters()
+        out = (bits(acc.cpu().numpy().reshape(-1, 4)), [x.cpu().numpy() for x in shots], st)
+        ctx.close()
+        return out
+
+    a0, s0, t0 = run(0)
+    a1, s1, t1 = run(lanes)
+    assert np.array_equal(a0, a1)
+    for x, y in zip(s0, s1):
+        assert np.array_equal(x, y)
+    assert (t0.primary_rays, t0.shadow_rays, t0.bounce_rays, t0.dda_cells) == (
+        t1.primary_rays, t1.shadow_rays, t1.bounce_rays, t1.dda_cells)
+
+
+@pytest.mark.parametrize("lanes", [2, 4])
+def test_frames_in_flight_sharded_accumulator(pkg, lanes):
+    """vpx_render_tiles_accum with lanes: a rank's packed running average and RGB8 over 4
+    frames equal the serial calls' bit for bit (2 ranks on one device)."""
+    sc = pkg.scene
+    desc = sc.city_scene("monu3", 128, 100, 70, 1)
+    desc.flags = pkg.abi.VPX_FLAG_AA
+    W, H, R = desc.width, desc.height, 2
+
+    def run(pipe):
+        ctx = pkg.context.Context(0)
+        s = torch.cuda.Stream()
+        ctx.set_stream(s.cuda_stream)
+        ctx.load_scene(desc)
+        ctx.set_pipeline(pipe)
+        L = ctx.packed_len(W, H, R)
+        accs = [torch.zeros(L * 4, dtype=torch.float32, device="cuda") for _ in range(R)]
+        rgbs = [torch.zeros(L, dtype=torch.int32, device="cuda") for _ in range(R)]
+        torch.cuda.synchronize()
+        for f in range(4):
+            for r in range(R):
+                ctx.render_tiles_accum(desc.frame_params(f), r, R, accs[r].data_ptr(), rgbs[r].data_ptr())
+        ctx.synchronize()
+        out = [bits(a.cpu().numpy()) for a in accs] + [g.cpu().numpy() for g in rgbs]
+        ctx.close()
+        return out
+
+    for x, y in zip(run(0), run(lanes)):
+        assert np.array_equal(x, y)

@@ -1,6 +1,7 @@
 """One rank's GPU time in the N-GPU strong-scaling run, measured on one GPU: rank 0's share
 of a config's frame (vpx_render_tiles_accum, rank 0 of R) for R = 1, 2, 4, 8 — the render
-part of bench.py --gpus R without the gather.  CFG (default C1), K frames per R.
+part of bench.py --gpus R without the gather.  CFG (default C1), K frames per R, PIPE frames
+in flight (vpx_set_pipeline lanes, default 0).
 """
 import os
 import sys
@@ -20,6 +21,7 @@ torch.cuda.set_stream(s)
 ctx = pkg.context.Context(0)
 ctx.set_stream(s.cuda_stream)
 ctx.load_scene(desc)
+ctx.set_pipeline(int(os.environ.get("PIPE", "0")))
 W, H = desc.width, desc.height
 spp = max(1, int(desc.spp))
 out = []
@@ -44,5 +46,5 @@ for R in (1, 2, 4, 8):
     out.append((R, ms))
     del acc, rgb
 base = out[0][1]
-print(cfg, " ".join(f"R={R}: {ms:.4f} ms (x{base / ms:.2f})" for R, ms in out))
+print(cfg, f"pipe={os.environ.get('PIPE', '0')}", " ".join(f"R={R}: {ms:.4f} ms (x{base / ms:.2f})" for R, ms in out))
 ctx.close()
