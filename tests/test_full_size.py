@@ -68,3 +68,58 @@ def test_full_size_config_sampled(pkg, orc, cfg):
     assert st.shadow_rays > 0 and abs(rate_g - rate_o) <= 0.1 * max(rate_o, 0.5), (rate_g, rate_o)
     del o
     gc.collect()
+
+
+# Ranks the full frame is cut into for the count check: rank 0's share is ~130 k pixels
+# (C1 / C2 at 1/16, C3 / C4 at 1/64), a few seconds of oracle time on the box's threads.
+SUBSET_RANKS = {"C1": 16, "C2": 16, "C3": 64, "C4": 64}
+
+
+def _oracle_threads():
+    import os
+    v = os.environ.get("OMP_NUM_THREADS", "")
+    return int(v) if v.isdigit() and int(v) > 0 else 8
+
+
+@pytest.mark.parametrize("cfg", ["C1", "C2", "C3", "C4"])
+def test_full_size_exact_counts(pkg, orc, cfg):
+    """The roofline numerator at full size: the frame's work counters are exact.
+    1. The full frame (vpx_render, frame 0) and the sum of its R tile shards (vpx_render_tiles,
+       rank r of R, the multi-GPU entry) count the same primary / shadow / bounce rays and
+       DDA cells — the shards partition the frame's work exactly.
+    2. Rank 0's shard — every R-th 16x16 tile of the full-size frame, the same walks the
+       whole frame makes for those pixels — counts exactly the oracle's primary / shadow /
+       bounce rays and DDA cells for the same pixels (scene.cpp:761-803, 1015-1045 loops,
+       counted cell by cell), and its samples are bit-identical."""
+    desc = pkg.scene.CONFIGS[cfg]()
+    W, H = desc.width, desc.height
+    R = SUBSET_RANKS[cfg]
+    p = desc.frame_params(0)
+    ctx = pkg.context.Context(0)
+    ctx.load_scene(desc)
+    acc = torch.zeros(W * H * 4, dtype=torch.float32, device="cuda")
+    full = ctx.render(p, acc.data_ptr(), None, stats=True)
+    del acc
+    L = ctx.packed_len(W, H, R)
+    packed = torch.zeros(L * 4, dtype=torch.float32, device="cuda")
+    tot = np.zeros(4, np.uint64)
+    for r in range(R - 1, -1, -1):  # rank 0 last: its samples stay in `packed`
+        st = ctx.render_tiles(p, r, R, packed.data_ptr(), stats=True)
+        tot += np.array([st.primary_rays, st.shadow_rays, st.bounce_rays, st.dda_cells], np.uint64)
+    torch.cuda.synchronize()
+    g0 = (st.primary_rays, st.shadow_rays, st.bounce_rays, st.dda_cells)
+    samples_g = packed.view(-1, 4).cpu().numpy()
+    ctx.close()
+    del packed
+    torch.cuda.empty_cache()
+    assert tuple(int(v) for v in tot) == (full.primary_rays, full.shadow_rays, full.bounce_rays, full.dda_cells)
+    assert full.primary_rays == W * H and full.dda_cells > 0
+
+    ids = pkg.dist.rank_pixel_ids(W, H, 0, R)
+    ok = ids >= 0
+    o = orc.Oracle(pkg.abi, desc)
+    samples_o, ost = o.render_pixels(p, ids[ok].astype(np.uint32), _oracle_threads())
+    del o
+    gc.collect()
+    assert g0 == (ost.primary_rays, ost.shadow_rays, ost.bounce_rays, ost.dda_cells), (cfg, g0, ost.as_dict())
+    assert np.array_equal(bits(samples_g[: len(ids)][ok]), bits(samples_o))
