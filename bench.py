@@ -171,7 +171,7 @@ def run_config(pkg, env, cfg, steps, warmup, weak=False, sha=None, pipeline=0):
         sharded.flush()
     torch.cuda.synchronize()
     warm = ctx.profile_read(reset=True)
-    timed_stages = [max(warm, key=lambda k: warm[k][0])] if warmup > 0 else None
+    timed_stages = [max(warm, key=lambda k: warm[k][3])] if warmup > 0 else None  # by busy time
     ctx.counters(reset=True)
     ctx.profile_select(timed_stages)
     ctx.profile_enable(steps * launches)
@@ -205,14 +205,18 @@ def run_config(pkg, env, cfg, steps, warmup, weak=False, sha=None, pipeline=0):
         K = steps
         ms_step = elapsed * 1000.0 / K
         prof = ctx.profile_read()
-        dom = max(prof, key=lambda k: prof[k][0])
-        dom_ms, dom_launches, dom_cells = prof[dom]
+        dom = max(prof, key=lambda k: prof[k][3])
+        dom_ms, dom_launches, dom_cells, dom_busy = prof[dom]
         split = warm if timed_stages else prof
-        kernel_ms = dom_ms / max(dom_launches, 1)
-        # the library runs the last level's shadow -> resolve -> finish as one launch
-        # (k_shadow_finish) unless built with VPX_FUSE_TAIL=0: then there is no
-        # separate finish stage, and the shadow stage carries the 36 B per pixel
-        fused = split.get("finish", (0.0, 0, 0))[1] == 0  # stages with no launch stay in the table
+        # a launch's duration = the stage's busy time (the union of its launch intervals) per
+        # launch: with frames in flight consecutive frames' launches overlap, and summing their
+        # start-to-end times would count the shared time twice; launch_ms is that sum per
+        # launch (what a kernel trace averages per dispatch)
+        kernel_ms = dom_busy / max(dom_launches, 1)
+        launch_ms = dom_ms / max(dom_launches, 1)
+        # the last level's shadow -> resolve -> finish run as one launch (k_shadow_finish,
+        # DESIGN.md §4): no separate finish stage, the shadow stage carries the 36 B per pixel
+        fused = split.get("finish", (0.0, 0, 0, 0.0))[1] == 0  # stages with no launch stay in the table
         kernels = dict(STAGE_KERNELS)
         if fused:
             kernels["shadow"] = "k_shadow_finish" if desc.max_bounces == 0 else "k_shadow_tile+k_shadow_finish"
@@ -243,12 +247,15 @@ def run_config(pkg, env, cfg, steps, warmup, weak=False, sha=None, pipeline=0):
                          "traffic_source": ("profiles/*_pmc_traffic.json for this library build (sha256 match)"
                                             if traffic is not None else
                                             "null: no PMC pass committed for this library build / workload"),
-                         "kernel": kernels[dom], "kernel_ms": round(kernel_ms, 4),
+                         "kernel": kernels[dom], "kernel_ms": round(kernel_ms, 4), "launch_ms": round(launch_ms, 4),
+                         "kernel_ms_def": "busy time of the kernel's launches over the timed region (overlapping "
+                                          "launches counted once) / launches; launch_ms = mean start-to-end per launch",
                          "alg_bytes_per_launch": round(alg_bytes),
-                         "stages_ms": {k: round(v[0] / max(v[1], 1), 4) for k, v in split.items() if v[1]},
+                         "stages_ms": {k: round(v[3] / max(v[1], 1), 4) for k, v in split.items() if v[1]},
                          "stages_ms_from": "last warmup step, every stage timed" if timed_stages else "timed region",
                          "frame_alg_bytes": round(frame_bytes),
                          "frame_achieved": round(frame_bytes / (ms_step * 1e-3) / 1e9, 2)},
+            "pipeline": pipeline,
         }
     del acc, rgb, sharded
     ctx.close()

@@ -366,6 +366,9 @@ typedef struct vpx_profile {
     float stage_ms[8];            /* summed device time per stage (HIP events on the stream) */
     uint32_t stage_launches[8];   /* kernel launches timed per stage                         */
     uint64_t stage_cells[8];      /* DDA cells read per stage (all launches, incl. untimed)  */
+    float stage_busy_ms[8];       /* union of the stage's launch intervals: launches that run
+                                     at the same time (frames in flight, vpx_set_pipeline)
+                                     count once; equals stage_ms when they do not overlap     */
 } vpx_profile;
 /* Time every stage launch of the next renders with HIP events on the library's stream
    (up to `max_launches` launches; 0 turns profiling off).  Adds no synchronisation. */

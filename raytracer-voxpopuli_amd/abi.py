@@ -93,7 +93,8 @@ class PrevCamera(C.Structure):
 
 
 class Profile(C.Structure):
-    _fields_ = [("stage_ms", C.c_float * 8), ("stage_launches", C.c_uint32 * 8), ("stage_cells", C.c_uint64 * 8)]
+    _fields_ = [("stage_ms", C.c_float * 8), ("stage_launches", C.c_uint32 * 8), ("stage_cells", C.c_uint64 * 8),
+                ("stage_busy_ms", C.c_float * 8)]
 
 
 class BvhTri(C.Structure):  # vpx_bvh_tri: BasicBVH Tri (BasicBVH.h:3-7) without the centroid
@@ -110,7 +111,7 @@ BVH_MAX_DEPTH = 63
 
 STAGES = ("primary", "shade", "shadow", "resolve", "bounce", "finish", "frame")
 
-STRUCT_SIZES = {PrevCamera: 64, Profile: 128, Volume: 160, Material: 32, PointLight: 24, SpotLight: 40, AreaLight: 32, DirLight: 24,
+STRUCT_SIZES = {PrevCamera: 64, Profile: 160, Volume: 160, Material: 32, PointLight: 24, SpotLight: 40, AreaLight: 32, DirLight: 24,
                 Sphere: 32, Triangle: 64, Camera: 80, FrameParams: 48, Ray: 32, Hit: 32, Stats: 40,
                 BvhTri: 36, BvhNode: 32}
 

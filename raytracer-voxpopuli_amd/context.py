@@ -181,10 +181,12 @@ class Context:
         self._chk(self.lib.vpx_profile_select(self.h, mask), "vpx_profile_select")
 
     def profile_read(self, reset=True):
-        """Per-stage device times / launches / DDA cells: {stage: (ms_total, launches, cells)}."""
+        """Per-stage device times / launches / DDA cells / busy time (the union of the launch
+        intervals): {stage: (ms_total, launches, cells, busy_ms)}."""
         pr = abi.Profile()
         self._chk(self.lib.vpx_profile_read(self.h, C.byref(pr), 1 if reset else 0), "vpx_profile_read")
-        return {name: (pr.stage_ms[i], pr.stage_launches[i], pr.stage_cells[i]) for i, name in enumerate(abi.STAGES)}
+        return {name: (pr.stage_ms[i], pr.stage_launches[i], pr.stage_cells[i], pr.stage_busy_ms[i])
+                for i, name in enumerate(abi.STAGES)}
 
     def counters(self, reset=False):
         st = abi.Stats()

@@ -249,7 +249,7 @@ int vpx_default_materials(vpx_material* out) {
 static_assert(sizeof(vpx_volume) == 160, "vpx_volume layout");
 static_assert(sizeof(vpx_material) == 32, "vpx_material layout");
 static_assert(sizeof(vpx_point_light) == 24 && sizeof(vpx_spot_light) == 40, "light layout");
-static_assert(sizeof(vpx_profile) == 128, "vpx_profile layout");
+static_assert(sizeof(vpx_profile) == 160, "vpx_profile layout");
 static_assert(sizeof(vpx_prev_camera) == 64, "vpx_prev_camera layout");
 static_assert(sizeof(vpx_area_light) == 32 && sizeof(vpx_dir_light) == 24, "light layout");
 static_assert(sizeof(vpx_sphere) == 32 && sizeof(vpx_triangle) == 64, "shape layout");

@@ -746,7 +746,9 @@ int launch_render(vpx_ctx* c, hipStream_t s, vpx_ctx::WaveStore& ws, const Scene
                   uint32_t tiles, float4* accum, uint32_t* rgb8, float4* packed, const Reproj* rp = nullptr) {
     const uint32_t P = tiles * (uint32_t)kTilePix;
     const uint32_t L = (uint32_t)std::max(1, f.max_bounces + 1);
-    const uint32_t S = (uint32_t)std::max(1, sv.area_samples);
+    // shadow slots per path: an area-light sample each, else one (point / spot / directional
+    // lights and the smoke probe use slot 0 only)
+    const uint32_t S = sv.num_areas ? (uint32_t)std::max(1, sv.area_samples) : 1u;
     int rc = ensure_wave(c, ws, P, L, S);
     if (rc) return rc;
     WaveBufs w = ws.w;
@@ -760,7 +762,10 @@ int launch_render(vpx_ctx* c, hipStream_t s, vpx_ctx::WaveStore& ws, const Scene
     const bool fuse_tail = !rp;
     if (one && fuse_tail && f.max_bounces == 0 && tiles <= kFuseFrameTiles) {
         prof_mark(c, s, VPX_STAGE_FRAME);  // the whole depth-0 frame, one launch (k_frame0)
-        hipLaunchKernelGGL((k_frame0<true, MODE>), grid, block, slds, s, sv, f, w, c->d_ctr, accum, rgb8, packed);
+        if (S == 1)  // one slot per path: the tile's slots live in LDS too
+            hipLaunchKernelGGL((k_frame0<true, MODE, true>), grid, block, slds, s, sv, f, w, c->d_ctr, accum, rgb8, packed);
+        else
+            hipLaunchKernelGGL((k_frame0<true, MODE, false>), grid, block, slds, s, sv, f, w, c->d_ctr, accum, rgb8, packed);
         prof_mark(c, s, -1);
         VPX_HIP(c, hipGetLastError());
         return VPX_OK;
@@ -2006,14 +2011,31 @@ extern "C" int vpx_profile_read(vpx_ctx* c, vpx_profile* out, int reset) {
     int rc = snapshot_counters(c, now);  // synchronises the stream
     if (rc) return rc;
     for (uint32_t st = 0; st < 8; ++st) out->stage_cells[st] = now[8 + st];
+    std::vector<std::pair<float, float>> iv[8];  // per stage: launch intervals, ms after the first event
     for (uint32_t i = 0; i + 1 < c->prof_used; i += 2) {
-        float ms = 0.f;
+        float ms = 0.f, t0 = 0.f;
         VPX_HIP(c, hipEventElapsedTime(&ms, c->prof_ev[i], c->prof_ev[i + 1]));
+        VPX_HIP(c, hipEventElapsedTime(&t0, c->prof_ev[0], c->prof_ev[i]));
         const int st = c->prof_stage[i];
         if (st >= 0 && st < 8) {
             out->stage_ms[st] += ms;
             ++out->stage_launches[st];
+            iv[st].emplace_back(t0, t0 + ms);
         }
+    }
+    for (uint32_t st = 0; st < 8; ++st) {  // busy time: the union of the intervals
+        std::sort(iv[st].begin(), iv[st].end());
+        float busy = 0.f, lo = 0.f, hi = -1.f;
+        for (const auto& v : iv[st]) {
+            if (v.first > hi) {
+                if (hi > lo) busy += hi - lo;
+                lo = v.first, hi = v.second;
+            } else if (v.second > hi) {
+                hi = v.second;
+            }
+        }
+        if (hi > lo) busy += hi - lo;
+        out->stage_busy_ms[st] = busy;
     }
     if (reset) {
         c->prof_used = 0;

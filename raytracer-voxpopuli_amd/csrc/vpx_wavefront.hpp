@@ -679,16 +679,25 @@ __device__ __forceinline__ void nearest_end_1v(const SceneView& sv, const PathRa
 // length in the previous frame measured faster per wave but not per tile (C1 0.697-0.704 vs
 // 0.712-0.715 ms with, C3 5.43 vs 5.54 — a tile costs its longest walk) and adds a
 // frame-to-frame dependency, so walkers run in pixel order.
+// The head's LDS: the compacted walker list, and with SHADE the tile's rays (O, D, H) and hit
+// records.  Declared by the kernel, so that k_frame0 can hand the regions on to its tail once
+// the head is done with them.
+template <bool SHADE>
+struct HeadLds {
+    uint32_t sh[4];
+    uint32_t lst[256];
+    float4 ray[SHADE ? 3 * 256 : 1];
+    uint32_t hm[SHADE ? 256 : 1];
+};
+
 template <bool ONE, bool SHADE>
 __device__ __forceinline__ void primary_tile(const SceneView& sv, const FrameArgs& f, const WaveBufs& w,
-                                             unsigned long long* __restrict__ ctr) {
-    __shared__ uint32_t sh[4];
-    __shared__ uint32_t lst[256];
-    __shared__ float4 s_ray[SHADE ? 3 * 256 : 1];
-    __shared__ uint32_t s_hm[SHADE ? 256 : 1];
+                                             HeadLds<SHADE>& L, unsigned long long* __restrict__ ctr) {
+    uint32_t* sh = L.sh;
+    uint32_t* lst = L.lst;
     const uint32_t tb = tile_block() * 256u;
     const uint32_t p = tb + threadIdx.x;
-    const PathRay pr = SHADE ? PathRay{s_ray, s_ray + 256, s_ray + 512, s_hm, tb} : PathRay{w.O, w.D, w.H, w.HM, 0u};
+    const PathRay pr = SHADE ? PathRay{L.ray, L.ray + 256, L.ray + 512, L.hm, tb} : PathRay{w.O, w.D, w.H, w.HM, 0u};
     Counters k{0u, 0u, 0u};
     uint32_t prim = 0;
     bool walk = false;
@@ -764,7 +773,8 @@ __device__ __forceinline__ void primary_tile(const SceneView& sv, const FrameArg
 template <bool ONE, bool SHADE = false>
 __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_NEAREST : VPX_WPE_MULTI_NEAREST) void k_primary(SceneView sv, FrameArgs f, WaveBufs w,
                                                  unsigned long long* __restrict__ ctr) {
-    primary_tile<ONE, SHADE>(sv, f, w, ctr);
+    __shared__ HeadLds<SHADE> L;
+    primary_tile<ONE, SHADE>(sv, f, w, L, ctr);
 }
 
 // Renderer::FindNearest for the active paths of a tile (bounce levels).  Rejected (DESIGN.md
@@ -1023,19 +1033,43 @@ constexpr uint32_t kFuseFrameTiles = 12288;
 #ifndef VPX_WPE_FRAME
 #define VPX_WPE_FRAME 5  // 6: 272 spilled VGPRs; 5: 9; 4: none but slower
 #endif
-template <bool ONE, int MODE>
+// The depth-0 frame's path state never leaves the workgroup: a path is shaded, its light
+// resolved and its pixel finished by the same thread, and its shadow slots are walked by the
+// same tile, so the shade's records (LA / leaf, SM, forms, smask) and — with one slot per path
+// (LSLOT: no area lights) — the slots themselves (SO, SD, SL) live in LDS.  They reuse the
+// head's regions once the head is done with them: the slots take the tile's ray records
+// (O / D / H: each thread reads its own path's before it writes its own slot), smask the hit
+// records, forms the walker list (dead after the walks' barrier).  The tile's WaveBufs view
+// points those arrays at LDS, shifted by the tile's first path so that path p indexes them
+// as p (level 0 and slot 0 only: every index is p).  HBM sees the accumulator / screen.
+template <bool ONE, int MODE, bool LSLOT>
 __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_FRAME : VPX_WPE_MULTI_NEAREST) void k_frame0(
     SceneView sv, FrameArgs f, WaveBufs w, unsigned long long* __restrict__ ctr, float4* __restrict__ accum,
     uint32_t* __restrict__ rgb8, float4* __restrict__ packed) {
-    const uint32_t p = tile_block() * 256u + threadIdx.x;
+    __shared__ HeadLds<true> L;
+    __shared__ float4 s_val[256];  // LA (a) or leaf of the path's one level
+    __shared__ float4 s_sm[256];   // SM: the pending light
     __shared__ uint32_t occ[kOccWords];
-    primary_tile<ONE, true>(sv, f, w, ctr);
+    const uint32_t tb = tile_block() * 256u;
+    const uint32_t p = tb + threadIdx.x;
+    WaveBufs wl = w;
+    wl.LA = s_val - tb;
+    wl.leaf = s_val - tb;  // a path has a leaf (sky / emissive) or a level, never both
+    wl.SM = s_sm - tb;
+    wl.smask = L.hm - tb;
+    wl.forms = L.lst - tb;
+    if (LSLOT) {
+        wl.SO = L.ray - tb;
+        wl.SD = L.ray + 256 - tb;
+        wl.SL = L.ray + 512 - tb;
+    }
+    primary_tile<ONE, true>(sv, f, wl, L, ctr);
     __syncthreads();
-    shadow_tile<ONE>(sv, w, ctr, occ);
+    shadow_tile<ONE>(sv, wl, ctr, occ);
     __syncthreads();
     LightSum ls;
-    resolve_path(sv, w, p, occ, &ls);
-    finish_path<MODE>(f, w, p, accum, rgb8, packed, &ls);
+    resolve_path(sv, wl, p, occ, &ls);
+    finish_path<MODE>(f, wl, p, accum, rgb8, packed, &ls);
 }
 
 // ------------------------------------------------------ static-camera reprojection
