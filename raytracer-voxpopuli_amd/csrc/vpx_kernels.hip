@@ -976,6 +976,16 @@ const char* vpx_last_error(const vpx_ctx* c) { return c ? c->err.c_str() : "null
 int vpx_set_stream(vpx_ctx* c, void* s) {
     if (!c) return VPX_E_INVALID;
     if (!c->members.empty()) return vpx_set_stream(c->members[0], s);  // a stream of the first device
+    VPX_HIP(c, hipSetDevice(c->device));
+    VPX_HIP(c, sync_all(c));
+    if (s && c->own_stream) {
+        // the caller's stream replaces the context's own: release it, so that its hardware
+        // queue goes to the streams that work (the pipeline lanes; GPU_MAX_HW_QUEUES is 4)
+        VPX_HIP(c, hipStreamDestroy(c->own_stream));
+        c->own_stream = nullptr;
+    } else if (!s && !c->own_stream) {
+        VPX_HIP(c, hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking));
+    }
     c->stream = s ? (hipStream_t)s : c->own_stream;
     return VPX_OK;
 }
