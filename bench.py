@@ -53,6 +53,10 @@ import __graft_entry__ as entry  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 METRIC = "Mray/s (primary+shadow) at 1920×1080, 1024³ world; 1/2/4/8-GPU"
 EXTRA_CONFIGS = ("C2", "C3", "C4")
+# Frames in flight per config (vpx_set_pipeline lanes), from the A/B on one MI355X (DESIGN.md
+# §5; ms per step, 0 / 3 / 4 lanes): C1 0.647 / 0.606 / 0.585, C2 4.18 / 2.98 / 3.48,
+# C3 5.16 / 4.98 / 5.11, C4 55.9 / 51.9 / 51.2.
+PIPELINE = {"C1": 4, "C2": 3, "C3": 3, "C4": 4}
 STAGE_KERNELS = {"primary": "k_primary", "shade": "k_shade", "shadow": "k_shadow_tile", "resolve": "k_resolve",
                  "bounce": "k_nearest_tile", "finish": "k_finish", "frame": "k_frame0"}
 
@@ -125,7 +129,7 @@ class Env:
         return f"tile-shard x{self.n}, accumulator sharded, RCCL gather of RGB8 to rank 0 (overlapped)"
 
 
-def run_config(pkg, env, cfg, steps, warmup, weak=False, sha=None, pipeline=0):
+def run_config(pkg, env, cfg, steps, warmup, weak=False, sha=None, pipeline=None):
     """Load `cfg` on this rank, run warmup + `steps` timed steps, return the result dict
     (rank 0; None elsewhere).  Frees the world before returning."""
     desc = pkg.scene.CONFIGS[cfg]()
@@ -135,6 +139,8 @@ def run_config(pkg, env, cfg, steps, warmup, weak=False, sha=None, pipeline=0):
     ctx = pkg.context.Context(env.dev)
     ctx.set_stream(env.stream.cuda_stream)
     ctx.load_scene(desc)
+    if pipeline is None:
+        pipeline = PIPELINE.get(cfg, 0)
     ctx.set_pipeline(pipeline)
     torch.cuda.synchronize()
     acc = rgb = sharded = None
@@ -372,8 +378,9 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip extra_configs / weak_scaling")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
-    ap.add_argument("--pipeline", type=int, default=int(os.environ.get("VPX_PIPELINE", "0")),
-                    help="frames in flight per GPU (vpx_set_pipeline lanes; 0 = serial frames)")
+    ap.add_argument("--pipeline", type=int, default=None,
+                    help="frames in flight per GPU (vpx_set_pipeline lanes; 0 = serial frames); default: "
+                         "per config, PIPELINE")
     args = ap.parse_args()
     if needs_launch(args.gpus):
         # `python bench.py --gpus N` without torchrun: start the N ranks as child processes
@@ -409,7 +416,7 @@ def main():
                        "build-defined 1024^3 / 2048^3 u8 grids on device; fixed lights/camera (SURVEY.md §8(d))",
                "config": {"workload": head["workload"], "width": head["width"], "height": head["height"],
                           "world_n": head["world_n"], "max_bounces": head["max_bounces"], "spp": head["spp"],
-                          "parallelism": env.parallelism(), "lib_sha256": sha},
+                          "parallelism": env.parallelism(), "frames_in_flight": head["pipeline"], "lib_sha256": sha},
                "rays_per_step": head["rays_per_step"], "mpix_per_s": head["mpix_per_s"],
                "total_mray_s": head["total_mray_s"], "roofline": head["roofline"], "cpu_baseline": None}
         if extra:
