@@ -29,7 +29,7 @@ def main():
             cur[k] = v
     print(f"{'VGPR':>5} {'vSpl':>5} {'sSpl':>5} {'scr':>5} {'occ':>4}  kernel")
     for r in rows:
-        n = re.sub(r"\(.*", "", r["name"]).replace("vpx::", "").replace("(anonymous namespace)::", "")
+        n = re.sub(r"\(.*", "", r["name"].replace("(anonymous namespace)::", "")).replace("vpx::", "")
         print(f"{r.get('VGPRs', '?'):>5} {r.get('VGPRs Spill', '?'):>5} {r.get('SGPRs Spill', '?'):>5} "
               f"{r.get('ScratchSize [bytes/lane]', '?'):>5} {r.get('Occupancy [waves/SIMD]', '?'):>4}  {n}")
 
