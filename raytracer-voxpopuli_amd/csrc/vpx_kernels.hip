@@ -685,8 +685,7 @@ int validate_frame(vpx_ctx* c, const vpx_frame_params* p) {
 int ensure_wave(vpx_ctx* c, vpx_ctx::WaveStore& ws, uint32_t P, uint32_t L, uint32_t S) {
     const size_t f4 = sizeof(float4);
     const size_t bytes = (size_t)P * (f4 * (5 + 2 * (size_t)L + 3 * (size_t)S + 1) + 3 * sizeof(uint32_t)) +
-                         sizeof(uint32_t) * (size_t)P + 16 * 256 +
-                         (L > 1 ? 2 * sizeof(uint32_t) * (size_t)P + sizeof(uint32_t) * (kBounceBins + 1) + 3 * 256 : 0);
+                         sizeof(uint32_t) * (size_t)P + 16 * 256;
     if (bytes > ws.bytes) {
         if (ws.d) {
             VPX_HIP(c, sync_all(c));
@@ -720,12 +719,6 @@ int ensure_wave(vpx_ctx* c, vpx_ctx::WaveStore& ws, uint32_t P, uint32_t L, uint
     w.depth = (int32_t*)take(4 * (size_t)P);
     w.forms = (uint32_t*)take(4 * (size_t)P);
     w.smask = (uint32_t*)take(4 * (size_t)P);
-    w.bkey = w.border = w.bhist = nullptr;
-    if (L > 1) {  // bounce levels: the frame-scope bounce order (vpx_wavefront.hpp k_bounce_*)
-        w.bkey = (uint32_t*)take(4 * (size_t)P);
-        w.border = (uint32_t*)take(4 * (size_t)P);
-        w.bhist = (uint32_t*)take(4 * (size_t)(kBounceBins + 1));
-    }
     return VPX_OK;
 }
 
@@ -747,11 +740,6 @@ struct Reproj {  // the static-camera tail (vpx_render_reproject)
     PrevCam prev;
     float4 *alb, *ill, *rd, *temp, *hist;
 };
-
-#ifndef VPX_BOUNCE_SORT
-#define VPX_BOUNCE_SORT 0
-#endif
-constexpr bool kBounceSort = VPX_BOUNCE_SORT != 0;
 
 template <int MODE>
 int launch_render(vpx_ctx* c, hipStream_t s, vpx_ctx::WaveStore& ws, const SceneView& sv, const FrameArgs& f,
@@ -813,17 +801,7 @@ int launch_render(vpx_ctx* c, hipStream_t s, vpx_ctx::WaveStore& ws, const Scene
         prof_mark(c, s, -1);
         if (level < f.max_bounces) {
             prof_mark(c, s, VPX_STAGE_BOUNCE);
-            if (kBounceSort) {  // the frame's bounce rays in (octant, origin region) order
-                VPX_HIP(c, hipMemsetAsync(w.bhist, 0, sizeof(uint32_t) * kBounceBins, s));
-                hipLaunchKernelGGL(k_bounce_key, grid, block, 0, s, sv, w);
-                hipLaunchKernelGGL(k_bounce_scan, dim3(1), dim3(1024), 0, s, w.bhist);
-                hipLaunchKernelGGL(k_bounce_scatter, grid, block, 0, s, w);
-                hipLaunchKernelGGL(one ? k_nearest_sorted<true> : k_nearest_sorted<false>, grid, block, 0, s, sv, w,
-                                   c->d_ctr);
-            } else {
-                hipLaunchKernelGGL(one ? k_nearest_tile<true> : k_nearest_tile<false>, grid, block, 0, s, sv, w,
-                                   c->d_ctr);
-            }
+            hipLaunchKernelGGL(one ? k_nearest_tile<true> : k_nearest_tile<false>, grid, block, 0, s, sv, w, c->d_ctr);
             prof_mark(c, s, -1);
         }
     }

@@ -94,9 +94,6 @@ struct WaveBufs {
     float4* SM;    // [P] pending light: xyz = kd (area), w = bits(kind | discard<<3 | count<<4 | level<<8 | lc<<16)
     uint32_t* smask;  // [P] shadow slots emitted this level (bit s = slot s, s < 15) | light key << 16
     float4* RD;    // [W*H] reprojection: level-0 intersection point, w = material bits (image order)
-    uint32_t* bkey;   // [P] bounce sort: the path's key (kNoKey: no bounce ray)
-    uint32_t* border; // [P] bounce sort: the frame's bounce rays in key order
-    uint32_t* bhist;  // [kBounceBins + 1] bounce sort: key histogram -> offsets; [kBounceBins] = total
     uint32_t P;    // paths (pixels) this call
     uint32_t S;    // shadow slots per path
 };
@@ -780,102 +777,14 @@ __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_NEAREST : VPX_WPE_MULTI_
     primary_tile<ONE, SHADE>(sv, f, w, L, ctr);
 }
 
-// ---------------------------------------------------------- frame-scope bounce order
-// Bounce rays leave surfaces in scattered directions, so a tile's bounce walks read
-// unrelated cache lines (C2: 3.8x the algorithmic bytes, L2 hit rate 51 %).  The frame's
-// bounce rays are instead walked in the order of a key — the ray's direction octant, then
-// the Morton index of its origin's 16^3-cell region of the world volume — so that a wave's
-// lanes start close together and head the same way.  A counting sort: per-path keys with a
-// histogram (k_bounce_key), one workgroup's exclusive scan (k_bounce_scan), the scatter
-// (k_bounce_scatter); k_nearest_sorted walks entry i of the order.  Any order gives the same
-// per-ray results (each walk is independent), so the frame stays bit-identical.
-constexpr uint32_t kBounceBins = 1u << 15;  // 3 octant bits + 12 Morton bits
-constexpr uint32_t kNoKey = 0xffffffffu;
-__device__ __forceinline__ uint32_t spread3_4(uint32_t v) {  // 4 bits -> every third bit
-    v &= 15u;
-    return (v & 1u) | ((v & 2u) << 2) | ((v & 4u) << 4) | ((v & 8u) << 6);
-}
-__device__ __forceinline__ uint32_t region_coord(float x, float lo, float hi) {
-    const float u = (x - lo) / (hi - lo) * 16.0f;
-    return u >= 15.0f ? 15u : (u > 0.0f ? (uint32_t)u : 0u);
-}
-__global__ __launch_bounds__(256) void k_bounce_key(SceneView sv, WaveBufs w) {
-    const uint32_t p = blockIdx.x * 256u + threadIdx.x;
-    if (p >= w.P) return;
-    const float4 d = w.D[p];
-    uint32_t key = kNoKey;
-    if (__float_as_uint(d.w) & kActive) {
-        const float4 o = w.O[p];
-        const vpx_volume* vol = uni_ptr(&sv.volumes[0]);
-        const f3 op = xform_pos_ssem(mk(o.x, o.y, o.z), vol->inv_matrix);
-        const uint32_t x = region_coord(op.x, vol->b0[0], vol->b1[0]), y = region_coord(op.y, vol->b0[1], vol->b1[1]),
-                       z = region_coord(op.z, vol->b0[2], vol->b1[2]);
-        const uint32_t oct = (__float_as_uint(d.x) >> 31) | ((__float_as_uint(d.y) >> 31) << 1) |
-                             ((__float_as_uint(d.z) >> 31) << 2);
-        key = (oct << 12) | spread3_4(x) | (spread3_4(y) << 1) | (spread3_4(z) << 2);
-        atomicAdd(&w.bhist[key], 1u);
-    }
-    w.bkey[p] = key;
-}
-// One workgroup of 1024: exclusive offsets of the kBounceBins counts in place, total at the end.
-__global__ __launch_bounds__(1024) void k_bounce_scan(uint32_t* __restrict__ hist) {
-    constexpr uint32_t kPer = kBounceBins / 1024u;
-    __shared__ uint32_t wsum[16];
-    uint32_t* h = hist + threadIdx.x * kPer;
-    uint32_t mine = 0;
-    for (uint32_t i = 0; i < kPer; ++i) mine += h[i];
-    uint32_t wt;
-    const uint32_t off = wave_prefix(mine, wt);
-    if ((threadIdx.x & 63u) == 0) wsum[threadIdx.x >> 6] = wt;
-    __syncthreads();
-    uint32_t base = 0, total = 0;
-    for (uint32_t i = 0; i < 16; ++i) {
-        base += i < (threadIdx.x >> 6) ? wsum[i] : 0u;
-        total += wsum[i];
-    }
-    uint32_t run = base + off;
-    for (uint32_t i = 0; i < kPer; ++i) {
-        const uint32_t c = h[i];
-        h[i] = run;
-        run += c;
-    }
-    if (threadIdx.x == 0) hist[kBounceBins] = total;
-}
-__global__ __launch_bounds__(256) void k_bounce_scatter(WaveBufs w) {
-    const uint32_t p = blockIdx.x * 256u + threadIdx.x;
-    if (p >= w.P) return;
-    const uint32_t key = w.bkey[p];
-    if (key != kNoKey) w.border[atomicAdd(&w.bhist[key], 1u)] = p;
-}
-// Renderer::FindNearest for entries [256 b, 256 b + 256) of the frame's bounce order.
-template <bool ONE>
-__global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_BOUNCE : VPX_WPE_MULTI_NEAREST) void k_nearest_sorted(
-    SceneView sv, WaveBufs w, unsigned long long* __restrict__ ctr) {
-    const uint32_t total = w.bhist[kBounceBins];  // the scatter turned the offsets into ends
-    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-    if (blockIdx.x * 256u >= total) return;  // the whole workgroup
-    Counters k{0u, 0u, 0u};
-    if (i < total) {
-        const uint32_t q = w.border[i];
-        if (ONE) {
-            nearest_record_1v<kSkipwBounce, kMincBounce, kRunBounce>(sv, PathRay{w.O, w.D, w.H, w.HM, 0u}, q, k);
-        } else {
-            const float4 o = w.O[q], d = w.D[q];
-            Ray r;
-            r.O = mk(o.x, o.y, o.z);
-            r.D = mk(d.x, d.y, d.z);
-            r.inside = (__float_as_uint(d.w) & kInside) != 0u;
-            nearest_record<kSkipwBounce, kMincBounce, kRunBounce>(sv, PathRay{w.O, w.D, w.H, w.HM, 0u}, q, r, k);
-        }
-    }
-    flush_counters(k, 0u, ctr, VPX_STAGE_BOUNCE);
-}
-
 // Renderer::FindNearest for the active paths of a tile (bounce levels).  Rejected (DESIGN.md
 // §4): grouping a tile's walks by direction octant (C2 4.88 vs 4.82 ms), gathering 2 / 4 / 8
 // tiles per workgroup (C1 2.87 / 3.22 / 4.36 vs 2.70 ms: walk lengths are heavy-tailed, a
 // wave costs its longest ray), continuing a tile's unfinished walks in repacked waves after a
-// step budget (C2 4.23-4.37 vs 4.28 ms).
+// step budget (C2 4.23-4.37 vs 4.28 ms), and walking the whole frame's bounce rays in the
+// order of a counting sort by (direction octant, Morton index of the origin's 16^3-cell
+// region): the sorted walker took 553 vs 541 us per level on C2 and the sort 350 us more —
+// coherent starts do not shorten the walks, whose cost is their length and step latency.
 template <bool ONE>
 __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_BOUNCE : VPX_WPE_MULTI_NEAREST) void k_nearest_tile(SceneView sv, WaveBufs w, unsigned long long* __restrict__ ctr) {
     __shared__ uint32_t sh[4];
