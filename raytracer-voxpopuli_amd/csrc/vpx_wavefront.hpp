@@ -1033,8 +1033,11 @@ __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_SHADOW : VPX_WPE_MULTI_S
 // workgroup barrier measured C1 0.725 vs 0.711 ms (the tile's barriers are not what sets the
 // small-launch floor; its longest walk chains are).
 constexpr uint32_t kFuseFrameTiles = 12288;
+// k_frame0 occupancy: with the path state in LDS (round 3) 6 waves/SIMD spill 22 VGPRs
+// (round 2: 272) and measured 1.5 % faster than 5 (no spills) with frames in flight
+// (profiles/r03_frame_occupancy_ab.txt); 7 would need 7 x 23 KiB of LDS per CU (> 160 KiB).
 #ifndef VPX_WPE_FRAME
-#define VPX_WPE_FRAME 5  // 6: 272 spilled VGPRs; 5: 9; 4: none but slower
+#define VPX_WPE_FRAME 6
 #endif
 // The depth-0 frame's path state never leaves the workgroup: a path is shaded, its light
 // resolved and its pixel finished by the same thread, and its shadow slots are walked by the
