@@ -221,13 +221,14 @@ int vpx_abi_version(void);
 int vpx_set_stream(vpx_ctx* ctx, void* hip_stream);
 int vpx_synchronize(vpx_ctx* ctx);
 /* Frames in flight (depth 2..4; 0 / 1 = off, the default).  With depth D, vpx_render and
-   vpx_render_tiles[_accum] render each frame on the next of D library-owned streams ("lanes",
+   vpx_render_tiles_accum render each frame on the next of D library-owned streams ("lanes",
    each with its own path-state buffers) into packed float4 samples, and queue only the
    frame's accumulate / tonemap / RGB8 pack (or the rank's packed running average) on the
    context's stream, after the previous frame's: frame f+1's walks run while frame f's last
    tiles drain.  Results are bit-identical (the same blend of the same sample, in frame order);
    accum / rgb8 are complete when the context's stream is.  Renders that take stats, the
-   static-camera path and VPX_FLAG_NO_TONEMAP frames run on the stream as without lanes.
+   static-camera path, VPX_FLAG_NO_TONEMAP frames and vpx_render_tiles (samples into the
+   caller's buffer) run on the stream as without lanes.
    World / table updates wait for the frames in flight.  No reference counterpart: the
    reference renders one frame per Tick (renderer.cpp:1646-1891). */
 int vpx_set_pipeline(vpx_ctx* ctx, uint32_t depth);

@@ -1581,15 +1581,17 @@ static int render_tiles_impl(int MODE, vpx_ctx* c, const vpx_frame_params* p, ui
     VPX_HIP(c, hipSetDevice(c->device));
     const SceneView sv = view_of(c, p->sky, p->area_samples, (p->flags & VPX_FLAG_SKY) != 0);
     const FrameArgs f = frame_of(c, p, rank, n_ranks);
-    if (!c->lanes.empty() && !stats) {  // frames in flight (vpx_set_pipeline)
+    // frames in flight (vpx_set_pipeline) for the sharded accumulator: the frame renders into
+    // the lane's own samples and only the blend runs on the caller's stream.  Packed samples
+    // into the caller's buffer stay serial: a lane would not wait for the caller's use of the
+    // previous frame's samples (e.g. a gather queued on its stream).
+    if (MODE == kFinishPackedAccum && !c->lanes.empty() && !stats) {
         vpx_ctx::Lane* L = nullptr;
-        if ((rc = lane_render(c, sv, f, f.tiles_per_rank, MODE == kFinishPackedSample ? packed : nullptr, L))) return rc;
-        if (MODE == kFinishPackedAccum) {  // this rank's running average, in frame order on the caller's stream
-            const uint32_t P = f.tiles_per_rank * (uint32_t)kTilePix;
-            hipLaunchKernelGGL(blend_packed, dim3(f.tiles_per_rank), dim3(kThreads), 0, c->stream, f, L->packed, accum,
-                               rgb8, P);
-            VPX_HIP(c, hipGetLastError());
-        }
+        if ((rc = lane_render(c, sv, f, f.tiles_per_rank, nullptr, L))) return rc;
+        const uint32_t P = f.tiles_per_rank * (uint32_t)kTilePix;  // this rank's running average, in frame order
+        hipLaunchKernelGGL(blend_packed, dim3(f.tiles_per_rank), dim3(kThreads), 0, c->stream, f, L->packed, accum, rgb8,
+                           P);
+        VPX_HIP(c, hipGetLastError());
         VPX_HIP(c, hipEventRecord(L->consumed, c->stream));
         return VPX_OK;
     }

@@ -1032,7 +1032,10 @@ __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_SHADOW : VPX_WPE_MULTI_S
 // each wave's 16x4 strip through the whole frame with wave-local compaction and no
 // workgroup barrier measured C1 0.725 vs 0.711 ms (the tile's barriers are not what sets the
 // small-launch floor; its longest walk chains are).
-constexpr uint32_t kFuseFrameTiles = 12288;
+#ifndef VPX_FUSE_FRAME_TILES
+#define VPX_FUSE_FRAME_TILES 12288
+#endif
+constexpr uint32_t kFuseFrameTiles = VPX_FUSE_FRAME_TILES;
 // k_frame0 occupancy: with the path state in LDS (round 3) 6 waves/SIMD spill 22 VGPRs
 // (round 2: 272) and measured 1.5 % faster than 5 (no spills) with frames in flight
 // (profiles/r03_frame_occupancy_ab.txt); 7 would need 7 x 23 KiB of LDS per CU (> 160 KiB).

@@ -917,3 +917,32 @@ def test_frames_in_flight_sharded_accumulator(pkg, lanes):
 
     for x, y in zip(run(0), run(lanes)):
         assert np.array_equal(x, y)
+
+
+def test_frames_in_flight_on_a_device_set(pkg):
+    """A device set ({0, 0}) with 3 lanes per member: the sharded-accumulator frames
+    (accum = NULL, RGB8 gathered) and the sample frames (accum given) equal one device's
+    serial frames over 4 AA frames at depth 1."""
+    sc = pkg.scene
+    desc = sc.city_scene("monu3", 128, 100, 70, 1)
+    desc.flags = pkg.abi.VPX_FLAG_AA
+    acc_ref, rgb_ref, _ = render_gpu(pkg, desc, frames=4)
+    W, H = desc.width, desc.height
+    torch.cuda.set_device(0)
+    ctx = pkg.context.Context(devices=[0, 0])
+    ctx.load_scene(desc)
+    ctx.set_pipeline(3)
+    acc = torch.zeros(W * H * 4, dtype=torch.float32, device="cuda")
+    rgb = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+    rgb2 = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    for f in range(4):
+        ctx.render(desc.frame_params(f), acc.data_ptr(), rgb.data_ptr())
+    ctx.synchronize()
+    for f in range(4):
+        ctx.render(desc.frame_params(f), 0, rgb2.data_ptr())
+    ctx.synchronize()
+    assert np.array_equal(bits(acc.cpu().numpy().reshape(-1, 4)), bits(acc_ref))
+    assert np.array_equal(rgb.cpu().numpy().view(np.uint32), rgb_ref)
+    assert np.array_equal(rgb2.cpu().numpy().view(np.uint32), rgb_ref)
+    ctx.close()
