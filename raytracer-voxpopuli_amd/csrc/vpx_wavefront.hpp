@@ -139,11 +139,10 @@ __device__ __forceinline__ bool path_pixel(const FrameArgs& f, uint32_t p, uint3
     return tile < f.num_tiles && x < f.width && y < f.height;
 }
 
-__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
+// Sum over the wave (every lane gets it).  DPP row shifts / mirrors rather than __shfl_xor:
+// the shuffles' lane-address registers were hoisted and kept live (spilled) across
+// k_frame0's walks, since the three counter flushes share them.
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) { return __reduce_add_sync(~0ull, v); }
 
 // Work counters: [0] shadow rays, [1] FindNearest calls, [2] DDA cells, [3] primary rays,
 // [8 + s] DDA cells of stage s (VPX_STAGE_*), striped over kCtrStripes copies of
@@ -296,15 +295,23 @@ __device__ __forceinline__ uint32_t emit_illumination(const SceneView& sv, const
 
 // One Trace level of the material switch (renderer.cpp:1100-1327) for an active path.
 // Exclusive wave prefix sum (inclusive scan by shuffles, minus self).
+// DPP form (no lane-address registers, see wave_sum): an inclusive scan inside each row of
+// 16 lanes by row shifts of 1, 2, 4, 8 (lanes shifted in from outside the row read 0), then
+// the rows' totals carried by row_bcast:15 (into rows 1 and 3) and row_bcast:31 (rows 2, 3).
+// Needs the whole wave active (every caller runs it in uniform control flow).
+template <int CTRL, int ROWS = 0xf>
+__device__ __forceinline__ uint32_t dpp_add(uint32_t x) {
+    return x + (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROWS, 0xf, true);
+}
 __device__ __forceinline__ uint32_t wave_prefix(uint32_t v, uint32_t& total) {
-    const uint32_t lane = threadIdx.x & 63u;
     uint32_t x = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(x, o, 64);
-        if (lane >= (uint32_t)o) x += y;
-    }
-    total = __shfl(x, 63, 64);
+    x = dpp_add<0x111>(x);        // row_shr:1
+    x = dpp_add<0x112>(x);        // row_shr:2
+    x = dpp_add<0x114>(x);        // row_shr:4
+    x = dpp_add<0x118>(x);        // row_shr:8
+    x = dpp_add<0x142, 0xa>(x);   // row_bcast:15
+    x = dpp_add<0x143, 0xc>(x);   // row_bcast:31
+    total = (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
     return x - v;
 }
 
@@ -786,7 +793,7 @@ __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_NEAREST : VPX_WPE_MULTI_
 // region): the sorted walker took 553 vs 541 us per level on C2 and the sort 350 us more —
 // coherent starts do not shorten the walks, whose cost is their length and step latency.
 template <bool ONE>
-__global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_BOUNCE : VPX_WPE_MULTI_NEAREST) void k_nearest_tile(SceneView sv, WaveBufs w, unsigned long long* __restrict__ ctr) {
+__device__ __forceinline__ void nearest_tile(const SceneView& sv, const WaveBufs& w, unsigned long long* __restrict__ ctr) {
     __shared__ uint32_t sh[4];
     __shared__ uint32_t lst[256];
     const uint32_t base = tile_block() * 256u;
@@ -811,6 +818,27 @@ __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_BOUNCE : VPX_WPE_MULTI_N
         }
     }
     flush_counters(k, 0u, ctr, VPX_STAGE_BOUNCE);
+}
+
+template <bool ONE>
+__global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_BOUNCE : VPX_WPE_MULTI_NEAREST) void k_nearest_tile(SceneView sv, WaveBufs w, unsigned long long* __restrict__ ctr) {
+    nearest_tile<ONE>(sv, w, ctr);
+}
+
+#ifndef VPX_FUSE_LEVEL
+#define VPX_FUSE_LEVEL 0
+#endif
+// (VPX_FUSE_LEVEL A/B) a bounce level's FindNearest walks and the next level's material
+// switch in one launch: the tile's walks, a workgroup barrier (the hit records the tile's
+// walkers wrote to HBM are then visible to the tile), each thread's shade.
+template <bool ONE>
+__global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_BOUNCE : VPX_WPE_MULTI_NEAREST) void k_nearest_shade(
+    SceneView sv, FrameArgs f, WaveBufs w, int level, unsigned long long* __restrict__ ctr) {
+    nearest_tile<ONE>(sv, w, ctr);
+    __syncthreads();
+    Counters ks{0u, 0u, 0u};
+    shade_path(sv, f, w, PathRay{w.O, w.D, w.H, w.HM, 0u}, tile_block() * 256u + threadIdx.x, level, ks);
+    flush_counters(ks, 0u, ctr, VPX_STAGE_SHADE);
 }
 
 // Renderer::IsOccluded for the shadow slots of a tile (entry = slot << 27 | path).  The
@@ -903,6 +931,17 @@ __device__ __forceinline__ void shadow_tile(const SceneView& sv, const WaveBufs&
 template <bool ONE>
 __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_SHADOW : VPX_WPE_MULTI_SHADOW) void k_shadow_tile(SceneView sv, WaveBufs w, unsigned long long* __restrict__ ctr) {
     shadow_tile<ONE>(sv, w, ctr);
+}
+
+// (VPX_FUSE_LEVEL A/B) a non-last level's IsOccluded walks and light sums in one launch: the
+// occluded flags in the tile's LDS bitmap, a barrier, each thread's resolve into LB.
+template <bool ONE>
+__global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_SHADOW : VPX_WPE_MULTI_SHADOW) void k_shadow_resolve(
+    SceneView sv, WaveBufs w, unsigned long long* __restrict__ ctr) {
+    __shared__ uint32_t occ[kOccWords];
+    shadow_tile<ONE>(sv, w, ctr, occ);
+    __syncthreads();
+    resolve_path(sv, w, tile_block() * 256u + threadIdx.x, occ);
 }
 
 // ------------------------------------------------------------------- stage 4
@@ -1076,9 +1115,13 @@ __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_FRAME : VPX_WPE_MULTI_NE
     __syncthreads();
     shadow_tile<ONE>(sv, wl, ctr, occ);
     __syncthreads();
+    // the tail's own copy of p: the shade's per-lane LDS addresses are re-derived here
+    // instead of being kept live (spilled) across the shadow walks
+    uint32_t pt = p;
+    asm volatile("" : "+v"(pt));
     LightSum ls;
-    resolve_path(sv, wl, p, occ, &ls);
-    finish_path<MODE>(f, wl, p, accum, rgb8, packed, &ls);
+    resolve_path(sv, wl, pt, occ, &ls);
+    finish_path<MODE>(f, wl, pt, accum, rgb8, packed, &ls);
 }
 
 // ------------------------------------------------------ static-camera reprojection
