@@ -781,7 +781,7 @@ int launch_render(vpx_ctx* c, hipStream_t s, vpx_ctx::WaveStore& ws, const Scene
     prof_mark(c, s, -1);
     // the last level's shadow -> resolve -> finish as one launch (k_shadow_finish)
     for (int level = 0; level <= f.max_bounces; ++level) {
-        if (!(fuse_head && level == 0) && !(VPX_FUSE_LEVEL && !rp && level > 0)) {
+        if (!(fuse_head && level == 0)) {
             prof_mark(c, s, VPX_STAGE_SHADE);
             hipLaunchKernelGGL(k_shade, grid, block, 0, s, sv, f, w, level, c->d_ctr);
             prof_mark(c, s, -1);
@@ -793,27 +793,15 @@ int launch_render(vpx_ctx* c, hipStream_t s, vpx_ctx::WaveStore& ws, const Scene
             prof_mark(c, s, -1);
             break;
         }
-        if (VPX_FUSE_LEVEL) {
-            prof_mark(c, s, VPX_STAGE_SHADOW);
-            hipLaunchKernelGGL(one ? k_shadow_resolve<true> : k_shadow_resolve<false>, grid, block, slds, s, sv, w,
-                               c->d_ctr);
-            prof_mark(c, s, -1);
-        } else {
-            prof_mark(c, s, VPX_STAGE_SHADOW);
-            hipLaunchKernelGGL(one ? k_shadow_tile<true> : k_shadow_tile<false>, grid, block, slds, s, sv, w, c->d_ctr);
-            prof_mark(c, s, -1);
-            prof_mark(c, s, VPX_STAGE_RESOLVE);
-            hipLaunchKernelGGL(k_resolve, grid, block, 0, s, sv, w);
-            prof_mark(c, s, -1);
-        }
+        prof_mark(c, s, VPX_STAGE_SHADOW);
+        hipLaunchKernelGGL(one ? k_shadow_tile<true> : k_shadow_tile<false>, grid, block, slds, s, sv, w, c->d_ctr);
+        prof_mark(c, s, -1);
+        prof_mark(c, s, VPX_STAGE_RESOLVE);
+        hipLaunchKernelGGL(k_resolve, grid, block, 0, s, sv, w);
+        prof_mark(c, s, -1);
         if (level < f.max_bounces) {
             prof_mark(c, s, VPX_STAGE_BOUNCE);
-            if (VPX_FUSE_LEVEL && !rp)  // the next level's shade at the end of the walks
-                hipLaunchKernelGGL(one ? k_nearest_shade<true> : k_nearest_shade<false>, grid, block, 0, s, sv, f, w,
-                                   level + 1, c->d_ctr);
-            else
-                hipLaunchKernelGGL(one ? k_nearest_tile<true> : k_nearest_tile<false>, grid, block, 0, s, sv, w,
-                                   c->d_ctr);
+            hipLaunchKernelGGL(one ? k_nearest_tile<true> : k_nearest_tile<false>, grid, block, 0, s, sv, w, c->d_ctr);
             prof_mark(c, s, -1);
         }
     }

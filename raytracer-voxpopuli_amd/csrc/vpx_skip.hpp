@@ -319,8 +319,8 @@ VPX_HD int classify(Walk& w, const GridView& g) {
 // The same class from the octant plane `pl` (g.dfp + octant * g.plane): one byte per step
 // from a plane an eighth the size of l1, and the brick's cell mask only when the byte says
 // occupied (0) — a dependent second load, but walks step mostly through empty bricks.
-// For an empty brick m1 gets the byte at the octant's shift, as the l1 word holds it, so
-// df_box reads the cube the same way.
+// For an empty brick m1 gets the byte itself (the cube, unshifted: cube_dfp reads it back
+// without the octant shift, so the walk loop keeps no shift live).
 VPX_HD uint32_t load_u8(const uint8_t* p, uint32_t i) {
 #if defined(__HIP_DEVICE_COMPILE__)
     return ((const __attribute__((address_space(1))) uint8_t*)p)[i];
@@ -338,18 +338,44 @@ VPX_HD int classify_dfp_byte(Walk& w, const GridView& g, uint32_t k) {
         const uint32_t cb = (X & 3u) | ((Y & 3u) << 2) | ((Z & 3u) << 4);
         return ((w.m1 >> cb) & 1ull) ? 0 : 1;
     }
-    w.m1 = (uint64_t)k << w.osh;
+    w.m1 = k;
     return k >= MINC ? 2 : 3;
 }
 template <uint32_t MINC = kMinCube>
 VPX_HD int classify_dfp(Walk& w, const GridView& g, const uint8_t* pl) {
     return classify_dfp_byte<MINC>(w, g, load_u8(pl, blk_index(w.X >> 2, w.Y >> 2, w.Z >> 2, g.nb2)));
 }
-// The empty box of a class-2 cell: its brick's distance-field cube toward the ray's
+// classify_dfp with the plane named by its first parent, opar = octant * nb2^3: the planes
+// are consecutive and parent-major, so octant and parent fold into one 32-bit parent index
+// (< 2^27 up to 4096^3 grids) and only the byte offset is formed in 64 bits — a walk keeps
+// one 32-bit value live for its plane instead of a 64-bit pointer.
+template <uint32_t MINC = kMinCube>
+VPX_HD int classify_dfp_o(Walk& w, const GridView& g, uint32_t opar) {
+    const uint32_t bx = w.X >> 2, by = w.Y >> 2, bz = w.Z >> 2, np = g.nb2;
+#if defined(__HIP_DEVICE_COMPILE__)
+    const uint32_t parent = opar + __umul24(bz >> 2, __umul24(np, np)) + __umul24(by >> 2, np) + (bx >> 2);
+#else
+    const uint32_t parent = opar + (bz >> 2) * np * np + (by >> 2) * np + (bx >> 2);
+#endif
+    const uint64_t i = (uint64_t)parent << 6 | ((bx & 3u) | ((by & 3u) << 2) | ((bz & 3u) << 4));
+#if defined(__HIP_DEVICE_COMPILE__)
+    const uint32_t k = ((const __attribute__((address_space(1))) uint8_t*)g.dfp)[i];
+#else
+    const uint32_t k = g.dfp[i];
+#endif
+    return classify_dfp_byte<MINC>(w, g, k);
+}
+// The first parent of octant o's plane (classify_dfp_o).
+VPX_HD uint32_t plane_parent(const GridView& g, uint32_t o) { return o * (g.nb2 * g.nb2 * g.nb2); }
+// The distance-field cube (in bricks) of an empty brick from m1: after classify (the l1
+// word, byte at the octant's shift) / after classify_dfp (the plane byte itself).
+VPX_HD uint32_t cube_l1(const Walk& w) { return (uint32_t)(w.m1 >> w.osh) & 255u; }
+VPX_HD uint32_t cube_dfp(const Walk& w) { return (uint32_t)w.m1 & 255u; }
+// The empty box of a class-2 cell: its brick's distance-field cube `k` toward the ray's
 // octant, clipped to the grid.  Only the faces ahead of the ray matter to skip_box, so the
 // faces behind are put at the current cell.
-VPX_HD void df_box(const Walk& w, uint32_t n, uint32_t lo[3], uint32_t hi[3]) {
-    const uint32_t k4 = ((uint32_t)(w.m1 >> w.osh) & 255u) * 4u;
+VPX_HD void df_box(const Walk& w, uint32_t n, uint32_t k, uint32_t lo[3], uint32_t hi[3]) {
+    const uint32_t k4 = k * 4u;
     const uint32_t c[3] = {w.X, w.Y, w.Z};
     const int32_t sg[3] = {w.sx, w.sy, w.sz};
     for (int k = 0; k < 3; ++k) {
@@ -723,7 +749,7 @@ VPX_HD bool walk_skip(const GridView& g, Walk& w, float bound, uint32_t& cells) 
         }
         if (cls == 2) {
             uint32_t lo[3], hi[3];
-            df_box(w, g.n, lo, hi);
+            df_box(w, g.n, cube_l1(w), lo, hi);
             if (skip_box_lean(w, lo, hi, bound, cells) == 1) return false;
         }
         ++cells;  // visit the (empty) current cell

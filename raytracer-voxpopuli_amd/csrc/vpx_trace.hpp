@@ -424,7 +424,7 @@ __device__ __forceinline__ bool walk_wave(const skip::GridView& g, skip::Walk& w
     constexpr bool kSeg2Branch = (RUN >> 17) & 1u;
     constexpr bool kMin2 = (RUN >> 18) & 1u;  // step1's two-compare axis choice (vpx_skip.hpp)
     static_assert(SKIPW > 0 && kRun > 0 && kPasses > 0, "walk_wave: skip weight, run cap and passes");
-    const uint8_t* pl = g.dfp + (uint64_t)(w.osh >> 3) * g.plane;  // the ray's octant plane
+    const uint32_t opar = skip::plane_parent(g, w.osh >> 3);  // the ray's octant plane
     int mode = kStep;
     VPX_PH(uint64_t cs = 0, ck = 0, ns = 0, nk = 0, ls = 0, lk = 0, fb = 0, cf = 0;)
     for (;;) {
@@ -448,7 +448,7 @@ __device__ __forceinline__ bool walk_wave(const skip::GridView& g, skip::Walk& w
                     if (!(w.t < bound)) {
                         mode = kMiss;
                     } else {
-                        const int cls = skip::classify_dfp<MINC>(w, g, pl);
+                        const int cls = skip::classify_dfp_o<MINC>(w, g, opar);
                         if (cls == 0) {
                             ++cells;
                             mode = kHit;
@@ -493,7 +493,7 @@ __device__ __forceinline__ bool walk_wave(const skip::GridView& g, skip::Walk& w
         VPX_MARK("skip phase");
         if (mode == kSkip) {
             uint32_t lo[3], hi[3];
-            skip::df_box(w, g.n, lo, hi);
+            skip::df_box(w, g.n, skip::cube_dfp(w), lo, hi);
             const int sr = skip::skip_box_lean<kSeg2Branch>(w, lo, hi, bound, cells);  // 2 (refused): a plain step
             VPX_MARK("skip end");
             VPX_PH(fb += __popcll(__ballot(sr == 2));)

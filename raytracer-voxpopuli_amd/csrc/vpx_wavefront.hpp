@@ -825,22 +825,6 @@ __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_BOUNCE : VPX_WPE_MULTI_N
     nearest_tile<ONE>(sv, w, ctr);
 }
 
-#ifndef VPX_FUSE_LEVEL
-#define VPX_FUSE_LEVEL 0
-#endif
-// (VPX_FUSE_LEVEL A/B) a bounce level's FindNearest walks and the next level's material
-// switch in one launch: the tile's walks, a workgroup barrier (the hit records the tile's
-// walkers wrote to HBM are then visible to the tile), each thread's shade.
-template <bool ONE>
-__global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_BOUNCE : VPX_WPE_MULTI_NEAREST) void k_nearest_shade(
-    SceneView sv, FrameArgs f, WaveBufs w, int level, unsigned long long* __restrict__ ctr) {
-    nearest_tile<ONE>(sv, w, ctr);
-    __syncthreads();
-    Counters ks{0u, 0u, 0u};
-    shade_path(sv, f, w, PathRay{w.O, w.D, w.H, w.HM, 0u}, tile_block() * 256u + threadIdx.x, level, ks);
-    flush_counters(ks, 0u, ctr, VPX_STAGE_SHADE);
-}
-
 // Renderer::IsOccluded for the shadow slots of a tile (entry = slot << 27 | path).  The
 // tile's slots are counting-sorted by the light they go to (LDS histogram, one wave's prefix
 // sum, the scatter), so a wave's lanes walk toward the same light and read the same
@@ -931,17 +915,6 @@ __device__ __forceinline__ void shadow_tile(const SceneView& sv, const WaveBufs&
 template <bool ONE>
 __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_SHADOW : VPX_WPE_MULTI_SHADOW) void k_shadow_tile(SceneView sv, WaveBufs w, unsigned long long* __restrict__ ctr) {
     shadow_tile<ONE>(sv, w, ctr);
-}
-
-// (VPX_FUSE_LEVEL A/B) a non-last level's IsOccluded walks and light sums in one launch: the
-// occluded flags in the tile's LDS bitmap, a barrier, each thread's resolve into LB.
-template <bool ONE>
-__global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_SHADOW : VPX_WPE_MULTI_SHADOW) void k_shadow_resolve(
-    SceneView sv, WaveBufs w, unsigned long long* __restrict__ ctr) {
-    __shared__ uint32_t occ[kOccWords];
-    shadow_tile<ONE>(sv, w, ctr, occ);
-    __syncthreads();
-    resolve_path(sv, w, tile_block() * 256u + threadIdx.x, occ);
 }
 
 // ------------------------------------------------------------------- stage 4

@@ -45,7 +45,7 @@ static World make_world(uint32_t n, uint64_t seed, double density) {
     return w;
 }
 
-// classify_dfp (octant plane, then the mask of an occupied brick) == classify (l1 + l2
+// classify_dfp (octant plane, then the mask of an occupied brick) == classify_dfp_o == classify (l1 + l2
 // words) at sampled cells for every octant: the same class and the same m1 where it is read
 // (the cell mask of an occupied brick, the octant's cube byte of an empty one).
 static long check_planes(const World& W, std::mt19937_64& r) {
@@ -60,10 +60,11 @@ static long check_planes(const World& W, std::mt19937_64& r) {
             a.X = (uint32_t)(c % W.n), a.Y = (uint32_t)((c / W.n) % W.n), a.Z = (uint32_t)(c / ((uint64_t)W.n * W.n));
             a.sx = (o & 1) ? -1 : 1, a.sy = (o & 2) ? -1 : 1, a.sz = (o & 4) ? -1 : 1;
             walk_begin(a);
-            Walk b = a;
+            Walk b = a, d = a;
             const int ca = classify(a, g), cb = classify_dfp(b, g, g.dfp + o * g.plane);
-            const bool m1_read = ca == 1 || ca == 0 ? a.m1 == b.m1 : ((a.m1 >> a.osh) & 255u) == ((b.m1 >> b.osh) & 255u);
-            if (ca != cb || !m1_read) {
+            const int cd = classify_dfp_o(d, g, plane_parent(g, o));  // the walkers' form
+            const bool m1_read = ca == 1 || ca == 0 ? a.m1 == b.m1 : cube_l1(a) == cube_dfp(b);
+            if (ca != cb || !m1_read || cd != cb || d.m1 != b.m1) {
                 if (bad < 5) printf("plane mismatch n=%u cell (%u,%u,%u) octant %u: class %d/%d\n", W.n, a.X, a.Y, a.Z, o, ca, cb);
                 ++bad;
             }
@@ -144,7 +145,7 @@ static void debug_walk(const GridView& g, Walk w, float bound) {
         if (cls == 0) return;
         if (cls == 2) {
             uint32_t lo[3], hi[3];
-            df_box(w, g.n, lo, hi);
+            df_box(w, g.n, cube_l1(w), lo, hi);
             Walk a = w, b = w;
             uint32_t ca = 0, cb = 0;
             const int ra = skip_box_lean(a, lo, hi, bound, ca), rb = skip_box(b, lo, hi, bound, cb);

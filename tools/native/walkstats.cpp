@@ -127,7 +127,7 @@ extern "C" void walk_sim(const uint8_t* cells, const uint64_t* l1, const uint64_
             if (cls == 2) {
                 ++skips;
                 uint32_t lo[3], hi[3];
-                df_box(w, n, lo, hi);
+                df_box(w, n, cube_l1(w), lo, hi);
                 if (slab) for (int q = 0; q < 3; ++q) lo[q] = slo[q], hi[q] = shi[q];
                 const uint32_t olo[3] = {lo[0], lo[1], lo[2]}, ohi[3] = {hi[0], hi[1], hi[2]};
                 {
