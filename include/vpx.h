@@ -301,8 +301,10 @@ int vpx_gl_unmap(vpx_ctx* ctx);
 int vpx_render(vpx_ctx* ctx, const vpx_frame_params* params, float* accum, uint32_t* rgb8,
                vpx_stats* stats);
 /* Tile-sharded variant for multi-GPU: render the tiles t (tile_w x tile_h, row-major tile
-   order) with t % n_ranks == rank into a packed float4 buffer (tile after tile, row-major
-   inside a tile; partial edge tiles padded with zeros).  DEVICE pointer.                */
+   order) with t % n_ranks == rank into a packed float4 buffer (tile after tile; inside a
+   16x16 tile entry i is pixel (8*((i>>6)&1) + (i&7), 8*(i>>7) + ((i>>3)&7)): the four 8x8
+   quadrants in row-major order, row-major inside each; partial edge tiles padded with
+   zeros).  DEVICE pointer.                                                               */
 int vpx_render_tiles(vpx_ctx* ctx, const vpx_frame_params* params, uint32_t tile_w,
                      uint32_t tile_h, uint32_t rank, uint32_t n_ranks, float* packed,
                      vpx_stats* stats);

@@ -3,7 +3,7 @@
 // Kernels:
 //   k_nearest / k_shade / k_shadow / k_finish   the frame as a wavefront of small kernels
 //                                 per bounce level (vpx_wavefront.hpp); one lane per pixel,
-//                                 16x16-pixel tiles per 256-thread workgroup (16x4 wave strips)
+//                                 16x16-pixel tiles per 256-thread workgroup (8x8 pixels per wave)
 //   composite_tiles               rank-0 unpack + accumulate + tonemap of gathered tiles.
 //   composite_rgb8                rank-0 unpack of gathered RGB8 tiles (sharded accumulator).
 //   find_nearest_k / is_occluded_k / trace_k   per-ray unit entries.
@@ -33,7 +33,8 @@ constexpr int kThreads = 256;
 __global__ __launch_bounds__(kThreads) void composite_tiles(FrameArgs f, const float4* __restrict__ gathered,
                                                             float4* __restrict__ accum, uint32_t* __restrict__ rgb8) {
     const uint32_t tile = blockIdx.x;
-    const uint32_t lx = threadIdx.x & 15u, ly = threadIdx.x >> 4;
+    uint32_t lx, ly;
+    tile_lane_xy(threadIdx.x, lx, ly);
     const uint32_t x = (tile % f.tiles_x) * kTile + lx;
     const uint32_t y = (tile / f.tiles_x) * kTile + ly;
     if (x >= f.width || y >= f.height) return;
@@ -67,7 +68,8 @@ __global__ __launch_bounds__(kThreads) void blend_packed(FrameArgs f, const floa
 __global__ __launch_bounds__(kThreads) void composite_rgb8(FrameArgs f, const uint32_t* __restrict__ gathered,
                                                            uint32_t* __restrict__ rgb8) {
     const uint32_t tile = blockIdx.x;
-    const uint32_t lx = threadIdx.x & 15u, ly = threadIdx.x >> 4;
+    uint32_t lx, ly;
+    tile_lane_xy(threadIdx.x, lx, ly);
     const uint32_t x = (tile % f.tiles_x) * kTile + lx;
     const uint32_t y = (tile / f.tiles_x) * kTile + ly;
     if (x >= f.width || y >= f.height) return;
@@ -993,8 +995,13 @@ int vpx_set_pipeline(vpx_ctx* c, uint32_t depth) {
     free_lanes(c);
     if (depth < 2) return VPX_OK;
     c->lanes.resize(depth);
+#ifndef VPX_LANE_PRIORITY
+#define VPX_LANE_PRIORITY 0
+#endif
+    int prio_lo = 0, prio_hi = 0;
+    VPX_HIP(c, hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
     for (auto& L : c->lanes) {
-        if (hipStreamCreateWithFlags(&L.s, hipStreamNonBlocking) != hipSuccess ||
+        if (hipStreamCreateWithPriority(&L.s, hipStreamNonBlocking, VPX_LANE_PRIORITY ? prio_hi : prio_lo) != hipSuccess ||
             hipEventCreateWithFlags(&L.rendered, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&L.consumed, hipEventDisableTiming) != hipSuccess) {
             free_lanes(c);

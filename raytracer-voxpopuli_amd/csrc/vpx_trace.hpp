@@ -702,7 +702,7 @@ __device__ __forceinline__ bool tlas_box(const TlasNode& nd, f3 o, f3 inv, float
 // The volume loop of Renderer::FindNearest / IsOccluded over the TLAS.  Volume 0 (the world,
 // first in the reference's order) is walked by every lane first; then the wave traverses the
 // tree once, wave-uniform (a node is entered when any lane's segment reaches its box: the
-// ray packet of a 16x4 pixel strip), each lane collecting the leaves IT reaches before its
+// ray packet of an 8x8 pixel block), each lane collecting the leaves IT reaches before its
 // bound as it stands after volume 0.  Every volume whose walk the reference would start and
 // read a cell of is among them (boxes hold the inflated bounding spheres of misses_volume,
 // and a box starting beyond the bound holds a cube whose walk ends before its first cell,

@@ -128,14 +128,23 @@ __device__ __forceinline__ Ray primary_ray(const FrameArgs& f, uint32_t x, uint3
     return make_ray(cp, P - cp);
 }
 
+// Lane -> pixel inside a 16x16 tile: the tile's four waves take its four 8x8 quadrants
+// (row-major quadrant order), each row-major inside — a wave's rays leave from an 8x8 block
+// rather than a 16x4 strip, so their walks overlap more (C1 / C3 -0.3 / -0.5 %, three
+// interleaved A/B rounds).  Also the order of a tile's 256 entries in the packed buffers.
+__device__ __forceinline__ void tile_lane_xy(uint32_t lane, uint32_t& lx, uint32_t& ly) {
+    lx = ((lane >> 6) & 1u) * 8u + (lane & 7u);
+    ly = (lane >> 7) * 8u + ((lane >> 3) & 7u);
+}
 // Path index -> pixel: path p = j*256 + lane covers the j-th tile of this rank
-// (tile = rank + j*n_ranks), lane in row-major order inside the 16x16 tile, so one
-// wave owns a 16x4 strip of neighbouring pixels.
+// (tile = rank + j*n_ranks), lane as tile_lane_xy.
 __device__ __forceinline__ bool path_pixel(const FrameArgs& f, uint32_t p, uint32_t& x, uint32_t& y) {
     const uint32_t j = p >> 8, lane = p & 255u;
     const uint32_t tile = f.rank + j * f.n_ranks;
-    x = (tile % f.tiles_x) * kTileW + (lane & 15u);
-    y = (tile / f.tiles_x) * kTileW + (lane >> 4);
+    uint32_t lx, ly;
+    tile_lane_xy(lane, lx, ly);
+    x = (tile % f.tiles_x) * kTileW + lx;
+    y = (tile / f.tiles_x) * kTileW + ly;
     return tile < f.num_tiles && x < f.width && y < f.height;
 }
 
@@ -1041,7 +1050,7 @@ __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_SHADOW : VPX_WPE_MULTI_S
 // 0.713; rank 0's share of C1 at 8 ranks 0.297 -> 0.228; C1 at 64x64 0.234 -> 0.198).  On
 // the big launches the two kernels stay apart (C3 5.84 vs 6.14; C4, 65 volumes, 59.3 vs
 // 64.5): there the separate kernels' 6 waves/SIMD pay more than the shared drain.  Running
-// each wave's 16x4 strip through the whole frame with wave-local compaction and no
+// each wave's pixels through the whole frame with wave-local compaction and no
 // workgroup barrier measured C1 0.725 vs 0.711 ms (the tile's barriers are not what sets the
 // small-launch floor; its longest walk chains are).
 #ifndef VPX_FUSE_FRAME_TILES

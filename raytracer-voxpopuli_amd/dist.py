@@ -3,8 +3,9 @@
 Layout contract (shared with libvpx_hip.so's vpx_render_tiles / vpx_composite_tiles):
   - the frame is cut into 16x16 tiles in row-major tile order, t = ty * tiles_x + tx;
   - tile t belongs to rank t % R (round-robin: spatially uneven cost is spread evenly);
-  - a rank's packed buffer holds its tiles in increasing t, 256 float4 each (row-major
-    inside the tile), edge tiles zero-padded; every rank's buffer has the same length
+  - a rank's packed buffer holds its tiles in increasing t, 256 float4 each in lane order
+    (tile_lanes: the tile's four 8x8 quadrants in row-major order, row-major inside each —
+    one wave each), edge tiles zero-padded; every rank's buffer has the same length
     ceil(num_tiles / R) * 256 so the gather is one fixed-size collective;
   - rank 0 receives the R buffers back to back and composites them (unpack + running-
     average accumulate + tonemap) into its accumulator and RGB8 screen.
@@ -37,11 +38,17 @@ def packed_len(width, height, n_ranks):
     return -(-(tx * ty) // n_ranks) * TILE * TILE
 
 
+def tile_lanes():
+    """(lx, ly) of a tile's 256 entries in packed order (csrc tile_lane_xy)."""
+    lane = np.arange(TILE * TILE)
+    return ((lane >> 6) & 1) * 8 + (lane & 7), (lane >> 7) * 8 + ((lane >> 3) & 7)
+
+
 def rank_pixel_ids(width, height, rank, n_ranks):
     """Pixel ids (y*W + x) in packed order for one rank; -1 marks padding."""
     tx, ty = tiles_xy(width, height)
     tiles = np.arange(rank, tx * ty, n_ranks)
-    ly, lx = np.divmod(np.arange(TILE * TILE), TILE)
+    lx, ly = tile_lanes()
     x = (tiles % tx)[:, None] * TILE + lx[None, :]
     y = (tiles // tx)[:, None] * TILE + ly[None, :]
     ids = np.where((x < width) & (y < height), y * width + x, -1).reshape(-1)
