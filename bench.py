@@ -53,10 +53,11 @@ import __graft_entry__ as entry  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 METRIC = "Mray/s (primary+shadow) at 1920×1080, 1024³ world; 1/2/4/8-GPU"
 EXTRA_CONFIGS = ("C2", "C3", "C4")
-# Frames in flight per config (vpx_set_pipeline lanes), from the A/B on one MI355X (DESIGN.md
-# §5; ms per step, 0 / 3 / 4 lanes): C1 0.647 / 0.606 / 0.585, C2 4.18 / 2.98 / 3.48,
-# C3 5.16 / 4.98 / 5.11, C4 55.9 / 51.9 / 51.2.
-PIPELINE = {"C1": 4, "C2": 3, "C3": 3, "C4": 4}
+# Frames in flight per config (vpx_set_pipeline lanes, each on a dedicated hardware queue),
+# from the A/B on one MI355X (ms per step, 2 / 3 / 4 lanes): C1 - / 0.551-0.554 /
+# 0.578-0.594, C2 2.94-2.95 / 2.89 / 2.99-3.02, C3 4.91-4.92 / 4.88-4.89 / 5.06-5.12,
+# C4 52.6 / 52.4 / 51.6.
+PIPELINE = {"C1": 3, "C2": 3, "C3": 3, "C4": 4}
 STAGE_KERNELS = {"primary": "k_primary", "shade": "k_shade", "shadow": "k_shadow_tile", "resolve": "k_resolve",
                  "bounce": "k_nearest_tile", "finish": "k_finish", "frame": "k_frame0"}
 

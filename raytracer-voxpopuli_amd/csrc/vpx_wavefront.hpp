@@ -879,7 +879,7 @@ __device__ __forceinline__ void shadow_tile(const SceneView& sv, const WaveBufs&
         if (threadIdx.x == 0) sh[0] = t;
     }
     __syncthreads();
-    total = sh[0];
+    total = __builtin_amdgcn_readfirstlane(sh[0]);  // wave-uniform: a scalar register
     {
         uint32_t at = m ? hist[key] + pos : 0u;
         for (uint32_t b = m; b; b &= b - 1u) lst_dyn[at++] = ((uint32_t)__ffs(b) - 1u) << 27 | p;
