@@ -222,7 +222,8 @@ int vpx_set_stream(vpx_ctx* ctx, void* hip_stream);
 int vpx_synchronize(vpx_ctx* ctx);
 /* Frames in flight (depth 2..4; 0 / 1 = off, the default).  With depth D, vpx_render and
    vpx_render_tiles_accum render each frame on the next of D library-owned streams ("lanes",
-   each with its own path-state buffers) into packed float4 samples, and queue only the
+   each with its own path-state buffers and its own hardware queue — CU-mask streams, outside
+   the GPU_MAX_HW_QUEUES pool the caller's streams share) into packed float4 samples, and queue only the
    frame's accumulate / tonemap / RGB8 pack (or the rank's packed running average) on the
    context's stream, after the previous frame's: frame f+1's walks run while frame f's last
    tiles drain.  Results are bit-identical (the same blend of the same sample, in frame order);
