@@ -225,6 +225,10 @@ def run_config(pkg, env, cfg, steps, warmup, weak=False, sha=None, pipeline=None
         # DESIGN.md §4): no separate finish stage, the shadow stage carries the 36 B per pixel
         fused = split.get("finish", (0.0, 0, 0, 0.0))[1] == 0  # stages with no launch stay in the table
         kernels = dict(STAGE_KERNELS)
+        if len(desc.volumes) == 1 and not (desc.spheres or desc.triangles):  # the pools
+            kernels["bounce"] = "k_nearest_pool"
+            if desc.areas and desc.area_samples > 1:
+                kernels.update(shadow="k_shadow_pool", finish="k_resolve_finish")
         if fused:
             kernels["shadow"] = "k_shadow_finish" if desc.max_bounces == 0 else "k_shadow_tile+k_shadow_finish"
         # rank 0's own work (its launches, cells and pixels)

@@ -411,6 +411,7 @@ __global__ void checksum_k(const uint8_t* __restrict__ cells, uint64_t count, un
 // =========================================================================== host side
 struct vpx_ctx {
     int device = 0;
+    uint32_t cus = 256;  // compute units of the device (the bounce pool's grid)
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
     std::string err;
@@ -687,7 +688,8 @@ int validate_frame(vpx_ctx* c, const vpx_frame_params* p) {
 int ensure_wave(vpx_ctx* c, vpx_ctx::WaveStore& ws, uint32_t P, uint32_t L, uint32_t S) {
     const size_t f4 = sizeof(float4);
     const size_t bytes = (size_t)P * (f4 * (5 + 2 * (size_t)L + 3 * (size_t)S + 1) + 3 * sizeof(uint32_t)) +
-                         sizeof(uint32_t) * (size_t)P + 16 * 256;
+                         sizeof(uint32_t) * (size_t)P + (size_t)P / 8 + sizeof(uint32_t) * 2 * kMaxLevels +
+                         (size_t)P * S + 19 * 256;
     if (bytes > ws.bytes) {
         if (ws.d) {
             VPX_HIP(c, sync_all(c));
@@ -721,6 +723,9 @@ int ensure_wave(vpx_ctx* c, vpx_ctx::WaveStore& ws, uint32_t P, uint32_t L, uint
     w.depth = (int32_t*)take(4 * (size_t)P);
     w.forms = (uint32_t*)take(4 * (size_t)P);
     w.smask = (uint32_t*)take(4 * (size_t)P);
+    w.amask = (uint64_t*)take((size_t)P / 8);  // P is a multiple of 256
+    w.pool = (uint32_t*)take(sizeof(uint32_t) * 2 * kMaxLevels);
+    w.occb = (uint8_t*)take((size_t)P * S);
     return VPX_OK;
 }
 
@@ -762,6 +767,21 @@ int launch_render(vpx_ctx* c, hipStream_t s, vpx_ctx::WaveStore& ws, const Scene
     // the last level's shadow -> resolve -> finish as one launch (k_shadow_finish), except
     // on the static-camera path, whose tail is the reprojection
     const bool fuse_tail = !rp;
+    // The shadow pool (k_shadow_pool, results in occb) for the single-volume walks towards area
+    // lights (several slots per path, long walks), except on the static-camera path (its
+    // reprojection test reads the tile kernel's SD flags).  Measured (ms per step, two runs
+    // each, pool / tile kernels): C3 3.72, 3.71 / 4.96, 4.94; C2 (one point light, one slot per
+    // path) 2.83, 2.84 / 2.64, 2.71 — so point / spot / directional lights keep the tile kernels.
+    const bool spool = one && !rp && S > 1;
+    if (!spool) w.occb = nullptr;  // k_resolve reads the slots' SD flags
+    const uint32_t sgrab = std::max(1u, std::min(4u, kShadowList / (64u * S)));
+    auto shadow_pool = [&](int level) {
+        const uint32_t grabs = (P / 64u + sgrab - 1u) / sgrab;
+        const uint32_t waves = std::min(grabs, c->cus * 4u * (uint32_t)VPX_WPE_SPOOL);
+        const uint32_t wpb = kPoolWg / 64u;
+        hipLaunchKernelGGL(k_shadow_pool, dim3((waves + wpb - 1u) / wpb), dim3(kPoolWg), 0, s, sv, w, level, sgrab,
+                           c->d_ctr);
+    };
     if (one && fuse_tail && f.max_bounces == 0 && tiles <= kFuseFrameTiles) {
         prof_mark(c, s, VPX_STAGE_FRAME);  // the whole depth-0 frame, one launch (k_frame0)
         if (S == 1)  // one slot per path: the tile's slots live in LDS too
@@ -790,20 +810,39 @@ int launch_render(vpx_ctx* c, hipStream_t s, vpx_ctx::WaveStore& ws, const Scene
         }
         if (fuse_tail && level == f.max_bounces) {
             prof_mark(c, s, VPX_STAGE_SHADOW);
-            hipLaunchKernelGGL((one ? k_shadow_finish<true, MODE> : k_shadow_finish<false, MODE>), grid, block, slds,
-                               s, sv, f, w, c->d_ctr, accum, rgb8, packed);
+            if (spool)
+                shadow_pool(level);
+            else
+                hipLaunchKernelGGL((one ? k_shadow_finish<true, MODE> : k_shadow_finish<false, MODE>), grid, block,
+                                   slds, s, sv, f, w, c->d_ctr, accum, rgb8, packed);
             prof_mark(c, s, -1);
+            if (spool) {
+                prof_mark(c, s, VPX_STAGE_FINISH);
+                hipLaunchKernelGGL((k_resolve_finish<MODE>), grid, block, 0, s, sv, f, w, accum, rgb8, packed);
+                prof_mark(c, s, -1);
+            }
             break;
         }
         prof_mark(c, s, VPX_STAGE_SHADOW);
-        hipLaunchKernelGGL(one ? k_shadow_tile<true> : k_shadow_tile<false>, grid, block, slds, s, sv, w, c->d_ctr);
+        if (spool)
+            shadow_pool(level);
+        else
+            hipLaunchKernelGGL(one ? k_shadow_tile<true> : k_shadow_tile<false>, grid, block, slds, s, sv, w, c->d_ctr);
         prof_mark(c, s, -1);
         prof_mark(c, s, VPX_STAGE_RESOLVE);
         hipLaunchKernelGGL(k_resolve, grid, block, 0, s, sv, w);
         prof_mark(c, s, -1);
         if (level < f.max_bounces) {
             prof_mark(c, s, VPX_STAGE_BOUNCE);
-            hipLaunchKernelGGL(one ? k_nearest_tile<true> : k_nearest_tile<false>, grid, block, 0, s, sv, w, c->d_ctr);
+            if (one) {  // the bounce pool: persistent waves, as many as the device keeps resident
+                const uint32_t grabs = (P / 64u + kPoolGrab - 1u) / kPoolGrab;
+                const uint32_t waves = std::min(grabs, c->cus * 4u * (uint32_t)VPX_WPE_BOUNCE);
+                const uint32_t wpb = kPoolWg / 64u;
+                hipLaunchKernelGGL(k_nearest_pool, dim3((waves + wpb - 1u) / wpb), dim3(kPoolWg), 0, s, sv, w, level,
+                                   c->d_ctr);
+            } else {
+                hipLaunchKernelGGL(k_nearest_tile, grid, block, 0, s, sv, w, c->d_ctr);
+            }
             prof_mark(c, s, -1);
         }
     }
@@ -907,6 +946,9 @@ int vpx_create(int device, vpx_ctx** out) {
     vpx_ctx* c = new (std::nothrow) vpx_ctx();
     if (!c) return VPX_E_NOMEM;
     c->device = device;
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
+        c->cus = (uint32_t)cus;
     if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc(&c->d_ctr, kCtrWords * kCtrStripes * sizeof(unsigned long long)) != hipSuccess ||
         hipMalloc(&c->d_sum, sizeof(unsigned long long)) != hipSuccess ||

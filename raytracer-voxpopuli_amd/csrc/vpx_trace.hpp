@@ -416,16 +416,21 @@ __device__ unsigned long long g_phase[32];
 // Phases are wave-uniform: cell steps while enough lanes want one (see SKIPW), then the
 // waiting lanes skip together.  Each lane runs exactly skip::walk_skip's sequence (the
 // reference's cells with the reference's floats).
-template <int PHK, uint32_t SKIPW, uint32_t MINC, uint32_t RUN>
-__device__ __forceinline__ bool walk_wave(const skip::GridView& g, skip::Walk& w, float bound, uint32_t& cells) {
-    enum : int { kStep = 0, kSkip = 1, kMiss = 2, kHit = 3 };
+// POOL (the bounce pool, k_nearest_pool): the lanes' modes come in and go out through *pmode
+// (lanes without a ray are kWalkMiss), and the walk also returns, with its lanes' state intact,
+// once `leave` or more lanes of the wave have finished, so that their rays can be replaced.
+constexpr int kWalkStep = 0, kWalkSkip = 1, kWalkMiss = 2, kWalkHit = 3;
+template <int PHK, uint32_t SKIPW, uint32_t MINC, uint32_t RUN, bool POOL = false>
+__device__ __forceinline__ bool walk_wave(const skip::GridView& g, skip::Walk& w, float bound, uint32_t& cells,
+                                          int* pmode = nullptr, uint32_t leave = 65u) {
+    enum : int { kStep = kWalkStep, kSkip = kWalkSkip, kMiss = kWalkMiss, kHit = kWalkHit };
     constexpr int kRun = (int)(RUN & 255u);
     constexpr int kPasses = (int)((RUN >> 8) & 255u);
     constexpr bool kSeg2Branch = (RUN >> 17) & 1u;
     constexpr bool kMin2 = (RUN >> 18) & 1u;  // step1's two-compare axis choice (vpx_skip.hpp)
     static_assert(SKIPW > 0 && kRun > 0 && kPasses > 0, "walk_wave: skip weight, run cap and passes");
     const uint32_t opar = skip::plane_parent(g, w.osh >> 3);  // the ray's octant plane
-    int mode = kStep;
+    int mode = POOL ? *pmode : kStep;
     VPX_PH(uint64_t cs = 0, ck = 0, ns = 0, nk = 0, ls = 0, lk = 0, fb = 0, cf = 0;)
     for (;;) {
         VPX_PH(uint64_t t0 = __builtin_amdgcn_s_memtime();)
@@ -434,7 +439,9 @@ __device__ __forceinline__ bool walk_wave(const skip::GridView& g, skip::Walk& w
             if (!stepping) break;
             // cost-weighted: a skip phase costs several step phases, so keep stepping while
             // steppers x SKIPW >= waiting skippers
-            if ((uint32_t)__popcll(stepping) * SKIPW < (uint32_t)__popcll(__ballot(mode == kSkip))) break;
+            const uint32_t nskip = (uint32_t)__popcll(__ballot(mode == kSkip));
+            if ((uint32_t)__popcll(stepping) * SKIPW < nskip) break;
+            if (POOL && 64u - (uint32_t)__popcll(stepping) - nskip >= leave) goto pool_out;
             VPX_PH(++ns; ls += __popcll(stepping); cf += __popcll(__ballot(mode >= kMiss));)  // cf: finished lanes per step iteration
             VPX_MARK("step body");
             // Brick runs: the class of a cell is a function of its brick's plane byte and cell
@@ -505,6 +512,10 @@ __device__ __forceinline__ bool walk_wave(const skip::GridView& g, skip::Walk& w
             }
         }
         VPX_PH(ck += __builtin_amdgcn_s_memtime() - t1;)
+    }
+    if (POOL) {
+    pool_out:
+        *pmode = mode;
     }
 #ifdef VPX_PHASE_PROF
     if ((threadIdx.x & 63) == __builtin_amdgcn_readfirstlane(threadIdx.x & 63)) {

@@ -93,6 +93,10 @@ struct WaveBufs {
     float4* SL;    // [S][P] unoccluded contribution of the slot
     float4* SM;    // [P] pending light: xyz = kd (area), w = bits(kind | discard<<3 | count<<4 | level<<8 | lc<<16)
     uint32_t* smask;  // [P] shadow slots emitted this level (bit s = slot s, s < 15) | light key << 16
+    uint64_t* amask;  // [P/64] bit p & 63 of word p >> 6: path p traces a next ray (the shades write it)
+    uint32_t* pool;   // [2 * kMaxLevels] the pools' grab counters: bounce walks of level l at [l], shadow walks
+                      // at [kMaxLevels + l] (k_primary zeroes them)
+    uint8_t* occb;    // [S][P] the shadow pool's result per slot: 1 = occluded (valid slots only)
     float4* RD;    // [W*H] reprojection: level-0 intersection point, w = material bits (image order)
     uint32_t P;    // paths (pixels) this call
     uint32_t S;    // shadow slots per path
@@ -335,10 +339,12 @@ __device__ __forceinline__ void wave_sync() {
 // L0: the call shades level 0 (the fused head in k_primary).  Level 0 rays are primary
 // rays, which never start inside glass or smoke, so the interior exit marches (a whole DDA
 // walker each) drop out of that instance; the forms word is known (no levels yet).
+// Returns whether the path traces a next ray (the bounce pool's mask bit).
 template <bool L0 = false>
-__device__ __forceinline__ void shade_path(const SceneView& sv, const FrameArgs& f, const WaveBufs& w,
+__device__ __forceinline__ bool shade_path(const SceneView& sv, const FrameArgs& f, const WaveBufs& w,
                                            const PathRay& pr, uint32_t p, int level, Counters& k) {
     uint32_t slots = 0;
+    bool cont = false;
     if (p < w.P) {
         float4 od = pr.D[pr.at(p)];
         uint32_t flags = __float_as_uint(od.w);
@@ -493,6 +499,7 @@ __device__ __forceinline__ void shade_path(const SceneView& sv, const FrameArgs&
                     w.O[p] = make_float4(next.O.x, next.O.y, next.O.z, __uint_as_float(g.s));
                     w.D[p] = make_float4(next.D.x, next.D.y, next.D.z, __uint_as_float(flags));
                     w.depth[p] = depth;
+                    cont = true;
                 }
                 // else: the child Trace(depth < 0) returns 0 (the leaf k_primary zeroed).
                 // Only the last level gets here (depth starts at max_bounces) and no kernel
@@ -509,12 +516,20 @@ __device__ __forceinline__ void shade_path(const SceneView& sv, const FrameArgs&
         if (!pending) w.SM[p] = make_float4(0.f, 0.f, 0.f, __uint_as_float(0u));
     }
     if (p < w.P) w.smask[p] = slots;
+    return cont;
+}
+
+// The bounce pool's mask word of this wave's 64 paths (p = the wave's first path + lane).
+__device__ __forceinline__ void put_amask(const WaveBufs& w, uint32_t p, bool cont) {
+    const uint64_t b = __ballot(cont);
+    if ((threadIdx.x & 63u) == 0 && p < w.P) w.amask[p >> 6] = b;
 }
 
 __global__ __launch_bounds__(256) void k_shade(SceneView sv, FrameArgs f, WaveBufs w, int level,
                                                unsigned long long* ctr) {
     Counters k{0u, 0u, 0u};
-    shade_path(sv, f, w, PathRay{w.O, w.D, w.H, w.HM, 0u}, blockIdx.x * 256u + threadIdx.x, level, k);
+    const uint32_t p = blockIdx.x * 256u + threadIdx.x;
+    put_amask(w, p, shade_path(sv, f, w, PathRay{w.O, w.D, w.H, w.HM, 0u}, p, level, k));
     flush_counters(k, 0u, ctr, VPX_STAGE_SHADE);
 }
 
@@ -542,7 +557,9 @@ __device__ __forceinline__ void resolve_path(const SceneView& sv, const WaveBufs
         const uint64_t i = (uint64_t)s * w.P + p;
         if (!((valid >> s) & 1u)) continue;
         const uint32_t b = s * 256u + (p & 255u);
-        if (occ ? (occ[b >> 5] >> (b & 31u)) & 1u : __float_as_uint(w.SD[i].w) & 4u /* kSlotOcc */) continue;
+        if (occ ? (occ[b >> 5] >> (b & 31u)) & 1u
+                : w.occb ? (uint32_t)w.occb[i] : __float_as_uint(w.SD[i].w) & 4u /* kSlotOcc */)
+            continue;
         const float4 v = w.SL[i];
         if (kind == kLightArea)
             acc = acc + mk(v.x, v.y, v.z);
@@ -717,6 +734,7 @@ __device__ __forceinline__ void primary_tile(const SceneView& sv, const FrameArg
     Counters k{0u, 0u, 0u};
     uint32_t prim = 0;
     bool walk = false;
+    if (blockIdx.x == 0 && threadIdx.x < 2u * kMaxLevels && w.pool) w.pool[threadIdx.x] = 0u;  // the frame's pools
     if (p < w.P) {
         uint32_t x, y;
         bool go = path_pixel(f, p, x, y);
@@ -781,7 +799,8 @@ __device__ __forceinline__ void primary_tile(const SceneView& sv, const FrameArg
     if (SHADE) {  // level 0's material switch for this thread's own path (k_primary_shade)
         __syncthreads();  // the tile's hit records, written by the compacted walkers
         Counters ks{0u, 0u, 0u};
-        shade_path<true>(sv, f, w, pr, p, 0, ks);
+        const bool cont = shade_path<true>(sv, f, w, pr, p, 0, ks);
+        if (f.max_bounces > 0) put_amask(w, p, cont);
         flush_counters(ks, 0u, ctr, VPX_STAGE_SHADE);
     }
 }
@@ -801,8 +820,9 @@ __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_NEAREST : VPX_WPE_MULTI_
 // order of a counting sort by (direction octant, Morton index of the origin's 16^3-cell
 // region): the sorted walker took 553 vs 541 us per level on C2 and the sort 350 us more —
 // coherent starts do not shorten the walks, whose cost is their length and step latency.
-template <bool ONE>
-__device__ __forceinline__ void nearest_tile(const SceneView& sv, const WaveBufs& w, unsigned long long* __restrict__ ctr) {
+// Multi-volume / shape scenes (the single-volume scenes walk their bounces in the pool below).
+__global__ __launch_bounds__(256) VPX_WPE(VPX_WPE_MULTI_NEAREST) void k_nearest_tile(SceneView sv, WaveBufs w,
+                                                                                    unsigned long long* __restrict__ ctr) {
     __shared__ uint32_t sh[4];
     __shared__ uint32_t lst[256];
     const uint32_t base = tile_block() * 256u;
@@ -815,23 +835,103 @@ __device__ __forceinline__ void nearest_tile(const SceneView& sv, const WaveBufs
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < total; i += 256u) {
         const uint32_t q = lst[i];
-        if (ONE) {
-            nearest_record_1v<kSkipwBounce, kMincBounce, kRunBounce>(sv, PathRay{w.O, w.D, w.H, w.HM, 0u}, q, k);
-        } else {
-            const float4 o = w.O[q], d = w.D[q];
-            Ray r;
-            r.O = mk(o.x, o.y, o.z);
-            r.D = mk(d.x, d.y, d.z);
-            r.inside = (__float_as_uint(d.w) & kInside) != 0u;
-            nearest_record<kSkipwBounce, kMincBounce, kRunBounce>(sv, PathRay{w.O, w.D, w.H, w.HM, 0u}, q, r, k);
-        }
+        const float4 o = w.O[q], d = w.D[q];
+        Ray r;
+        r.O = mk(o.x, o.y, o.z);
+        r.D = mk(d.x, d.y, d.z);
+        r.inside = (__float_as_uint(d.w) & kInside) != 0u;
+        nearest_record<kSkipwBounce, kMincBounce, kRunBounce>(sv, PathRay{w.O, w.D, w.H, w.HM, 0u}, q, r, k);
     }
     flush_counters(k, 0u, ctr, VPX_STAGE_BOUNCE);
 }
 
-template <bool ONE>
-__global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_BOUNCE : VPX_WPE_MULTI_NEAREST) void k_nearest_tile(SceneView sv, WaveBufs w, unsigned long long* __restrict__ ctr) {
-    nearest_tile<ONE>(sv, w, ctr);
+// The bounce pool (single-volume scenes): Renderer::FindNearest for the level's traced rays,
+// walked by persistent waves that refill their finished lanes.  A tile's bounce walks are
+// heavy-tailed (C2: of a walk iteration's 64 lanes 16 step, 9 wait to skip and 39 are already
+// done), and a tile's ~90 bounce rays leave its second wave mostly empty; here each wave takes
+// the next kPoolGrab x 64 paths at a time (one global atomic), lists the traced ones of them in
+// its LDS (their bits in the shades' amask words), and hands them to its lanes as lanes free up:
+// the walk returns once kPoolLeave lanes have finished, their hit records are written, and new
+// rays start in their place while the others keep their walk state.  Every ray is walked by
+// exactly the per-lane sequence of nearest_record_1v (same cells, same counts, same records);
+// only which lane and when differ.  Waves are independent (no barriers; four per workgroup).
+// Measured (C2, ms per step, three interleaved runs each): tile kernel 3.03 / 3.01 / 3.03,
+// pool 2.72 / 2.68 / 2.70; 64-thread workgroups 2.83 / 2.82 / 2.77; leave at 8 finished lanes
+// 2.75 / 2.73 / 2.74, at 32 2.71 / 2.72 / 2.65; grabs of 2 words 2.84 / 2.77 / 2.82, of 8
+// 2.79 / 2.79 / 2.71.
+#ifndef VPX_POOL_GRAB
+#define VPX_POOL_GRAB 4
+#endif
+#ifndef VPX_POOL_LEAVE
+#define VPX_POOL_LEAVE 16
+#endif
+#ifndef VPX_POOL_WG
+#define VPX_POOL_WG 256
+#endif
+constexpr uint32_t kPoolGrab = VPX_POOL_GRAB;    // mask words (x 64 paths) per grab
+constexpr uint32_t kPoolLeave = VPX_POOL_LEAVE;  // finished lanes that end a walk while rays are left
+constexpr uint32_t kPoolWg = VPX_POOL_WG;        // threads per workgroup (its waves are independent)
+__device__ __forceinline__ uint32_t lane_rank(uint64_t m) {  // set bits of m below this lane
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+__global__ __launch_bounds__(kPoolWg) VPX_WPE(VPX_WPE_BOUNCE) void k_nearest_pool(SceneView sv, WaveBufs w, int level,
+                                                                               unsigned long long* __restrict__ ctr) {
+    __shared__ uint32_t lst_wg[kPoolWg / 64][kPoolGrab * 64];
+    uint32_t* lst = lst_wg[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)];
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t words = (w.P + 63u) >> 6, grabs = (words + kPoolGrab - 1u) / kPoolGrab;
+    const PathRay pr{w.O, w.D, w.H, w.HM, 0u};
+    const skip::GridView gv = grid_view(sv.grids[uni_ptr(&sv.volumes[0])->grid_id]);
+    Counters k{0u, 0u, 0u};
+    skip::Walk wk;
+    uint32_t q = ~0u;     // the path this lane walks (~0u: none)
+    int mode = kWalkMiss;
+    uint32_t avail = 0u, cur = 0u;  // listed paths not yet handed out, and where they start
+    bool more = true;               // paths may be left in the pool
+    for (;;) {
+        if (q != ~0u && mode >= kWalkMiss) {  // finished: its hit record
+            nearest_end_1v(sv, pr, q, wk, mode == kWalkHit);
+            q = ~0u;
+        }
+        while (more) {
+            const uint64_t idle = __ballot(q == ~0u);
+            if (!idle) break;
+            if (avail == 0u) {  // take the next paths from the pool and list the traced ones
+                uint32_t g = 0u;
+                if (lane == 0u) g = atomicAdd(&w.pool[level], 1u);
+                g = __builtin_amdgcn_readfirstlane(g);
+                if (g >= grabs) {
+                    more = false;
+                    break;
+                }
+                wave_sync();  // the wave's earlier reads of lst are done
+                uint32_t n = 0u;
+#pragma unroll
+                for (uint32_t j = 0; j < kPoolGrab; ++j) {
+                    const uint32_t wi = g * kPoolGrab + j;
+                    const uint64_t m = wi < words ? w.amask[wi] : 0ull;
+                    if ((m >> lane) & 1ull) lst[n + lane_rank(m)] = wi * 64u + lane;
+                    n += (uint32_t)__popcll(m);
+                }
+                wave_sync();
+                avail = n;
+                cur = 0u;
+                continue;
+            }
+            const uint32_t take = min((uint32_t)__popcll(idle), avail);
+            const uint32_t r = lane_rank(idle);
+            if (q == ~0u && r < take) {
+                q = lst[cur + r];
+                mode = nearest_begin_1v(sv, pr, q, k, wk) ? kWalkStep : kWalkMiss;
+            }
+            cur += take;
+            avail -= take;
+        }
+        if (!__ballot(q != ~0u)) break;  // the pool is empty and every lane is done
+        walk_wave<0, kSkipwBounce, kMincBounce, kRunBounce, true>(gv, wk, kBig, k.cells, &mode,
+                                                                   more ? kPoolLeave : 65u);
+    }
+    flush_counters(k, 0u, ctr, VPX_STAGE_BOUNCE);
 }
 
 // Renderer::IsOccluded for the shadow slots of a tile (entry = slot << 27 | path).  The
@@ -926,6 +1026,119 @@ __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_SHADOW : VPX_WPE_MULTI_S
     shadow_tile<ONE>(sv, w, ctr);
 }
 
+// The shadow pool (single-volume scenes): Renderer::IsOccluded for a level's shadow slots,
+// walked by persistent waves that refill their finished lanes, as the bounce pool does for
+// FindNearest.  A grab is `grab` mask words of paths (64 each, at most kShadowList slots);
+// their slots are listed in the wave's LDS grouped by light key (the tile kernels' bucketing:
+// a wave's lanes head for the same light), entry = slot << 27 | path.  Each slot's result goes
+// to occb (1 = occluded) for k_resolve / k_resolve_finish; a slot is walked by exactly
+// shadow_tile's per-lane sequence, so counts and occlusion are the same.
+constexpr uint32_t kShadowList = 1024;  // listed slots per wave (LDS: 4 KiB)
+// At 7 waves/SIMD (72 VGPRs) it spilled 29 VGPRs, 21 scratch accesses inside the skip phase;
+// at 5 (96 VGPRs) one.  Measured C3 (ms, two runs each): 7 -> 4.85 / 4.81, 6 -> 3.83 / 3.80,
+// 5 -> 3.72 / 3.71, against 4.96 / 4.94 for the tile kernels.
+#ifndef VPX_WPE_SPOOL
+#define VPX_WPE_SPOOL 5
+#endif
+__global__ __launch_bounds__(kPoolWg) VPX_WPE(VPX_WPE_SPOOL) void k_shadow_pool(SceneView sv, WaveBufs w, int level,
+                                                                              uint32_t grab,
+                                                                              unsigned long long* __restrict__ ctr) {
+    __shared__ uint32_t lst_wg[kPoolWg / 64][kShadowList];
+    __shared__ uint32_t hist_wg[kPoolWg / 64][kLightKeys];
+    uint32_t* lst = lst_wg[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)];
+    uint32_t* hist = hist_wg[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)];
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t words = (w.P + 63u) >> 6, grabs = (words + grab - 1u) / grab;
+    const vpx_volume* vol = uni_ptr(&sv.volumes[0]);
+    const DevGrid g = sv.grids[vol->grid_id];
+    const skip::GridView gv = grid_view(g);
+    Counters k{0u, 0u, 0u};
+    skip::Walk wk;
+    uint32_t e = ~0u;  // the slot entry this lane walks (~0u: none)
+    uint32_t walked = 0u;
+    float bound = 0.f;
+    int mode = kWalkMiss;
+    uint32_t avail = 0u, cur = 0u;
+    bool more = true;
+    for (;;) {
+        if (e != ~0u && mode >= kWalkMiss) {
+            w.occb[(uint64_t)(e >> 27) * w.P + (e & 0x07ffffffu)] = mode == kWalkHit ? 1u : 0u;
+            e = ~0u;
+        }
+        while (more) {
+            const uint64_t idle = __ballot(e == ~0u);
+            if (!idle) break;
+            if (avail == 0u) {
+                uint32_t gi = 0u;
+                if (lane == 0u) gi = atomicAdd(&w.pool[kMaxLevels + level], 1u);
+                gi = __builtin_amdgcn_readfirstlane(gi);
+                if (gi >= grabs) {
+                    more = false;
+                    break;
+                }
+                wave_sync();
+                // the grab's slots, grouped by light key: a counting sort over the wave (LDS
+                // histogram with atomics, the buckets' prefix sum, the scatter)
+                if (lane < kLightKeys) hist[lane] = 0u;
+                wave_sync();
+                uint32_t smv[4], pos[4];
+#pragma unroll
+                for (uint32_t j = 0; j < 4; ++j) {
+                    const uint32_t p = (gi * grab + j) * 64u + lane;
+                    smv[j] = (j < grab && p < w.P) ? w.smask[p] : 0u;
+                    const uint32_t m = smv[j] & kSlotBits;
+                    pos[j] = m ? atomicAdd(&hist[smv[j] >> 16], (uint32_t)__popc(m)) : 0u;
+                }
+                wave_sync();
+                uint32_t n;
+                const uint32_t ex = wave_prefix(lane < kLightKeys ? hist[lane] : 0u, n);
+                wave_sync();
+                if (lane < kLightKeys) hist[lane] = ex;
+                wave_sync();
+#pragma unroll
+                for (uint32_t j = 0; j < 4; ++j) {
+                    const uint32_t m = smv[j] & kSlotBits;
+                    if (m) {
+                        const uint32_t p = (gi * grab + j) * 64u + lane;
+                        uint32_t at = hist[smv[j] >> 16] + pos[j];
+                        for (uint32_t b = m; b; b &= b - 1u) lst[at++] = ((uint32_t)__ffs(b) - 1u) << 27 | p;
+                    }
+                }
+                wave_sync();
+                avail = n;
+                cur = 0u;
+                continue;
+            }
+            const uint32_t take = min((uint32_t)__popcll(idle), avail);
+            const uint32_t r = lane_rank(idle);
+            if (e == ~0u && r < take) {
+                e = lst[cur + r];
+                const uint64_t slot = (uint64_t)(e >> 27) * w.P + (e & 0x07ffffffu);
+                const float4 so = w.SO[slot], sd = w.SD[slot];
+                ORay o;
+                o.O = xform_pos(mk(so.x, so.y, so.z), vol->inv_matrix);
+                o.D = xform_vec(mk(sd.x, sd.y, sd.z), vol->inv_matrix);
+                o.rD = mk(__fdiv_rn(1.0f, o.D.x), __fdiv_rn(1.0f, o.D.y), __fdiv_rn(1.0f, o.D.z));
+                Dda s;
+                bound = so.w;
+                mode = kWalkMiss;
+                if (dda_setup(*vol, g.n, o, s)) {
+                    wk = to_walk(s);
+                    mode = kWalkStep;
+                }
+            }
+            cur += take;
+            avail -= take;
+            walked += take;  // IsOccluded calls (a scalar: no register across the walks)
+        }
+        if (!__ballot(e != ~0u)) break;
+        walk_wave<16, kSkipwShadow, kMincShadow, kRunShadow, true>(gv, wk, bound, k.cells, &mode,
+                                                                   more ? kPoolLeave : 65u);
+    }
+    k.shadow = lane == 0u ? walked : 0u;
+    flush_counters(k, 0u, ctr, VPX_STAGE_SHADOW);
+}
+
 // ------------------------------------------------------------------- stage 4
 // GetLuminance / ApplyReinhardJodie / RGBF32_to_RGB8 (renderer.cpp:2222-2240,
 // template/precomp.h:372-388).
@@ -1015,6 +1228,17 @@ template <int MODE>
 __global__ __launch_bounds__(256) void k_finish(FrameArgs f, WaveBufs w, float4* __restrict__ accum,
                                                 uint32_t* __restrict__ rgb8, float4* __restrict__ packed) {
     finish_path<MODE>(f, w, blockIdx.x * 256u + threadIdx.x, accum, rgb8, packed);
+}
+
+// The last level's resolve and the finish after the shadow pool (occb): k_shadow_finish's
+// per-path tail as its own launch.
+template <int MODE>
+__global__ __launch_bounds__(256) void k_resolve_finish(SceneView sv, FrameArgs f, WaveBufs w, float4* __restrict__ accum,
+                                                        uint32_t* __restrict__ rgb8, float4* __restrict__ packed) {
+    const uint32_t p = blockIdx.x * 256u + threadIdx.x;
+    LightSum ls;
+    resolve_path(sv, w, p, nullptr, &ls);
+    finish_path<MODE>(f, w, p, accum, rgb8, packed, &ls);
 }
 
 // The last level's tail in one launch: IsOccluded for the tile's shadow slots, then (after

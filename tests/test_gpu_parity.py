@@ -122,6 +122,29 @@ def test_depth_sweep_fused_head_tail(pkg, orc, depth, lights):
         assert s.bounce_rays == 0 and s.dda_cells == 0
 
 
+@pytest.mark.parametrize("samples,wh,depth", [(2, (16, 16), 0), (15, (40, 24), 2), (7, (96, 64), 1)])
+def test_pools_slot_counts(pkg, orc, samples, wh, depth):
+    """The pools: bounce walks of every level and the area-light shadow walks
+    by persistent waves that refill finished lanes.  Edges: one tile (a single grab), 15 slots
+    per path (a grab of one mask word, up to 960 listed slots per wave), 2 slots per path; the
+    shadow results go through occb to k_resolve (depth > 0) and k_resolve_finish."""
+    sc = pkg.scene
+    desc = sc.city_scene("roomGlass", 128, wh[0], wh[1], depth, areas=sc.C3_AREAS)
+    desc.area_samples = samples
+    acc_g, rgb_g, st = render_gpu(pkg, desc, frames=2)
+    o = orc.Oracle(pkg.abi, desc)
+    acc = None
+    ost = None
+    for f in range(2):
+        acc, rgb, ost = o.render(desc.frame_params(f), accum=acc)
+    assert np.array_equal(bits(acc_g), bits(acc))
+    assert np.array_equal(rgb_g, rgb)
+    s = st[-1]
+    assert (s.primary_rays, s.shadow_rays, s.bounce_rays, s.dda_cells) == (
+        ost.primary_rays, ost.shadow_rays, ost.bounce_rays, ost.dda_cells)
+    assert s.shadow_rays > 0
+
+
 @pytest.mark.parametrize("depth", [13, 14])
 def test_deepest_levels(pkg, orc, depth):
     """Renderer::maxBounces = 14 (renderer.h:175), the API's maximum: 15 levels of records
