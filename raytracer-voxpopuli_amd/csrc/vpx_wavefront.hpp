@@ -589,12 +589,13 @@ __global__ __launch_bounds__(256) void k_resolve(SceneView sv, WaveBufs w) {
 #ifndef VPX_WPE_NEAREST
 #define VPX_WPE_NEAREST 6
 #endif
+// The bounce pool (k_nearest_pool) at 5 (96 VGPRs, no spills): C2 2.62 / 2.64 vs 2.67 / 2.68 ms
+// at 6 (4 spills), 7: 2.78 / 2.82.
 #ifndef VPX_WPE_BOUNCE
-#define VPX_WPE_BOUNCE VPX_WPE_NEAREST
+#define VPX_WPE_BOUNCE 5
 #endif
 // Shadow kernels (k_shadow_tile, k_shadow_finish) at 7 with the octant planes (13 spilled
-// VGPRs): C3 5.68 -> 5.60 ms, C2 unchanged; 8 measured 6.03 / 4.51.  Bounce walks: 5 / 7
-// measured 4.35 / 4.29 vs 4.28 ms on C2, kept at 6.
+// VGPRs): C3 5.68 -> 5.60 ms, C2 unchanged; 8 measured 6.03 / 4.51.
 #ifndef VPX_WPE_SHADOW
 #define VPX_WPE_SHADOW 7
 #endif
