@@ -55,9 +55,9 @@ METRIC = "Mray/s (primary+shadow) at 1920×1080, 1024³ world; 1/2/4/8-GPU"
 EXTRA_CONFIGS = ("C2", "C3", "C4")
 # Frames in flight per config (vpx_set_pipeline lanes, each on a dedicated hardware queue),
 # from the A/B on one MI355X (ms per step, 2 / 3 / 4 lanes): C1 - / 0.551-0.554 /
-# 0.578-0.594, C2 2.94-2.95 / 2.89 / 2.99-3.02, C3 4.91-4.92 / 4.88-4.89 / 5.06-5.12,
-# C4 52.6 / 52.4 / 51.6.
-PIPELINE = {"C1": 3, "C2": 3, "C3": 3, "C4": 4}
+# 0.578-0.594, C4 52.6 / 52.4 / 51.6; with the pools (round 3) C2 2.76-2.77 / 2.50-2.52 /
+# 2.42-2.45, C3 3.70-3.71 / 3.65 / 3.67-3.71.
+PIPELINE = {"C1": 3, "C2": 4, "C3": 3, "C4": 4}
 STAGE_KERNELS = {"primary": "k_primary", "shade": "k_shade", "shadow": "k_shadow_tile", "resolve": "k_resolve",
                  "bounce": "k_nearest_tile", "finish": "k_finish", "frame": "k_frame0"}
 
