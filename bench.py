@@ -56,8 +56,9 @@ EXTRA_CONFIGS = ("C2", "C3", "C4")
 # Frames in flight per config (vpx_set_pipeline lanes, each on a dedicated hardware queue),
 # from the A/B on one MI355X (ms per step, 2 / 3 / 4 lanes): C1 - / 0.551-0.554 /
 # 0.578-0.594, C4 52.6 / 52.4 / 51.6; with the pools (round 3) C2 2.76-2.77 / 2.50-2.52 /
-# 2.42-2.45, C3 3.70-3.71 / 3.65 / 3.67-3.71.
-PIPELINE = {"C1": 3, "C2": 4, "C3": 3, "C4": 4}
+# 2.42-2.45 as the process's first config but 2.57-2.69 (3) vs 2.87-2.90 (4) as an extra
+# config after C1 (the line the driver runs), C3 3.70-3.71 / 3.65 / 3.67-3.71.
+PIPELINE = {"C1": 3, "C2": 3, "C3": 3, "C4": 4}
 STAGE_KERNELS = {"primary": "k_primary", "shade": "k_shade", "shadow": "k_shadow_tile", "resolve": "k_resolve",
                  "bounce": "k_nearest_tile", "finish": "k_finish", "frame": "k_frame0"}
 
@@ -227,8 +228,9 @@ def run_config(pkg, env, cfg, steps, warmup, weak=False, sha=None, pipeline=None
         kernels = dict(STAGE_KERNELS)
         if len(desc.volumes) == 1 and not (desc.spheres or desc.triangles):  # the pools
             kernels["bounce"] = "k_nearest_pool"
-            if desc.areas and desc.area_samples > 1:
-                kernels.update(shadow="k_shadow_pool", finish="k_resolve_finish")
+        if desc.areas and desc.area_samples > 1:  # area lights: the shadow pool (+ k_shadow_inst)
+            kernels.update(shadow="k_shadow_pool" if len(desc.volumes) == 1 and not (desc.spheres or desc.triangles)
+                           else "k_shadow_pool+k_shadow_inst", finish="k_resolve_finish")
         if fused:
             kernels["shadow"] = "k_shadow_finish" if desc.max_bounces == 0 else "k_shadow_tile+k_shadow_finish"
         # rank 0's own work (its launches, cells and pixels)

@@ -772,7 +772,10 @@ int launch_render(vpx_ctx* c, hipStream_t s, vpx_ctx::WaveStore& ws, const Scene
     // reprojection test reads the tile kernel's SD flags).  Measured (ms per step, two runs
     // each, pool / tile kernels): C3 3.72, 3.71 / 4.96, 4.94; C2 (one point light, one slot per
     // path) 2.83, 2.84 / 2.64, 2.71 — so point / spot / directional lights keep the tile kernels.
-    const bool spool = one && !rp && S > 1;
+    // Multi-volume / shape scenes: the world's walks (volume 0, first in IsOccluded's loop) in
+    // the pool, the rest of the loop in k_shadow_inst for the slots the world left unoccluded:
+    // C4 51.7 / 51.8 -> 47.6 / 47.7 ms per 16-spp step (shadow stage 2.13 -> 1.62 + 0.15 ms).
+    const bool spool = !rp && S > 1;
     if (!spool) w.occb = nullptr;  // k_resolve reads the slots' SD flags
     const uint32_t sgrab = std::max(1u, std::min(4u, kShadowList / (64u * S)));
     auto shadow_pool = [&](int level) {
@@ -781,6 +784,7 @@ int launch_render(vpx_ctx* c, hipStream_t s, vpx_ctx::WaveStore& ws, const Scene
         const uint32_t wpb = kPoolWg / 64u;
         hipLaunchKernelGGL(k_shadow_pool, dim3((waves + wpb - 1u) / wpb), dim3(kPoolWg), 0, s, sv, w, level, sgrab,
                            c->d_ctr);
+        if (!one) hipLaunchKernelGGL(k_shadow_inst, grid, block, slds, s, sv, w, c->d_ctr);
     };
     if (one && fuse_tail && f.max_bounces == 0 && tiles <= kFuseFrameTiles) {
         prof_mark(c, s, VPX_STAGE_FRAME);  // the whole depth-0 frame, one launch (k_frame0)

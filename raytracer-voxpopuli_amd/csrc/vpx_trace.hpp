@@ -818,7 +818,9 @@ __device__ __forceinline__ int32_t find_nearest(const SceneView& sv, Ray& r, Cou
 // Renderer::IsOccluded, renderer.cpp:209-243 (scalar transforms, exact 1/D).  The linear
 // volume loop: through the instance TLAS it measured slower (C4 IsOccluded 2.67 vs 2.57 ms:
 // most shadow rays end in the world volume, the rest cross the instance lattice).
-__device__ __forceinline__ bool is_occluded(const SceneView& sv, const Ray& r, Counters& k) {
+// first: the volume the loop starts at (k_shadow_inst: 1, after the shadow pool walked the
+// world, volume 0).
+__device__ __forceinline__ bool is_occluded(const SceneView& sv, const Ray& r, Counters& k, uint32_t first = 0) {
     bool occ = false;
     auto visit = [&](uint32_t i) {
         if (misses_volume(sv.vbounds[i], r.O, r.D)) return true;  // Setup3DDDA would fail
@@ -835,7 +837,7 @@ __device__ __forceinline__ bool is_occluded(const SceneView& sv, const Ray& r, C
         occ = walk_wave<16, kSkipwShadow, kMincShadow, kRunShadow>(grid_view(g), w, r.t, k.cells);
         return !occ;
     };
-    for (uint32_t i = 0; i < sv.num_volumes && !occ; ++i) visit(i);
+    for (uint32_t i = first; i < sv.num_volumes && !occ; ++i) visit(i);
     if (occ) return true;
     for (uint32_t i = 0; i < sv.num_spheres; ++i)
         if (sphere_is_hit(sv.spheres[i], r)) return true;

@@ -1140,6 +1140,39 @@ __global__ __launch_bounds__(kPoolWg) VPX_WPE(VPX_WPE_SPOOL) void k_shadow_pool(
     flush_counters(k, 0u, ctr, VPX_STAGE_SHADOW);
 }
 
+// Multi-volume / shape scenes with area lights: the rest of Renderer::IsOccluded for the slots
+// the world left unoccluded (k_shadow_pool walked volume 0, the first in the reference's loop,
+// renderer.cpp:209-243): volumes 1.. in order, then the shapes; an occluder sets the slot's
+// occb byte.  The slots' IsOccluded calls were counted by the pool.
+__global__ __launch_bounds__(256) VPX_WPE(VPX_WPE_MULTI_SHADOW) void k_shadow_inst(SceneView sv, WaveBufs w,
+                                                                                  unsigned long long* __restrict__ ctr) {
+    __shared__ uint32_t sh[4];
+    extern __shared__ uint32_t lst_dyn[];  // [S * 256]
+    const uint32_t p = tile_block() * 256u + threadIdx.x;
+    Counters k{0u, 0u, 0u};
+    const uint32_t m = p < w.P ? w.smask[p] & kSlotBits : 0u;
+    uint32_t mine = 0u;
+    for (uint32_t b = m; b; b &= b - 1u) {
+        const uint32_t sl = (uint32_t)__ffs(b) - 1u;
+        if (!w.occb[(uint64_t)sl * w.P + p]) mine |= 1u << sl;
+    }
+    uint32_t total;
+    uint32_t at = block_scan((uint32_t)__popc(mine), total, sh);
+    for (uint32_t b = mine; b; b &= b - 1u) lst_dyn[at++] = ((uint32_t)__ffs(b) - 1u) << 27 | p;
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < total; i += 256u) {
+        const uint32_t e = lst_dyn[i];
+        const uint64_t slot = (uint64_t)(e >> 27) * w.P + (e & 0x07ffffffu);
+        const float4 so = w.SO[slot], sd = w.SD[slot];
+        Ray r;
+        r.O = mk(so.x, so.y, so.z);
+        r.D = mk(sd.x, sd.y, sd.z);
+        r.t = so.w;
+        if (is_occluded(sv, r, k, 1u)) w.occb[slot] = 1u;
+    }
+    flush_counters(k, 0u, ctr, VPX_STAGE_SHADOW);
+}
+
 // ------------------------------------------------------------------- stage 4
 // GetLuminance / ApplyReinhardJodie / RGBF32_to_RGB8 (renderer.cpp:2222-2240,
 // template/precomp.h:372-388).

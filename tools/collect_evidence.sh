@@ -15,7 +15,7 @@ for c in C1 C2 C3 C4; do
   fi
   if [ -f $E/${TAG}_pmc_traffic_$c.json ]; then
     cp $E/${TAG}_pmc_traffic_$c.json profiles/
-    python tools/pmc_summary.py $E/pmc_$c > profiles/${TAG}_pmc_counters_$c.txt
+    python tools/pmc_summary.py $E/pmc_$c k_ composite blend > profiles/${TAG}_pmc_counters_$c.txt
   fi
 done
 if [ -f $E/share_C1.log ]; then grep -h 'R=1' $E/share_C*.log > profiles/${TAG}_rank_share.txt; fi
