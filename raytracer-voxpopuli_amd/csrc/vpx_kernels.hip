@@ -786,12 +786,11 @@ int launch_render(vpx_ctx* c, hipStream_t s, vpx_ctx::WaveStore& ws, const Scene
                            c->d_ctr);
         if (!one) hipLaunchKernelGGL(k_shadow_inst, grid, block, slds, s, sv, w, c->d_ctr);
     };
-    if (one && fuse_tail && f.max_bounces == 0 && tiles <= kFuseFrameTiles) {
-        prof_mark(c, s, VPX_STAGE_FRAME);  // the whole depth-0 frame, one launch (k_frame0)
-        if (S == 1)  // one slot per path: the tile's slots live in LDS too
-            hipLaunchKernelGGL((k_frame0<true, MODE, true>), grid, block, slds, s, sv, f, w, c->d_ctr, accum, rgb8, packed);
-        else
-            hipLaunchKernelGGL((k_frame0<true, MODE, false>), grid, block, slds, s, sv, f, w, c->d_ctr, accum, rgb8, packed);
+    if (one && fuse_tail && f.max_bounces == 0 && tiles <= kFuseFrameTiles && S == 1) {
+        // the whole depth-0 frame in one launch (k_frame0), its path state and one shadow slot
+        // per path in LDS; with area lights the frame splits to use the shadow pool
+        prof_mark(c, s, VPX_STAGE_FRAME);
+        hipLaunchKernelGGL((k_frame0<true, MODE>), grid, block, slds, s, sv, f, w, c->d_ctr, accum, rgb8, packed);
         prof_mark(c, s, -1);
         VPX_HIP(c, hipGetLastError());
         return VPX_OK;

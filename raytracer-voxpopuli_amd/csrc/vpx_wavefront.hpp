@@ -1323,14 +1323,17 @@ constexpr uint32_t kFuseFrameTiles = VPX_FUSE_FRAME_TILES;
 #endif
 // The depth-0 frame's path state never leaves the workgroup: a path is shaded, its light
 // resolved and its pixel finished by the same thread, and its shadow slots are walked by the
-// same tile, so the shade's records (LA / leaf, SM, forms, smask) and — with one slot per path
-// (LSLOT: no area lights) — the slots themselves (SO, SD, SL) live in LDS.  They reuse the
+// same tile, so the shade's records (LA / leaf, SM, forms, smask) and — one slot per path: the
+// kernel runs scenes without area lights only — the slots themselves (SO, SD, SL) live in LDS.
+// With area lights (several slots per path) the split frame with the shadow pool is faster
+// (C3's rank-0 share at 4 ranks, 8100 tiles: 1.31 ms through k_frame0 with its slots in HBM,
+// 2.6 x the 2-rank share).  They reuse the
 // head's regions once the head is done with them: the slots take the tile's ray records
 // (O / D / H: each thread reads its own path's before it writes its own slot), smask the hit
 // records, forms the walker list (dead after the walks' barrier).  The tile's WaveBufs view
 // points those arrays at LDS, shifted by the tile's first path so that path p indexes them
 // as p (level 0 and slot 0 only: every index is p).  HBM sees the accumulator / screen.
-template <bool ONE, int MODE, bool LSLOT>
+template <bool ONE, int MODE>
 __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_FRAME : VPX_WPE_MULTI_NEAREST) void k_frame0(
     SceneView sv, FrameArgs f, WaveBufs w, unsigned long long* __restrict__ ctr, float4* __restrict__ accum,
     uint32_t* __restrict__ rgb8, float4* __restrict__ packed) {
@@ -1346,11 +1349,9 @@ __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_FRAME : VPX_WPE_MULTI_NE
     wl.SM = s_sm - tb;
     wl.smask = L.hm - tb;
     wl.forms = L.lst - tb;
-    if (LSLOT) {
-        wl.SO = L.ray - tb;
-        wl.SD = L.ray + 256 - tb;
-        wl.SL = L.ray + 512 - tb;
-    }
+    wl.SO = L.ray - tb;
+    wl.SD = L.ray + 256 - tb;
+    wl.SL = L.ray + 512 - tb;
     primary_tile<ONE, true>(sv, f, wl, L, ctr);
     __syncthreads();
     shadow_tile<ONE>(sv, wl, ctr, occ);

@@ -254,10 +254,12 @@ def test_fused_frame_equals_two_launch_frame(pkg):
     """The depth-0 frame runs as one launch (k_frame0) up to kFuseFrameTiles (12288)
     tiles and as k_primary + k_shadow_finish above.  The same 2048x1600 frame (12800 tiles)
     rendered whole (two launches) and as two ranks' halves (6400 tiles each: fused) must
-    agree bit for bit over 2 AA frames with area lights; the profile names the stage each
-    path ran (frame vs primary + shadow) and the cells add up."""
+    agree bit for bit over 2 AA frames with the city's point and directional lights (one
+    shadow slot per path: k_frame0 keeps it in LDS; area lights take the split frame and the
+    shadow pool); the profile names the stage each path ran (frame vs primary + shadow) and
+    the cells add up."""
     sc = pkg.scene
-    desc = sc.city_scene("monu3", 128, 2048, 1600, 0, areas=sc.C3_AREAS[:2])
+    desc = sc.city_scene("monu3", 128, 2048, 1600, 0)
     desc.flags = pkg.abi.VPX_FLAG_AA
     W, H = desc.width, desc.height
     ctx = make_ctx(pkg, desc)
