@@ -396,6 +396,34 @@ constexpr uint32_t kMincNearest = 2, kMincBounce = 2, kMincShadow = 1;
 constexpr uint32_t kRunNearest = 3u | 2u << 8 | 1u << 17 | 1u << 18;
 constexpr uint32_t kRunBounce = 4u | 1u << 8 | 0u << 17 | 1u << 18;
 constexpr uint32_t kRunShadow = 3u | 1u << 8 | 1u << 17 | 0u << 18;
+// The pools' walks (k_nearest_pool, k_shadow_pool: 96 VGPRs at 5 waves/SIMD) have their own
+// words (A/B overrides: VPX_*_POOL).  With the pool's registers the shadow walks take the
+// two-compare step without spilling: C3 3.684-3.719 vs 3.724-3.756 ms (three interleaved runs,
+// round 3; skip weight 2 / 8 or skip minimum 2 on top: 3.70-3.73 / 3.70-3.72 / 3.77-3.78).
+// The bounce pool keeps the tile walker's words: seg2, skip weight 1 / 4, runs of 3 cells in
+// two passes measured C2 2.63-2.66 / 2.60-2.64 / 2.66-2.75 / 2.65-2.71 vs 2.59-2.65 ms.
+#ifndef VPX_RUN_SHADOW_POOL
+#define VPX_RUN_SHADOW_POOL (3u | 1u << 8 | 1u << 17 | 1u << 18)
+#endif
+#ifndef VPX_SKIPW_SHADOW_POOL
+#define VPX_SKIPW_SHADOW_POOL 4u
+#endif
+#ifndef VPX_MINC_SHADOW_POOL
+#define VPX_MINC_SHADOW_POOL 1u
+#endif
+#ifndef VPX_RUN_BOUNCE_POOL
+#define VPX_RUN_BOUNCE_POOL (4u | 1u << 8 | 0u << 17 | 1u << 18)
+#endif
+#ifndef VPX_SKIPW_BOUNCE_POOL
+#define VPX_SKIPW_BOUNCE_POOL 2u
+#endif
+#ifndef VPX_MINC_BOUNCE_POOL
+#define VPX_MINC_BOUNCE_POOL 2u
+#endif
+constexpr uint32_t kRunShadowPool = VPX_RUN_SHADOW_POOL, kSkipwShadowPool = VPX_SKIPW_SHADOW_POOL,
+                   kMincShadowPool = VPX_MINC_SHADOW_POOL;
+constexpr uint32_t kRunBouncePool = VPX_RUN_BOUNCE_POOL, kSkipwBouncePool = VPX_SKIPW_BOUNCE_POOL,
+                   kMincBouncePool = VPX_MINC_BOUNCE_POOL;
 #ifdef VPX_ASM_MARKS  // analysis builds only: label the walk phases in the ISA listing
 #define VPX_MARK(s) asm volatile("; MARK " s)
 #else
@@ -819,7 +847,9 @@ __device__ __forceinline__ int32_t find_nearest(const SceneView& sv, Ray& r, Cou
 // volume loop: through the instance TLAS it measured slower (C4 IsOccluded 2.67 vs 2.57 ms:
 // most shadow rays end in the world volume, the rest cross the instance lattice).
 // first: the volume the loop starts at (k_shadow_inst: 1, after the shadow pool walked the
-// world, volume 0).
+// world, volume 0).  The instances alone through the TLAS (the world's walk left to the pool)
+// were slower too: C4 48.6-48.9 vs 47.2-47.4 ms per step at 5 waves/SIMD (8 spilled VGPRs),
+// 50.4-50.6 at 4 (round 3, three interleaved runs).
 __device__ __forceinline__ bool is_occluded(const SceneView& sv, const Ray& r, Counters& k, uint32_t first = 0) {
     bool occ = false;
     auto visit = [&](uint32_t i) {

@@ -929,7 +929,7 @@ __global__ __launch_bounds__(kPoolWg) VPX_WPE(VPX_WPE_BOUNCE) void k_nearest_poo
             avail -= take;
         }
         if (!__ballot(q != ~0u)) break;  // the pool is empty and every lane is done
-        walk_wave<0, kSkipwBounce, kMincBounce, kRunBounce, true>(gv, wk, kBig, k.cells, &mode,
+        walk_wave<0, kSkipwBouncePool, kMincBouncePool, kRunBouncePool, true>(gv, wk, kBig, k.cells, &mode,
                                                                    more ? kPoolLeave : 65u);
     }
     flush_counters(k, 0u, ctr, VPX_STAGE_BOUNCE);
@@ -951,7 +951,11 @@ __device__ __forceinline__ void mark_occluded(const WaveBufs& w, uint64_t slot, 
 }
 
 // occ: the fused tails' LDS bitmap of occluded slots (one tile per workgroup), else nullptr.
-template <bool ONE>
+// RUN: the shadow walks' RUN word (vpx_trace.hpp kRun*).  k_frame0's shadow walks (80 VGPRs)
+// keep kRunShadow: the two-compare step (5 spilled VGPRs instead of 3) measured C1
+// 0.5824-0.5839 vs 0.5833-0.5859 ms and runs of 4 cells 0.5843-0.5873 (round 3, three
+// interleaved runs each: noise / slower).
+template <bool ONE, uint32_t RUN = kRunShadow>
 __device__ __forceinline__ void shadow_tile(const SceneView& sv, const WaveBufs& w, unsigned long long* __restrict__ ctr,
                                             uint32_t* occ = nullptr) {
     __shared__ uint32_t sh[4];
@@ -1005,7 +1009,7 @@ __device__ __forceinline__ void shadow_tile(const SceneView& sv, const WaveBufs&
                 Dda s;
                 if (dda_setup(*vol, g.n, o, s)) {
                     skip::Walk wk = to_walk(s);
-                    hit = walk_wave<16, kSkipwShadow, kMincShadow, kRunShadow>(grid_view(g), wk, so.w, k.cells);
+                    hit = walk_wave<16, kSkipwShadow, kMincShadow, RUN>(grid_view(g), wk, so.w, k.cells);
                 }
             }
             asm volatile("" ::: "memory");
@@ -1133,7 +1137,7 @@ __global__ __launch_bounds__(kPoolWg) VPX_WPE(VPX_WPE_SPOOL) void k_shadow_pool(
             walked += take;  // IsOccluded calls (a scalar: no register across the walks)
         }
         if (!__ballot(e != ~0u)) break;
-        walk_wave<16, kSkipwShadow, kMincShadow, kRunShadow, true>(gv, wk, bound, k.cells, &mode,
+        walk_wave<16, kSkipwShadowPool, kMincShadowPool, kRunShadowPool, true>(gv, wk, bound, k.cells, &mode,
                                                                    more ? kPoolLeave : 65u);
     }
     k.shadow = lane == 0u ? walked : 0u;
@@ -1354,7 +1358,7 @@ __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_FRAME : VPX_WPE_MULTI_NE
     wl.SL = L.ray + 512 - tb;
     primary_tile<ONE, true>(sv, f, wl, L, ctr);
     __syncthreads();
-    shadow_tile<ONE>(sv, wl, ctr, occ);
+    shadow_tile<ONE, kRunShadow>(sv, wl, ctr, occ);
     __syncthreads();
     // the tail's own copy of p: the shade's per-lane LDS addresses are re-derived here
     // instead of being kept live (spilled) across the shadow walks
