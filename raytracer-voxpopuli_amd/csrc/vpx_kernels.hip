@@ -30,6 +30,10 @@ namespace {
 constexpr int kTile = 16;  // 16x16 pixels per tile / 256-thread workgroup
 constexpr int kThreads = 256;
 
+// One tile per workgroup.  Several tiles per workgroup with their loads issued together
+// measured within noise (round 3, four interleaved runs, ms per step: C1 0.5829-0.5888 with 1,
+// 0.5808-0.5907 with 2, 0.5780-0.5849 with 4, 0.5847-0.6010 with 8; C3 3.689-3.699 with 1,
+// 3.674-3.711 with 4): the blend is not what a frame in flight waits for.
 __global__ __launch_bounds__(kThreads) void composite_tiles(FrameArgs f, const float4* __restrict__ gathered,
                                                             float4* __restrict__ accum, uint32_t* __restrict__ rgb8) {
     const uint32_t tile = blockIdx.x;
