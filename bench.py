@@ -16,7 +16,7 @@ rank accumulates and tonemaps its own tiles (the accumulator is sharded with the
 RCCL gather (torch.distributed, backend nccl) brings the packed RGB8 of the step's last
 frame to rank 0's screen, overlapped with the next step's renders.  Timed region: barrier
 + sync on both sides (the last gather included), max over ranks; value = all ranks' rays /
-that time.  Weak scaling (N x 1920x1080 pixels) is reported as the extra key
+that time.  Weak scaling (about N x the pixels at the same field of view, weak_size) is the extra key
 `weak_scaling`.
 
 Extra keys: `extra_configs` C2 / C3 / C4 (same N, their stated sizes, fewer steps), each
@@ -64,13 +64,12 @@ STAGE_KERNELS = {"primary": "k_primary", "shade": "k_shade", "shadow": "k_shadow
 
 
 def weak_size(n, base=(1920, 1080)):
-    """Frame of N x the config's own frame: for C1, 1 -> 1920x1080, 2 -> 3840x1080,
-    4 -> 3840x2160, 8 -> 7680x2160."""
-    a = 1 << math.ceil(math.log2(n) / 2) if n > 1 else 1
-    b = n // a
-    if a * b != n:
-        a, b = n, 1
-    return base[0] * a, base[1] * b
+    """Frame of about N x the config's own pixels at the SAME field of view: both sides scaled
+    by sqrt(N) (C1: 1 -> 1920x1080, 2 -> 2715x1527, 4 -> 3840x2160, 8 -> 5431x3055), rendered
+    with the base frame's camera (its TL / TR / BL corners, camera.h:90-105, u = x / W), so the
+    extra pixels sample the same view more densely instead of widening it onto free sky."""
+    r = math.sqrt(n)
+    return int(round(base[0] * r)), int(round(base[1] * r))
 
 
 def lib_sha256(pkg):
@@ -79,12 +78,13 @@ def lib_sha256(pkg):
         return hashlib.sha256(f.read()).hexdigest()
 
 
-def pmc_traffic(kernel, config, W, H, sha):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of this
-    workload AND this library build (FETCH_SIZE x2 + WRITE_SIZE per the gfx950
-    correction); None when no summary for this exact build / workload exists."""
+def pmc_summary(kernel, config, W, H, sha):
+    """The committed rocprofv3 PMC summary of `kernel` for this workload AND this library
+    build (tools/pmc_traffic.py: hbm_bytes_per_launch = FETCH_SIZE x2 + WRITE_SIZE per the
+    gfx950 correction, valu_busy, wait_frac, l2_hit_rate) and the file it came from; (None,
+    None) when no summary for this exact build / workload exists."""
     import glob
-    best = None
+    best, src = None, None
     for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_traffic*.json"))):
         try:
             d = json.load(open(f))
@@ -92,8 +92,42 @@ def pmc_traffic(kernel, config, W, H, sha):
             continue
         if (d.get("config") == config and d.get("width") == W and d.get("height") == H
                 and d.get("lib_sha256") == sha and kernel in d.get("kernels", {})):
-            best = d["kernels"][kernel]["hbm_bytes_per_launch"]
-    return best
+            best, src = d["kernels"][kernel], os.path.relpath(f, REPO)
+    return best, src
+
+
+def limiter(pmc, kernel_ms):
+    """What bounds the dominant kernel, from its committed counters: its real HBM fraction
+    (measured traffic / busy time / peak) against its VALU busy fraction."""
+    if not pmc:
+        return {"hbm_frac_measured": None, "valu_busy": None, "bound_by": "unknown: no PMC summary for this build"}
+    hbm = pmc["hbm_bytes_per_launch"] / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
+    vb = pmc.get("valu_busy")
+    if vb is not None and vb >= 0.6 and vb > hbm:
+        why = "VALU issue (valu_busy %.2f; real HBM %.3f of peak)" % (vb, hbm)
+    elif hbm >= 0.6:
+        why = "HBM bandwidth (real HBM %.2f of peak)" % hbm
+    else:
+        why = ("load latency: dependent gather chains (real HBM %.3f of peak, valu_busy %s, waves parked %s of cycles)"
+               % (hbm, "%.2f" % vb if vb is not None else "n/a",
+                  "%.2f" % pmc["wait_frac"] if pmc.get("wait_frac") is not None else "n/a"))
+    return {"hbm_frac_measured": round(hbm, 4), "valu_busy": vb, "wait_frac": pmc.get("wait_frac"),
+            "l2_hit_rate": pmc.get("l2_hit_rate"), "bound_by": why}
+
+
+def rank_summary(dist, n, render_ms, primary, device="cpu"):
+    """Every rank's render time per step and primary rays per step, gathered (all ranks call
+    it): the process group's backend and world size as torch.distributed sees them, min / max
+    render ms and the slowest rank — so a multi-GPU line shows whether RCCL saw N ranks and
+    which rank sets the time."""
+    mine = torch.tensor([float(render_ms), float(primary)], dtype=torch.float64, device=device)
+    every = [torch.zeros_like(mine) for _ in range(n)]
+    dist.all_gather(every, mine)
+    ms = [float(x[0]) for x in every]
+    return {"process_group": {"backend": str(dist.get_backend()), "world_size": dist.get_world_size()},
+            "render_ms_per_step": {"min": round(min(ms), 4), "max": round(max(ms), 4),
+                                   "slowest_rank": int(np.argmax(ms)), "per_rank": [round(x, 4) for x in ms]},
+            "primary_rays_per_step_per_rank": [int(x[1]) for x in every]}
 
 
 class Env:
@@ -131,12 +165,12 @@ class Env:
         return f"tile-shard x{self.n}, accumulator sharded, RCCL gather of RGB8 to rank 0 (overlapped)"
 
 
-def run_config(pkg, env, cfg, steps, warmup, weak=False, sha=None, pipeline=None):
+def run_config(pkg, env, cfg, steps, warmup, weak=False, sha=None, pipeline=None, serial_frames=0):
     """Load `cfg` on this rank, run warmup + `steps` timed steps, return the result dict
     (rank 0; None elsewhere).  Frees the world before returning."""
     desc = pkg.scene.CONFIGS[cfg]()
-    if weak:
-        desc = desc.with_size(*weak_size(env.n, (desc.width, desc.height)))
+    if weak:  # N x the pixels at the same field of view (the base frame's camera)
+        desc = desc.with_resolution(*weak_size(env.n, (desc.width, desc.height)))
     W, H, spp = desc.width, desc.height, max(1, int(desc.spp))
     ctx = pkg.context.Context(env.dev)
     ctx.set_stream(env.stream.cuda_stream)
@@ -193,18 +227,21 @@ def run_config(pkg, env, cfg, steps, warmup, weak=False, sha=None, pipeline=None
     if sharded is not None:
         sharded.flush()  # the last step's gather + scatter belong to the timed region
     torch.cuda.synchronize()
+    t_local = time.perf_counter() - t0  # this rank's own render (+ its part of the gather), before the barrier
     if env.dist:
         env.dist.barrier()
     elapsed = time.perf_counter() - t0
     st = ctx.counters()
     vals = torch.tensor([elapsed, float(st.primary_rays), float(st.shadow_rays), float(st.bounce_rays),
                          float(st.dda_cells)], dtype=torch.float64, device="cpu" if env.shared else "cuda")
+    ranks = None
     if env.dist:
         mx, sm = vals.clone(), vals.clone()
         env.dist.all_reduce(mx, op=env.dist.ReduceOp.MAX)
         env.dist.all_reduce(sm, op=env.dist.ReduceOp.SUM)
         elapsed = mx[0].item()
         prim, shad, bounce, cells = (sm[i].item() for i in range(1, 5))
+        ranks = rank_summary(env.dist, env.n, t_local * 1000.0 / steps, float(st.primary_rays) / steps, vals.device)
     else:
         prim, shad, bounce, cells = float(st.primary_rays), float(st.shadow_rays), float(st.bounce_rays), \
             float(st.dda_cells)
@@ -245,7 +282,8 @@ def run_config(pkg, env, cfg, steps, warmup, weak=False, sha=None, pipeline=None
                 alg_bytes += local_pix * 36.0 / max(dom_launches, 1)
         achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
         frame_bytes = (cells + prim * 36.0) / K
-        traffic = pmc_traffic(kernels[dom], cfg, W, H, sha) if env.n == 1 else None
+        pmc, pmc_src = pmc_summary(kernels[dom], cfg, W, H, sha) if env.n == 1 else (None, None)
+        traffic = pmc["hbm_bytes_per_launch"] if pmc else None
         out = {
             "config": cfg, "value": round((prim + shad) / elapsed / 1e6, 3), "ms_per_step": round(ms_step, 4),
             "total_mray_s": round((prim + shad + bounce) / elapsed / 1e6, 3),
@@ -257,9 +295,11 @@ def run_config(pkg, env, cfg, steps, warmup, weak=False, sha=None, pipeline=None
             "mpix_per_s": round(prim / elapsed / 1e6, 3),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                         "traffic_source": ("profiles/*_pmc_traffic.json for this library build (sha256 match)"
+                         "traffic_source": (pmc_src + " (this library build: sha256 match)"
                                             if traffic is not None else
                                             "null: no PMC pass committed for this library build / workload"),
+                         "traffic_over_alg": round(traffic / alg_bytes, 3) if traffic else None,
+                         **limiter(pmc, kernel_ms),
                          "kernel": kernels[dom], "kernel_ms": round(kernel_ms, 4), "launch_ms": round(launch_ms, 4),
                          "kernel_ms_def": "busy time of the kernel's launches over the timed region (overlapping "
                                           "launches counted once) / launches; launch_ms = mean start-to-end per launch",
@@ -270,6 +310,23 @@ def run_config(pkg, env, cfg, steps, warmup, weak=False, sha=None, pipeline=None
                          "frame_achieved": round(frame_bytes / (ms_step * 1e-3) / 1e9, 2)},
             "pipeline": pipeline,
         }
+        if ranks is not None:
+            out["ranks"] = ranks
+    if env.n == 1 and serial_frames:
+        # what a per-frame-synchronous host (the tmpl8 loop: Tick, then present, every frame,
+        # template.cpp:300-305) sees: one frame at a time, no lanes, the host waits for each
+        ctx.set_pipeline(0)
+        for f in range(2):  # the serial path's own path-state buffers, warm
+            ctx.render(desc.frame_params(frame_index=f), acc.data_ptr(), rgb.data_ptr())
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for f in range(serial_frames):
+            ctx.render(desc.frame_params(frame_index=f % spp), acc.data_ptr(), rgb.data_ptr())
+            torch.cuda.synchronize()
+        if out is not None:
+            out["serial_ms_per_frame"] = round((time.perf_counter() - t1) * 1000.0 / serial_frames, 4)
+            out["serial_def"] = (f"{serial_frames} frames at --pipeline 0 with a host synchronize after each "
+                                 "(a per-frame-synchronous Tick); ms_per_step / launch_ms are the frames-in-flight figures")
     del acc, rgb, sharded
     ctx.close()
     torch.cuda.synchronize()
@@ -404,13 +461,15 @@ def main():
     pkg = entry.load_package()
     env = Env(args.gpus)
     sha = lib_sha256(pkg)
-    head = run_config(pkg, env, args.config, args.steps, args.warmup, sha=sha, pipeline=args.pipeline)
+    head = run_config(pkg, env, args.config, args.steps, args.warmup, sha=sha, pipeline=args.pipeline,
+                      serial_frames=args.steps)
     extra, weak = {}, None
     if not args.no_extra:
         xs = max(3, args.steps // 4)
         for cfg in EXTRA_CONFIGS:
             if cfg != args.config:
-                r = run_config(pkg, env, cfg, xs, min(args.warmup, 2), sha=sha, pipeline=args.pipeline)
+                r = run_config(pkg, env, cfg, xs, min(args.warmup, 2), sha=sha, pipeline=args.pipeline,
+                               serial_frames=xs)
                 if r is not None:
                     extra[cfg] = r
         if env.n > 1:
@@ -426,6 +485,9 @@ def main():
                           "parallelism": env.parallelism(), "frames_in_flight": head["pipeline"], "lib_sha256": sha},
                "rays_per_step": head["rays_per_step"], "mpix_per_s": head["mpix_per_s"],
                "total_mray_s": head["total_mray_s"], "roofline": head["roofline"], "cpu_baseline": None}
+        for k in ("serial_ms_per_frame", "serial_def", "ranks"):
+            if k in head:
+                out[k] = head[k]
         if extra:
             out["extra_configs"] = extra
         if weak is not None:

@@ -53,7 +53,7 @@
 extern "C" {
 #endif
 
-#define VPX_ABI_VERSION 1
+#define VPX_ABI_VERSION 2  /* 1 -> 2: vpx_profile grew to 160 bytes (stage_busy_ms); packed tiles hold 8x8 quadrants */
 
 /* ---- status codes ---------------------------------------------------------------- */
 #define VPX_OK 0
@@ -231,7 +231,13 @@ int vpx_synchronize(vpx_ctx* ctx);
    static-camera path, VPX_FLAG_NO_TONEMAP frames and vpx_render_tiles (samples into the
    caller's buffer) run on the stream as without lanes.
    World / table updates wait for the frames in flight.  No reference counterpart: the
-   reference renders one frame per Tick (renderer.cpp:1646-1891). */
+   reference renders one frame per Tick (renderer.cpp:1646-1891).
+   Queues and ordering: each lane takes a hardware queue of its own (D per context, and per
+   member of a device set), up to 16 such lanes per process; lanes past that cap are plain
+   non-blocking streams from the process's shared queue pool.  Dedicated-queue lanes are
+   blocking streams: they synchronise with the legacy null stream (hipStreamLegacy / torch's
+   default stream), so work the caller queues there serialises with the frames in flight —
+   render on a created stream (vpx_set_stream) to keep them overlapped. */
 int vpx_set_pipeline(vpx_ctx* ctx, uint32_t depth);
 
 /* ---- world ----------------------------------------------------------------------------- */
@@ -384,6 +390,10 @@ int vpx_profile_select(vpx_ctx* ctx, uint32_t stage_mask);
 /* Synchronise, sum the recorded stage times and return them (reset: clear events and
    the per-stage cell counters). */
 int vpx_profile_read(vpx_ctx* ctx, vpx_profile* out, int reset);
+/* The busy-time rule vpx_profile_read applies (host only, no device): the length of the union
+   of n intervals [se[2i], se[2i+1]) in ms, overlaps counted once.  Starts may be negative
+   (a lane's launch that began before the first recorded event). */
+float vpx_profile_busy_union(const float* se, uint32_t n);
 
 /* ---- unit entries (host pointers; mirror the reference per-ray functions) ---------- */
 int vpx_find_nearest(vpx_ctx* ctx, const vpx_ray* rays, uint32_t n, vpx_hit* hits);

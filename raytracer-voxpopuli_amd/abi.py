@@ -10,7 +10,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libvpx_hip.so")
-ABI_VERSION = 1
+ABI_VERSION = 2  # 2: vpx_profile 160 B (stage_busy_ms), packed tiles in 8x8 quadrants
 
 VPX_OK = 0
 VPX_E_INVALID, VPX_E_DEVICE, VPX_E_NOMEM, VPX_E_STATE = -1, -2, -3, -4  # include/vpx.h status codes
@@ -173,6 +173,7 @@ SIGNATURES = {
     "vpx_profile_enable": (C.c_int, [C.c_void_p, C.c_uint32]),
     "vpx_profile_select": (C.c_int, [C.c_void_p, C.c_uint32]),
     "vpx_profile_read": (C.c_int, [C.c_void_p, C.POINTER(Profile), C.c_int]),
+    "vpx_profile_busy_union": (C.c_float, [C.POINTER(C.c_float), C.c_uint32]),
     "vpx_find_nearest": (C.c_int, [C.c_void_p, C.POINTER(Ray), C.c_uint32, C.POINTER(Hit)]),
     "vpx_is_occluded": (C.c_int, [C.c_void_p, C.POINTER(Ray), C.c_uint32, C.c_void_p]),
     "vpx_trace": (C.c_int, [C.c_void_p, C.POINTER(Ray), C.c_void_p, C.c_uint32, C.c_int32, C.POINTER(C.c_float),

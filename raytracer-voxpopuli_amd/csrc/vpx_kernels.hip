@@ -19,6 +19,7 @@
 #include <cstring>
 #include <string>
 #include <array>
+#include <atomic>
 #include <vector>
 
 #include "vpx_wavefront.hpp"
@@ -483,6 +484,7 @@ struct vpx_ctx {
         size_t packed_len = 0;
         hipEvent_t rendered = nullptr, consumed = nullptr;
         bool used = false;
+        bool dedicated = false;  // on a CU-mask stream (its own hardware queue), counted in g_lane_queues
     };
     std::vector<Lane> lanes;
     uint32_t lane_next = 0;
@@ -904,8 +906,15 @@ int lane_render(vpx_ctx* c, const SceneView& sv, const FrameArgs& f, uint32_t ti
     return VPX_OK;
 }
 
+// Lanes on dedicated hardware queues across the process (every context, every device-set
+// member): each takes a queue of its own, so the count is capped (kMaxLaneQueues); lanes past
+// the cap are plain non-blocking streams from the shared pool.
+std::atomic<int> g_lane_queues{0};
+constexpr int kMaxLaneQueues = 16;
+
 void free_lanes(vpx_ctx* c) {
     for (auto& L : c->lanes) {
+        if (L.dedicated) g_lane_queues.fetch_sub(1);
         if (L.s) (void)hipStreamSynchronize(L.s);
         if (L.ws.d) (void)hipFree(L.ws.d);
         if (L.packed) (void)hipFree(L.packed);
@@ -1053,8 +1062,15 @@ int vpx_set_pipeline(vpx_ctx* c, uint32_t depth) {
     int n_cu = 0;
     VPX_HIP(c, hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, c->device));
     std::vector<uint32_t> all_cus(((uint32_t)n_cu + 31u) / 32u, 0xffffffffu);
+    // CU-mask streams are blocking streams (no flags argument): they synchronise with the
+    // legacy null stream like any default-flag stream (documented in vpx.h).
     for (auto& L : c->lanes) {
-        if (hipExtStreamCreateWithCUMask(&L.s, (uint32_t)all_cus.size(), all_cus.data()) != hipSuccess ||
+        L.dedicated = g_lane_queues.fetch_add(1) < kMaxLaneQueues;
+        if (!L.dedicated) g_lane_queues.fetch_sub(1);
+        const hipError_t se = L.dedicated
+                                  ? hipExtStreamCreateWithCUMask(&L.s, (uint32_t)all_cus.size(), all_cus.data())
+                                  : hipStreamCreateWithFlags(&L.s, hipStreamNonBlocking);
+        if (se != hipSuccess ||
             hipEventCreateWithFlags(&L.rendered, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&L.consumed, hipEventDisableTiming) != hipSuccess) {
             free_lanes(c);
@@ -2069,6 +2085,29 @@ extern "C" int vpx_profile_enable(vpx_ctx* c, uint32_t max_launches) {
     return VPX_OK;
 }
 
+// Length of the union of [first, second) intervals (any sign), overlaps counted once.
+static float interval_union_ms(std::vector<std::pair<float, float>>& iv) {
+    if (iv.empty()) return 0.f;
+    std::sort(iv.begin(), iv.end());
+    float busy = 0.f, lo = iv[0].first, hi = iv[0].second;
+    for (const auto& v : iv) {
+        if (v.first > hi) {
+            busy += hi - lo;
+            lo = v.first, hi = v.second;
+        } else if (v.second > hi) {
+            hi = v.second;
+        }
+    }
+    return busy + (hi - lo);
+}
+
+// Host check of the union (tests/test_abi.py): n intervals as (start, end) pairs.
+extern "C" float vpx_profile_busy_union(const float* se, uint32_t n) {
+    std::vector<std::pair<float, float>> iv;
+    for (uint32_t i = 0; i < n; ++i) iv.emplace_back(se[2 * i], se[2 * i + 1]);
+    return interval_union_ms(iv);
+}
+
 extern "C" int vpx_profile_read(vpx_ctx* c, vpx_profile* out, int reset) {
     VPX_GROUP_FIRST(c, vpx_profile_read(m_, out, reset));
     if (!c || !out) return fail(c, VPX_E_INVALID, "null argument");
@@ -2089,20 +2128,10 @@ extern "C" int vpx_profile_read(vpx_ctx* c, vpx_profile* out, int reset) {
             iv[st].emplace_back(t0, t0 + ms);
         }
     }
-    for (uint32_t st = 0; st < 8; ++st) {  // busy time: the union of the intervals
-        std::sort(iv[st].begin(), iv[st].end());
-        float busy = 0.f, lo = 0.f, hi = -1.f;
-        for (const auto& v : iv[st]) {
-            if (v.first > hi) {
-                if (hi > lo) busy += hi - lo;
-                lo = v.first, hi = v.second;
-            } else if (v.second > hi) {
-                hi = v.second;
-            }
-        }
-        if (hi > lo) busy += hi - lo;
-        out->stage_busy_ms[st] = busy;
-    }
+    // busy time: the union of the intervals.  Offsets are measured from prof_ev[0], which may
+    // sit on another lane's stream, so a launch can start before it (a negative offset): the
+    // union starts from the first sorted interval, not from a sentinel at 0.
+    for (uint32_t st = 0; st < 8; ++st) out->stage_busy_ms[st] = interval_union_ms(iv[st]);
     if (reset) {
         c->prof_used = 0;
         unsigned long long* d = c->d_ctr;

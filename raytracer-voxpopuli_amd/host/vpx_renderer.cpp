@@ -25,6 +25,10 @@ const char* Renderer::LastError() const {
 
 int Renderer::Init(uint32_t width, uint32_t height) {
     if (status_) return status_;
+    if (vpx_abi_version() != VPX_ABI_VERSION) {  // a stale libvpx_hip.so
+        err_ = "libvpx_hip.so ABI version differs from include/vpx.h";
+        return status_ = VPX_E_STATE;
+    }
     if (!width || !height) return VPX_E_INVALID;
     if (hipSetDevice(device_) != hipSuccess ||
         hipMalloc(&accumulator_, sizeof(float) * 4 * width * height) != hipSuccess ||

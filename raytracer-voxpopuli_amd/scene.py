@@ -144,12 +144,6 @@ class GridSpec:
     period: tuple = None              # (px, py, pz)
     ground: int = 2
 
-    def host_cells(self):
-        if self.dense is not None:
-            return self.dense
-        from_oracle = _tiled_numpy(self)
-        return from_oracle
-
     def upload(self, lib, ctx, grid_id):
         if self.dense is not None:
             arr = np.ascontiguousarray(self.dense, np.uint8)
@@ -238,6 +232,14 @@ class SceneDesc:
         """Same scene at another resolution (camera ASPECT follows W/H, camera.h:183)."""
         d = dataclasses.replace(self, width=width, height=height)
         d.camera = look_at(self._cam_pos, self._cam_target, width, height)
+        d._cam_pos, d._cam_target = self._cam_pos, self._cam_target
+        return d
+
+    def with_resolution(self, width, height):
+        """Same scene and the SAME camera (its TL / TR / BL corners, camera.h:90-105) at another
+        resolution: pixel (x, y) samples u = x / W, v = y / H of the same view, so more pixels
+        sample it more densely (the weak-scaling frames of bench.py) instead of widening it."""
+        d = dataclasses.replace(self, width=width, height=height)
         d._cam_pos, d._cam_target = self._cam_pos, self._cam_target
         return d
 

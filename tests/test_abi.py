@@ -37,6 +37,30 @@ def test_struct_layouts(pkg):
         assert C.sizeof(s) == size, s
 
 
+def test_abi_version_matches_header(pkg):
+    text = open(os.path.join(REPO, "include", "vpx.h")).read()
+    hdr = int(re.search(r"#define VPX_ABI_VERSION (\d+)", text).group(1))
+    assert hdr == pkg.abi.ABI_VERSION == pkg.load_library().vpx_abi_version() == 2
+
+
+@pytest.mark.parametrize("iv,want", [
+    ([], 0.0),
+    ([(0.0, 1.0)], 1.0),
+    ([(0.0, 1.0), (0.5, 2.0)], 2.0),          # overlap counted once
+    ([(0.0, 1.0), (3.0, 4.0)], 2.0),          # disjoint
+    ([(-3.0, -1.0), (0.0, 1.0)], 3.0),        # a lane's launch before the first event (negative start)
+    ([(-2.0, 0.5), (0.0, 1.0)], 3.0),
+    ([(1.0, 2.0), (-5.0, -4.5), (1.5, 1.7)], 1.5),
+])
+def test_profile_busy_union(pkg, iv, want):
+    """vpx_profile_read's busy time is the union of the launch intervals, also when a launch
+    on another lane started before the first recorded event (the old sentinels
+    clipped such intervals to [0, hi])."""
+    lib = pkg.load_library()
+    flat = (C.c_float * max(1, 2 * len(iv)))(*[x for ab in iv for x in ab])
+    assert abs(lib.vpx_profile_busy_union(flat, len(iv)) - want) < 1e-6
+
+
 def test_create_without_gpu_fails_cleanly(pkg):
     torch = pytest.importorskip("torch")
     if torch.cuda.device_count() > 0:

@@ -881,7 +881,7 @@ def test_frames_in_flight_equal_serial_frames(pkg, lanes, depth):
     W, H = desc.width, desc.height
     box = np.full((6, 6, 6), 1, np.uint8)  # NON_METAL_RED cells
 
-    def run(pipe):
+    def run(pipe, edit=True):
         ctx = pkg.context.Context(0)
         s = torch.cuda.Stream()
         ctx.set_stream(s.cuda_stream)
@@ -894,8 +894,9 @@ def test_frames_in_flight_equal_serial_frames(pkg, lanes, depth):
         shots = []
         with torch.cuda.stream(s):
             for f in range(5):
-                if f == 3:  # a prop edit (LoadModelPartial) between frames
-                    ctx.lib.vpx_grid_write_box(ctx.h, 0, box.ctypes.data_as(C.c_void_p), 60, 40, 60, 6, 6, 6)
+                if f == 3 and edit:  # a prop edit (LoadModelPartial) between frames
+                    rc = ctx.lib.vpx_grid_write_box(ctx.h, 0, box.ctypes.data_as(C.c_void_p), 60, 40, 60, 6, 6, 6)
+                    assert rc == 0, ctx.lib.vpx_last_error(ctx.h)
                 ctx.render(desc.frame_params(f), acc.data_ptr(), rgb.data_ptr())
                 shots.append(rgb.clone())
         ctx.synchronize()
@@ -909,6 +910,12 @@ def test_frames_in_flight_equal_serial_frames(pkg, lanes, depth):
     assert np.array_equal(a0, a1)
     for x, y in zip(s0, s1):
         assert np.array_equal(x, y)
+    # the edit has an effect: without it frames 0-2 are the same and frames 3-4 differ
+    _, s2, _ = run(0, edit=False)
+    for f in range(3):
+        assert np.array_equal(s0[f], s2[f])
+    for f in (3, 4):
+        assert not np.array_equal(s0[f], s2[f]), f"frame {f}: the world edit changed nothing"
     assert (t0.primary_rays, t0.shadow_rays, t0.bounce_rays, t0.dda_cells) == (
         t1.primary_rays, t1.shadow_rays, t1.bounce_rays, t1.dda_cells)
 

@@ -21,11 +21,24 @@ for f in sorted(glob.glob(f"{root}/p*/run_counter_collection.csv")):
 kernels = {}
 for k, d in vals.items():
     if "FETCH_SIZE" not in d or "WRITE_SIZE" not in d:
-        continue
+        continue  # (every pass of tools/gpu_pmc.sh sees every kernel)
     fetch = sum(d["FETCH_SIZE"]) / len(d["FETCH_SIZE"])
     write = sum(d["WRITE_SIZE"]) / len(d["WRITE_SIZE"])
     kernels[k] = {"fetch_kib": round(fetch, 1), "write_kib": round(write, 1), "launches_sampled": len(d["FETCH_SIZE"]),
                   "hbm_bytes_per_launch": round((2.0 * fetch + write) * 1024.0)}
+    mean = lambda c: sum(d[c]) / len(d[c])
+    if "SQ_ACTIVE_INST_VALU" in d and "GRBM_GUI_ACTIVE" in d:
+        # VALU busy: SQ_ACTIVE_INST_VALU counts quad-cycles summed over the chip's 1024 SIMDs,
+        # GRBM_GUI_ACTIVE cycles summed over its 8 XCDs (MI355X_MICROARCH.md, cycle constants
+        # and DVFS rows): busy = VALU x 4 / 1024 / (GUI_ACTIVE / 8), per (serialised) dispatch
+        gui = mean("GRBM_GUI_ACTIVE") / 8.0
+        kernels[k]["valu_busy"] = round(mean("SQ_ACTIVE_INST_VALU") * 4.0 / 1024.0 / gui, 4) if gui > 0 else None
+        kernels[k]["gui_active_cycles"] = round(gui)
+    if "SQ_WAIT_ANY" in d and "SQ_WAVE_CYCLES" in d and mean("SQ_WAVE_CYCLES") > 0:
+        kernels[k]["wait_frac"] = round(mean("SQ_WAIT_ANY") / mean("SQ_WAVE_CYCLES"), 4)
+    if "TCC_HIT_sum" in d and "TCC_MISS_sum" in d:
+        h, m = mean("TCC_HIT_sum"), mean("TCC_MISS_sum")
+        kernels[k]["l2_hit_rate"] = round(h / (h + m), 4) if h + m > 0 else None
 import os
 sha = None
 if os.path.exists(f"{root}/lib.sha256"):  # written on the GPU box by tools/gpu_pmc.sh
