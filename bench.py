@@ -60,7 +60,7 @@ EXTRA_CONFIGS = ("C2", "C3", "C4")
 # config after C1 (the line the driver runs), C3 3.70-3.71 / 3.65 / 3.67-3.71.
 PIPELINE = {"C1": 3, "C2": 3, "C3": 3, "C4": 4}
 STAGE_KERNELS = {"primary": "k_primary", "shade": "k_shade", "shadow": "k_shadow_tile", "resolve": "k_resolve",
-                 "bounce": "k_nearest_tile", "finish": "k_finish", "frame": "k_frame0"}
+                 "bounce": "k_nearest_tile", "finish": "k_finish", "frame": "k_frame0", "paths": "k_path_pool"}
 
 
 def weak_size(n, base=(1920, 1080)):
@@ -276,6 +276,8 @@ def run_config(pkg, env, cfg, steps, warmup, weak=False, sha=None, pipeline=None
             alg_bytes = local_pix / K / spp * 36.0
         elif dom == "frame":  # k_frame0: the whole depth-0 frame (every stage's cells + the finish)
             alg_bytes = (sum(float(v[2]) for v in prof.values()) + local_pix * 36.0) / max(dom_launches, 1)
+        elif dom == "paths":  # k_path_pool: the bounce levels' walks (shadow + bounce rays) and the finish
+            alg_bytes = (float(dom_cells) + local_pix * 36.0) / max(dom_launches, 1)
         else:
             alg_bytes = float(dom_cells) / max(dom_launches, 1)
             if dom == "shadow" and fused:

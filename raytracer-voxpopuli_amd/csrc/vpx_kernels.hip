@@ -417,6 +417,9 @@ __global__ void checksum_k(const uint8_t* __restrict__ cells, uint64_t count, un
 struct vpx_ctx {
     int device = 0;
     uint32_t cus = 256;  // compute units of the device (the bounce pool's grid)
+    // bounce levels through the path pool (k_path_pool); VPX_PATH_POOL=0 in the environment at
+    // vpx_create selects the per-level kernels instead (A/B and parity tests)
+    bool path_pool = true;
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
     std::string err;
@@ -801,6 +804,23 @@ int launch_render(vpx_ctx* c, hipStream_t s, vpx_ctx::WaveStore& ws, const Scene
         VPX_HIP(c, hipGetLastError());
         return VPX_OK;
     }
+    if (one && fuse_tail && f.max_bounces > 0 && c->path_pool) {
+        // the bounce levels in one persistent launch (k_path_pool): the fused head walks the
+        // primary rays and shades level 0, the pool carries every path through the rest of
+        // its chain and finishes its pixel
+        prof_mark(c, s, VPX_STAGE_PRIMARY);
+        hipLaunchKernelGGL((k_primary<true, true>), grid, block, 0, s, sv, f, w, c->d_ctr);
+        prof_mark(c, s, -1);
+        const uint32_t grabs = (P / 64u + kPoolGrab - 1u) / kPoolGrab;
+        const uint32_t waves = std::min(grabs, c->cus * 4u * (uint32_t)VPX_WPE_PATHS);
+        const uint32_t wpb = kPoolWg / 64u;
+        prof_mark(c, s, VPX_STAGE_PATHS);
+        hipLaunchKernelGGL((k_path_pool<MODE>), dim3((waves + wpb - 1u) / wpb), dim3(kPoolWg), 0, s, sv, f, w,
+                           c->d_ctr, accum, rgb8, packed);
+        prof_mark(c, s, -1);
+        VPX_HIP(c, hipGetLastError());
+        return VPX_OK;
+    }
     prof_mark(c, s, VPX_STAGE_PRIMARY);
     const bool fuse_head = f.max_bounces >= 0;  // level 0's shade at the end of k_primary
     if (fuse_head)
@@ -975,6 +995,7 @@ int vpx_create(int device, vpx_ctx** out) {
     }
     c->stream = c->own_stream;
     (void)hipMemset(c->d_ctr, 0, kCtrWords * kCtrStripes * sizeof(unsigned long long));
+    if (const char* e = std::getenv("VPX_PATH_POOL")) c->path_pool = std::strcmp(e, "0") != 0;
     *out = c;
     return VPX_OK;
 }

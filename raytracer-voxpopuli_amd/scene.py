@@ -406,6 +406,94 @@ def instanced_scene(n=2048, inst_n=64, width=3840, height=2160, model="monu3", s
                   CITY_LIGHTS["dir_light"], (1.6, 1.9, -1.2), (0.5, 0.7, 0.5), width, height, spp=spp)
 
 
+def _cos_degrees(d):
+    """CosDegrees (tmpl8math.h) in float: cosf(d * PI / 180)."""
+    r = np.float32(np.float32(d) * np.float32(math.pi) / np.float32(180.0))
+    return float(np.float32(math.cos(float(r))))
+
+
+def zone_scene(width=1920, height=1080, max_bounces=14, sky=True):
+    """The reference's own scene shape: Renderer::SetUpFirstZone (renderer.cpp:592-657) with
+    its CreateBridge (:482-529) and CreateBridgeBlind (:531-590), CreateTrianglePattern
+    (:460-469) and SetUpLights (:93-100: 1 point light, 5 spot lights, the directional light
+    with its default zero colour, renderer.cpp:638-654 for the spots), maxBounces 14
+    (renderer.h:175), activateSky (renderer.h:216; the HDR asset is missing from the reference
+    tree, so the synthetic sky stands in), the camera's default pose (camera.h:20-21).
+    21 volumes (Scene(position, N) + SetTransform, so the reference's matrices) and 10
+    triangles.  Build-defined where the reference draws at run time: the Rand() material picks
+    (fixed values from the same ranges), the FastNoise2 smoke of the 64^3 checkpoint volume
+    (GenerateSomeSmoke) — a deterministic smoke ball instead — and the Text model's random
+    materials (LoadModelRandomMaterials) — its palette materials instead."""
+    MET_LOW, GLASS, PINK = 7, 8, 4
+    mats = default_materials()
+    psize, pvox, ppal = load_model("player")
+    tsize, tvox, tpal = load_model("Text")
+    mats = palette_materials(mats, pvox, ppal)
+    mats = palette_materials(mats, tvox, tpal)
+    grids, gid = [], {}
+
+    def grid(key, n, dense):
+        if key not in gid:
+            gid[key] = len(grids)
+            grids.append(GridSpec(n=n, dense=dense))
+        return gid[key]
+
+    def solid(m):  # a 1^3 Scene after ResetGrid(m)
+        return grid(f"solid{m}", 1, np.full(1, m, np.uint8))
+
+    n = 64  # the checkpoint's smoke: a ball of smoke cells (SMOKE_LOW_DENSITY..SMOKE_PLAYER - 1)
+    z, y, x = np.meshgrid(*(np.arange(n, dtype=np.float32),) * 3, indexing="ij")
+    r = np.sqrt((x - 31.5) ** 2 + (y - 31.5) ** 2 + (z - 31.5) ** 2)
+    smoke = np.where(r < 20.0, (9 + (r.astype(np.int64) % 5)).astype(np.uint8), np.uint8(NONE)).reshape(-1)
+    vols = []
+
+    def vol(pos, scl, g):
+        vols.append(volume(pos, scl, (0.0, 0.0, 0.0), grid_id=g))
+
+    vol((0.0, 0.0, 0.0), (1.0, 1.0, 1.0), grid("player", 16, load_model_grid(psize, pvox, 16)))  # the player
+    vol((0.0, -1.0, 0.0), (5.0, 1.0, 5.0), solid(MET_LOW))  # environment (ResetGrid METAL_LOW)
+    vol((6.0, 0.0, 0.0), (5.0, 5.0, 5.0), solid(MET_LOW))
+    vol((-10.0, 2.0, 0.0), (5.0, 5.0, 5.0), solid(MET_LOW))
+    vol((0.0, 4.0, 0.0), (10.0, 1.0, 10.0), solid(MET_LOW))
+    vol((0.0, 0.3, 0.0), (3.0, 3.0, 3.0), grid("smoke", 64, smoke))  # checkpoint
+    vol((0.0, 3.0, -3.0), (5.0, 5.0, 5.0), grid("text", 32, load_model_grid(tsize, tvox, 32)))  # Text
+    none64 = grid("none64", 64, np.full(64 ** 3, NONE, np.uint8))
+    # CreateBridge({0, 0, 0}) (enterOffset {0}, door GLASS)
+    vol((0.0, 4.0, -7.0), (10.0, 1.0, 5.0), solid(1))
+    vol((-1.0, 0.0, -11.0), (3.0, 10.0, 1.0), solid(GLASS))
+    vol((-5.0, 1.0, -12.0), (2.0, 3.0, 10.0), solid(2))
+    vol((-3.0, 1.0, -19.0), (7.0, 1.0, 1.0), solid(3))
+    vol((0.0, -1.0, -18.0), (5.0, 1.0, 5.0), solid(6))  # Rand(METAL_HIGH, GLASS)
+    vol((0.0, 0.3, -17.0), (2.0, 2.0, 2.0), none64)
+    # CreateBridgeBlind({0, 0, -17}, {0, -6, 0}, GLASS)
+    vol((0.0, -2.0, -24.0), (10.0, 1.0, 5.0), solid(0))
+    vol((-1.0, 0.0, -28.0), (3.0, 10.0, 1.0), solid(GLASS))
+    vol((5.0, -41.0, -29.0), (2.0, 3.0, 10.0), solid(MET_LOW))
+    vol((-5.0, 1.0, -29.0), (2.0, 3.0, 10.0), solid(PINK))  # not reset: the Scene ctor's NON_METAL_PINK
+    vol((3.0, 51.0, -36.0), (7.0, 1.0, 1.0), solid(GLASS))  # Rand(METAL_HIGH, GLASS)
+    vol((-3.0, 1.0, -36.0), (7.0, 1.0, 1.0), solid(2))
+    vol((0.0, -1.0, -35.0), (5.0, 1.0, 5.0), solid(1))
+    vol((0.0, 0.3, -34.0), (2.0, 2.0, 2.0), none64)
+    tris = []
+    for i in range(10):  # CreateTrianglePattern: scale 0.25 from (-1.75, 0, 3), step 2 * scale
+        px = float(np.float32(-1.75) + np.float32(0.5) * np.float32(i))
+        tris.append(abi.Triangle(abi.vec3((px, 0.0, 3.0)), abi.vec3((-0.25, 0.0, 0.0)), abi.vec3((0.0, 0.25, 0.0)),
+                                 abi.vec3((0.25, 0.0, 0.0)), i % 8, (C.c_uint32 * 3)()))
+    spots = []
+    fixed = [(0.9, 0.3, 0.6, 30.0), (0.2, 0.8, 0.4, 25.0), (0.7, 0.6, 0.1, 40.0)]
+    for i in range(5):
+        if i >= 2:
+            cr, cg, cb, deg = fixed[i - 2]
+            pos = (-3.0, float(np.float32(math.sin(float(i))) + np.float32(1.0)), -25.0 - 2.0 * i)
+            spots.append(spot_light(pos, (1.0, 0.0, 0.0), (cr, cg, cb), _cos_degrees(deg)))
+        else:
+            spots.append(spot_light((0.0, 0.0, -22.0 - 3.0 * i), (0.0, 1.0, 0.0)))
+    d = _scene("zone1", grids, vols, mats, [point_light()], spots, [], dir_light(), (0.0, 0.0, -2.0),
+               (0.0, 0.0, -1.0), width, height, max_bounces=max_bounces)
+    d.triangles = tris
+    return with_sky(d) if sky else d
+
+
 CONFIGS = {
     "C0": lambda: model_scene("teapot", 128, 640, 360, 0),
     "C0m": lambda: model_scene("monu3", 128, 640, 360, 0),
@@ -413,4 +501,7 @@ CONFIGS = {
     "C2": lambda: city_scene("roomGlass", 1024, 1920, 1080, 4),
     "C3": lambda: city_scene("monu3", 2048, 3840, 2160, 0, areas=C3_AREAS),
     "C4": lambda: instanced_scene(),
+    # the reference's own scene shape (SetUpFirstZone, depth 14): 21 volumes, 10 triangles,
+    # point + 5 spot + directional lights (build-defined where the reference draws at run time)
+    "Z1": lambda: zone_scene(1920, 1080, 14),
 }
