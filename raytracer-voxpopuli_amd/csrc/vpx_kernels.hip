@@ -29,6 +29,9 @@ using namespace vpx;
 namespace {
 
 constexpr int kTile = 16;  // 16x16 pixels per tile / 256-thread workgroup
+#ifndef VPX_LANE_TAIL
+#define VPX_LANE_TAIL 1  // frames in flight blend in their own tail launch where they have one (lane_tail_ok)
+#endif
 constexpr int kThreads = 256;
 
 // One tile per workgroup.  Several tiles per workgroup with their loads issued together
@@ -486,6 +489,7 @@ struct vpx_ctx {
         float4* packed = nullptr;  // the lane's frame: one float4 sample per path (tile order)
         size_t packed_len = 0;
         hipEvent_t rendered = nullptr, consumed = nullptr;
+        hipEvent_t caller = nullptr;  // the caller's stream at the frame's vpx_render (lane_tail_ok frames)
         bool used = false;
         bool dedicated = false;  // on a CU-mask stream (its own hardware queue), counted in g_lane_queues
     };
@@ -757,9 +761,12 @@ struct Reproj {  // the static-camera tail (vpx_render_reproject)
     float4 *alb, *ill, *rd, *temp, *hist;
 };
 
+// tail_wait: an event the frame's separate tail launch (k_resolve_finish, after the shadow
+// pool) waits for — frames in flight that blend on their own lane (lane_tail_ok).
 template <int MODE>
 int launch_render(vpx_ctx* c, hipStream_t s, vpx_ctx::WaveStore& ws, const SceneView& sv, const FrameArgs& f,
-                  uint32_t tiles, float4* accum, uint32_t* rgb8, float4* packed, const Reproj* rp = nullptr) {
+                  uint32_t tiles, float4* accum, uint32_t* rgb8, float4* packed, const Reproj* rp = nullptr,
+                  const hipEvent_t* tail_wait = nullptr) {
     const uint32_t P = tiles * (uint32_t)kTilePix;
     const uint32_t L = (uint32_t)std::max(1, f.max_bounces + 1);
     // shadow slots per path: an area-light sample each, else one (point / spot / directional
@@ -846,6 +853,7 @@ int launch_render(vpx_ctx* c, hipStream_t s, vpx_ctx::WaveStore& ws, const Scene
                                    slds, s, sv, f, w, c->d_ctr, accum, rgb8, packed);
             prof_mark(c, s, -1);
             if (spool) {
+                if (tail_wait) VPX_HIP(c, hipStreamWaitEvent(s, *tail_wait, 0));
                 prof_mark(c, s, VPX_STAGE_FINISH);
                 hipLaunchKernelGGL((k_resolve_finish<MODE>), grid, block, 0, s, sv, f, w, accum, rgb8, packed);
                 prof_mark(c, s, -1);
@@ -895,6 +903,15 @@ int launch_render(vpx_ctx* c, hipStream_t s, vpx_ctx::WaveStore& ws, const Scene
     return VPX_OK;
 }
 
+// Whether a frame's blend can run as its own tail launch on the lane (launch_render's spool
+// tail, k_resolve_finish): area lights with several samples (the shadow pool), outside the
+// path pool (single volume with bounces: its finish is inside the persistent launch).
+bool lane_tail_ok(const vpx_ctx* c, const SceneView& sv, const FrameArgs& f) {
+    const uint32_t S = sv.num_areas ? (uint32_t)std::max(1, sv.area_samples) : 1u;
+    const bool one = sv.num_volumes == 1 && !(sv.num_spheres | sv.num_triangles);
+    return VPX_LANE_TAIL && S > 1 && f.max_bounces >= 0 && !(one && f.max_bounces > 0 && c->path_pool);
+}
+
 // Frames in flight: render `tiles` tiles of frame f as packed float4 samples (into `out`, or
 // the lane's own buffer when null) on the next lane's stream, in that lane's path state; the
 // caller's stream waits for the render.  The caller then queues the frame's composite on
@@ -940,6 +957,7 @@ void free_lanes(vpx_ctx* c) {
         if (L.packed) (void)hipFree(L.packed);
         if (L.rendered) (void)hipEventDestroy(L.rendered);
         if (L.consumed) (void)hipEventDestroy(L.consumed);
+        if (L.caller) (void)hipEventDestroy(L.caller);
         if (L.s) (void)hipStreamDestroy(L.s);
     }
     c->lanes.clear();
@@ -1093,7 +1111,8 @@ int vpx_set_pipeline(vpx_ctx* c, uint32_t depth) {
                                   : hipStreamCreateWithFlags(&L.s, hipStreamNonBlocking);
         if (se != hipSuccess ||
             hipEventCreateWithFlags(&L.rendered, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&L.consumed, hipEventDisableTiming) != hipSuccess) {
+            hipEventCreateWithFlags(&L.consumed, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&L.caller, hipEventDisableTiming) != hipSuccess) {
             free_lanes(c);
             return fail(c, VPX_E_DEVICE, "pipeline lane stream / events");
         }
@@ -1582,6 +1601,24 @@ int vpx_render(vpx_ctx* c, const vpx_frame_params* p, float* accum, uint32_t* rg
     VPX_HIP(c, hipSetDevice(c->device));
     const SceneView sv = view_of(c, p->sky, p->area_samples, (p->flags & VPX_FLAG_SKY) != 0);
     const FrameArgs f = frame_of(c, p, 0, 1);
+    if (!c->lanes.empty() && !stats && !(p->flags & VPX_FLAG_NO_TONEMAP) && lane_tail_ok(c, sv, f)) {
+        // frames in flight whose tail is a launch of its own (k_resolve_finish after the shadow
+        // pool): the whole frame runs on its lane, the tail blending straight into the caller's
+        // accumulator once the caller's stream has reached this call (which orders it after
+        // the previous frame's tail): no packed sample, no composite (32 B per pixel less)
+        vpx_ctx::Lane& L = c->lanes[c->lane_next];
+        c->lane_next = (c->lane_next + 1u) % (uint32_t)c->lanes.size();
+        if (L.used) VPX_HIP(c, hipStreamWaitEvent(L.s, L.consumed, 0));
+        VPX_HIP(c, hipEventRecord(L.caller, c->stream));
+        if ((rc = launch_render<kFinishImage>(c, L.s, L.ws, sv, f, f.num_tiles, reinterpret_cast<float4*>(accum), rgb8,
+                                              nullptr, nullptr, &L.caller)))
+            return rc;
+        VPX_HIP(c, hipEventRecord(L.rendered, L.s));
+        VPX_HIP(c, hipStreamWaitEvent(c->stream, L.rendered, 0));
+        VPX_HIP(c, hipEventRecord(L.consumed, L.s));
+        L.used = true;
+        return VPX_OK;
+    }
     if (!c->lanes.empty() && !stats && !(p->flags & VPX_FLAG_NO_TONEMAP)) {
         // frames in flight: the frame renders on a lane; its accumulate / tonemap runs on the
         // caller's stream after the previous frame's (the same blend of the same sample)

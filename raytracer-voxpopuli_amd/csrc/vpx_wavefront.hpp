@@ -1167,10 +1167,54 @@ __global__ __launch_bounds__(kPoolWg) VPX_WPE(VPX_WPE_SPOOL) void k_shadow_pool(
 // the world left unoccluded (k_shadow_pool walked volume 0, the first in the reference's loop,
 // renderer.cpp:209-243): volumes 1.. in order, then the shapes; an occluder sets the slot's
 // occb byte.  The slots' IsOccluded calls were counted by the pool.
+// The instances' bounding spheres (up to 64: volumes 1..64, bit k = volume k + 1) are tested
+// first, all of them, from a copy in LDS — a branch-free loop of independent tests — and the
+// walks then visit the candidates in increasing index order (wave-uniform: one grid per walk),
+// each lane stopping at its first occluder: the reference's loop (renderer.cpp:209-243)
+// restricted to the volumes whose Setup3DDDA can succeed (misses_volume), so the same
+// occlusion and cell counts.  The linear loop read each volume's sphere with a dependent
+// vector load per iteration.
+#ifndef VPX_INST_MASK
+#define VPX_INST_MASK 1
+#endif
+__device__ __forceinline__ bool occluded_instances(const SceneView& sv, const float4* vb, const Ray& r, Counters& k) {
+    const uint32_t nv = sv.num_volumes;
+    uint64_t cand = 0ull;
+    for (uint32_t i = 1; i < nv; ++i)
+        cand |= (misses_volume(vb[i], r.O, r.D) ? 0ull : 1ull) << (i - 1u);
+    bool occ = false;
+    // the volumes in increasing index order, wave-uniform (a walk needs one grid per wave); a
+    // volume no lane of the wave can reach costs one ballot
+    for (uint32_t i = 1; i < nv; ++i) {
+        const bool want = !occ && ((cand >> (i - 1u)) & 1ull);
+        if (!__ballot(want)) continue;
+        if (!want) continue;
+        const vpx_volume& vol = sv.volumes[i];
+        ORay o;
+        o.O = xform_pos(r.O, vol.inv_matrix);
+        o.D = xform_vec(r.D, vol.inv_matrix);
+        o.rD = mk(__fdiv_rn(1.0f, o.D.x), __fdiv_rn(1.0f, o.D.y), __fdiv_rn(1.0f, o.D.z));
+        const DevGrid g = sv.grids[vol.grid_id];
+        Dda s;
+        if (!dda_setup(vol, g.n, o, s)) continue;
+        skip::Walk wk = to_walk(s);
+        occ = walk_wave<16, kSkipwShadow, kMincShadow, kRunShadow>(grid_view(g), wk, r.t, k.cells);
+    }
+    if (occ) return true;
+    for (uint32_t i = 0; i < sv.num_spheres; ++i)
+        if (sphere_is_hit(sv.spheres[i], r)) return true;
+    for (uint32_t i = 0; i < sv.num_triangles; ++i)
+        if (tri_is_hit(sv.triangles[i], r)) return true;
+    return false;
+}
+
 __global__ __launch_bounds__(256) VPX_WPE(VPX_WPE_MULTI_SHADOW) void k_shadow_inst(SceneView sv, WaveBufs w,
                                                                                   unsigned long long* __restrict__ ctr) {
     __shared__ uint32_t sh[4];
+    __shared__ float4 vb[kTlasMaxVolumes];
     extern __shared__ uint32_t lst_dyn[];  // [S * 256]
+    if (VPX_INST_MASK && threadIdx.x < sv.num_volumes && threadIdx.x < kTlasMaxVolumes)
+        vb[threadIdx.x] = sv.vbounds[threadIdx.x];  // published by block_scan's barriers
     const uint32_t p = tile_block() * 256u + threadIdx.x;
     Counters k{0u, 0u, 0u};
     const uint32_t m = p < w.P ? w.smask[p] & kSlotBits : 0u;
@@ -1191,7 +1235,9 @@ __global__ __launch_bounds__(256) VPX_WPE(VPX_WPE_MULTI_SHADOW) void k_shadow_in
         r.O = mk(so.x, so.y, so.z);
         r.D = mk(sd.x, sd.y, sd.z);
         r.t = so.w;
-        if (is_occluded(sv, r, k, 1u)) w.occb[slot] = 1u;
+        const bool occ = (VPX_INST_MASK && sv.num_volumes <= kTlasMaxVolumes) ? occluded_instances(sv, vb, r, k)
+                                                                              : is_occluded(sv, r, k, 1u);
+        if (occ) w.occb[slot] = 1u;
     }
     flush_counters(k, 0u, ctr, VPX_STAGE_SHADOW);
 }
