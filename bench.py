@@ -52,15 +52,17 @@ import __graft_entry__ as entry  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 METRIC = "Mray/s (primary+shadow) at 1920×1080, 1024³ world; 1/2/4/8-GPU"
-EXTRA_CONFIGS = ("C2", "C3", "C4")
+# Z1: the reference's own scene shape (SetUpFirstZone: 21 volumes, 10 triangles, point + 5 spot +
+# directional lights, depth 14, sky; scene.zone_scene) at 1920x1080
+EXTRA_CONFIGS = ("C2", "C3", "C4", "Z1")
 # Frames in flight per config (vpx_set_pipeline lanes, each on a dedicated hardware queue),
 # from the A/B on one MI355X (ms per step, 2 / 3 / 4 lanes): C1 - / 0.551-0.554 /
 # 0.578-0.594, C4 52.6 / 52.4 / 51.6; with the pools (round 3) C2 2.76-2.77 / 2.50-2.52 /
 # 2.42-2.45 as the process's first config but 2.57-2.69 (3) vs 2.87-2.90 (4) as an extra
 # config after C1 (the line the driver runs), C3 3.70-3.71 / 3.65 / 3.67-3.71.
-PIPELINE = {"C1": 3, "C2": 3, "C3": 3, "C4": 4}
+PIPELINE = {"C1": 3, "C2": 3, "C3": 3, "C4": 4, "Z1": 3}
 STAGE_KERNELS = {"primary": "k_primary", "shade": "k_shade", "shadow": "k_shadow_tile", "resolve": "k_resolve",
-                 "bounce": "k_nearest_tile", "finish": "k_finish", "frame": "k_frame0", "paths": "k_path_pool"}
+                 "bounce": "k_nearest_tile", "finish": "k_finish", "frame": "k_frame0", "instances": "k_instances"}
 
 
 def weak_size(n, base=(1920, 1080)):
@@ -276,8 +278,6 @@ def run_config(pkg, env, cfg, steps, warmup, weak=False, sha=None, pipeline=None
             alg_bytes = local_pix / K / spp * 36.0
         elif dom == "frame":  # k_frame0: the whole depth-0 frame (every stage's cells + the finish)
             alg_bytes = (sum(float(v[2]) for v in prof.values()) + local_pix * 36.0) / max(dom_launches, 1)
-        elif dom == "paths":  # k_path_pool: the bounce levels' walks (shadow + bounce rays) and the finish
-            alg_bytes = (float(dom_cells) + local_pix * 36.0) / max(dom_launches, 1)
         else:
             alg_bytes = float(dom_cells) / max(dom_launches, 1)
             if dom == "shadow" and fused:
@@ -289,10 +289,13 @@ def run_config(pkg, env, cfg, steps, warmup, weak=False, sha=None, pipeline=None
         out = {
             "config": cfg, "value": round((prim + shad) / elapsed / 1e6, 3), "ms_per_step": round(ms_step, 4),
             "total_mray_s": round((prim + shad + bounce) / elapsed / 1e6, 3),
-            "workload": f"{cfg}: {W}x{H}, {desc.grids[0].n}^3 {desc.name}, {spp} spp, Trace depth {desc.max_bounces}"
+            "workload": f"{cfg}: {W}x{H}, {max(g.n for g in desc.grids)}^3 {desc.name}, {spp} spp, Trace depth "
+                        f"{desc.max_bounces}"
                         + (f", {len(desc.volumes)} volumes" if len(desc.volumes) > 1 else "")
+                        + (f", {len(desc.triangles)} triangles" if desc.triangles else "")
+                        + (f", {len(desc.spots)} spot lights" if desc.spots else "")
                         + (f", {len(desc.areas)} area lights x {desc.area_samples} samples" if desc.areas else ""),
-            "width": W, "height": H, "world_n": desc.grids[0].n, "max_bounces": desc.max_bounces, "spp": spp,
+            "width": W, "height": H, "world_n": max(g.n for g in desc.grids), "max_bounces": desc.max_bounces, "spp": spp,
             "rays_per_step": {"primary": prim / K, "shadow": shad / K, "bounce": bounce / K, "dda_cells": cells / K},
             "mpix_per_s": round(prim / elapsed / 1e6, 3),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",

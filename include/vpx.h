@@ -371,9 +371,9 @@ int vpx_get_counters(vpx_ctx* ctx, vpx_stats* out, int reset);
 #define VPX_STAGE_FINISH 5   /* fold + accumulate + tonemap (or tile pack)              */
 #define VPX_STAGE_FRAME 6    /* a whole Trace-depth-0 frame in one launch (small launches,
                                 single volume: stages 0, 1, 2, 3, 5 fused)    */
-#define VPX_STAGE_PATHS 7    /* the bounce levels of a single-volume frame in one persistent
-                                launch after the primary stage (the path pool: levels' shadow
-                                walks, light sums, bounce walks, shades, and the finish)    */
+#define VPX_STAGE_INSTANCES 7 /* multi-volume scenes: the primary rays' Renderer::FindNearest
+                                over the volumes after the world (volume 0, walked in stage 0)
+                                and the analytic shapes, then level 0's shade */
 #define VPX_NUM_STAGES 8
 typedef struct vpx_profile {
     float stage_ms[8];            /* summed device time per stage (HIP events on the stream) */

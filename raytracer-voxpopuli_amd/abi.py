@@ -109,7 +109,7 @@ class BvhNode(C.Structure):  # vpx_bvh_node: BVHNode (BasicBVH.h:11-20)
 BVH_MAX_TRIS = 512
 BVH_MAX_DEPTH = 63
 
-STAGES = ("primary", "shade", "shadow", "resolve", "bounce", "finish", "frame", "paths")
+STAGES = ("primary", "shade", "shadow", "resolve", "bounce", "finish", "frame", "instances")
 
 STRUCT_SIZES = {PrevCamera: 64, Profile: 160, Volume: 160, Material: 32, PointLight: 24, SpotLight: 40, AreaLight: 32, DirLight: 24,
                 Sphere: 32, Triangle: 64, Camera: 80, FrameParams: 48, Ray: 32, Hit: 32, Stats: 40,

@@ -29,6 +29,9 @@ using namespace vpx;
 namespace {
 
 constexpr int kTile = 16;  // 16x16 pixels per tile / 256-thread workgroup
+#ifndef VPX_SPLIT_PRIMARY
+#define VPX_SPLIT_PRIMARY 1  // multi-volume primary rays: lean world walk + instance pass (k_instances)
+#endif
 #ifndef VPX_LANE_TAIL
 #define VPX_LANE_TAIL 1  // frames in flight blend in their own tail launch where they have one (lane_tail_ok)
 #endif
@@ -420,9 +423,6 @@ __global__ void checksum_k(const uint8_t* __restrict__ cells, uint64_t count, un
 struct vpx_ctx {
     int device = 0;
     uint32_t cus = 256;  // compute units of the device (the bounce pool's grid)
-    // bounce levels through the path pool (k_path_pool); VPX_PATH_POOL=0 in the environment at
-    // vpx_create selects the per-level kernels instead (A/B and parity tests)
-    bool path_pool = true;
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
     std::string err;
@@ -811,32 +811,26 @@ int launch_render(vpx_ctx* c, hipStream_t s, vpx_ctx::WaveStore& ws, const Scene
         VPX_HIP(c, hipGetLastError());
         return VPX_OK;
     }
-    if (one && fuse_tail && f.max_bounces > 0 && c->path_pool) {
-        // the bounce levels in one persistent launch (k_path_pool): the fused head walks the
-        // primary rays and shades level 0, the pool carries every path through the rest of
-        // its chain and finishes its pixel
-        prof_mark(c, s, VPX_STAGE_PRIMARY);
-        hipLaunchKernelGGL((k_primary<true, true>), grid, block, 0, s, sv, f, w, c->d_ctr);
-        prof_mark(c, s, -1);
-        const uint32_t grabs = (P / 64u + kPoolGrab - 1u) / kPoolGrab;
-        const uint32_t waves = std::min(grabs, c->cus * 4u * (uint32_t)VPX_WPE_PATHS);
-        const uint32_t wpb = kPoolWg / 64u;
-        prof_mark(c, s, VPX_STAGE_PATHS);
-        hipLaunchKernelGGL((k_path_pool<MODE>), dim3((waves + wpb - 1u) / wpb), dim3(kPoolWg), 0, s, sv, f, w,
-                           c->d_ctr, accum, rgb8, packed);
-        prof_mark(c, s, -1);
-        VPX_HIP(c, hipGetLastError());
-        return VPX_OK;
-    }
     prof_mark(c, s, VPX_STAGE_PRIMARY);
     const bool fuse_head = f.max_bounces >= 0;  // level 0's shade at the end of k_primary
-    if (fuse_head)
+    // multi-volume / shape scenes: the world walk in the lean head, then the instance pass
+    // (the rest of FindNearest for the rays that can still meet a later volume or a shape, and
+    // level 0's shade; k_instances)
+    const bool split = !one && fuse_head && VPX_SPLIT_PRIMARY;
+    if (split)
+        hipLaunchKernelGGL((k_primary<true, false>), grid, block, 0, s, sv, f, w, c->d_ctr);
+    else if (fuse_head)
         hipLaunchKernelGGL((one ? k_primary<true, true> : k_primary<false, true>), grid, block, 0, s, sv, f, w,
                            c->d_ctr);
     else
         hipLaunchKernelGGL((one ? k_primary<true, false> : k_primary<false, false>), grid, block, 0, s, sv, f,
                            w, c->d_ctr);
     prof_mark(c, s, -1);
+    if (split) {
+        prof_mark(c, s, VPX_STAGE_INSTANCES);
+        hipLaunchKernelGGL(k_instances, grid, block, 0, s, sv, f, w, c->d_ctr);
+        prof_mark(c, s, -1);
+    }
     // the last level's shadow -> resolve -> finish as one launch (k_shadow_finish)
     for (int level = 0; level <= f.max_bounces; ++level) {
         if (!(fuse_head && level == 0)) {
@@ -904,12 +898,10 @@ int launch_render(vpx_ctx* c, hipStream_t s, vpx_ctx::WaveStore& ws, const Scene
 }
 
 // Whether a frame's blend can run as its own tail launch on the lane (launch_render's spool
-// tail, k_resolve_finish): area lights with several samples (the shadow pool), outside the
-// path pool (single volume with bounces: its finish is inside the persistent launch).
-bool lane_tail_ok(const vpx_ctx* c, const SceneView& sv, const FrameArgs& f) {
+// tail, k_resolve_finish): area lights with several samples (the shadow pool).
+bool lane_tail_ok(const SceneView& sv, const FrameArgs& f) {
     const uint32_t S = sv.num_areas ? (uint32_t)std::max(1, sv.area_samples) : 1u;
-    const bool one = sv.num_volumes == 1 && !(sv.num_spheres | sv.num_triangles);
-    return VPX_LANE_TAIL && S > 1 && f.max_bounces >= 0 && !(one && f.max_bounces > 0 && c->path_pool);
+    return VPX_LANE_TAIL && S > 1 && f.max_bounces >= 0;
 }
 
 // Frames in flight: render `tiles` tiles of frame f as packed float4 samples (into `out`, or
@@ -1013,7 +1005,6 @@ int vpx_create(int device, vpx_ctx** out) {
     }
     c->stream = c->own_stream;
     (void)hipMemset(c->d_ctr, 0, kCtrWords * kCtrStripes * sizeof(unsigned long long));
-    if (const char* e = std::getenv("VPX_PATH_POOL")) c->path_pool = std::strcmp(e, "0") != 0;
     *out = c;
     return VPX_OK;
 }
@@ -1601,7 +1592,7 @@ int vpx_render(vpx_ctx* c, const vpx_frame_params* p, float* accum, uint32_t* rg
     VPX_HIP(c, hipSetDevice(c->device));
     const SceneView sv = view_of(c, p->sky, p->area_samples, (p->flags & VPX_FLAG_SKY) != 0);
     const FrameArgs f = frame_of(c, p, 0, 1);
-    if (!c->lanes.empty() && !stats && !(p->flags & VPX_FLAG_NO_TONEMAP) && lane_tail_ok(c, sv, f)) {
+    if (!c->lanes.empty() && !stats && !(p->flags & VPX_FLAG_NO_TONEMAP) && lane_tail_ok(sv, f)) {
         // frames in flight whose tail is a launch of its own (k_resolve_finish after the shadow
         // pool): the whole frame runs on its lane, the tail blending straight into the caller's
         // accumulator once the caller's stream has reached this call (which orders it after

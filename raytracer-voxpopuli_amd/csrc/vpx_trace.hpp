@@ -749,7 +749,9 @@ __device__ __forceinline__ bool tlas_box(const TlasNode& nd, f3 o, f3 inv, float
 // candidates in increasing index order, each lane only its own — the linear loop restricted
 // to volumes some lane can reach, one call site of the walk.  body(i) returns false to end
 // the lane's loop (IsOccluded's first occluder).
-template <class Body>
+// SKIP0: volume 0 was walked already (the instance pass, k_instances, after the world pass):
+// start from the tree with the bound as it stands.
+template <bool SKIP0 = false, class Body>
 __device__ __forceinline__ void for_volumes(const SceneView& sv, f3 o, f3 d, const float& bound, Body body) {
     bool live = true, first = true;
     uint64_t mine = 0, any = 0;  // this lane's / the wave's candidates, bit k = volume k + 1
@@ -760,7 +762,7 @@ __device__ __forceinline__ void for_volumes(const SceneView& sv, f3 o, f3 d, con
             i = (uint32_t)__ffsll((unsigned long long)any);
             any &= any - 1;
         }
-        if (live && (first || ((mine >> (i - 1u)) & 1u))) live = body(i);
+        if (live && (first ? !SKIP0 : ((mine >> (i - 1u)) & 1u))) live = body(i);
         if (first) {
             first = false;
             mine = sv.tlas_always;
@@ -841,6 +843,70 @@ __device__ __forceinline__ int32_t find_nearest(const SceneView& sv, Ray& r, Cou
         }
     }
     return vox;
+}
+
+// Renderer::FindNearest from volume 1 on (renderer.cpp:946-1018), for a ray whose walk of
+// volume 0 already left r.t / the hit record (*vox = 0 on a hit there, else -2): the
+// instance pass of multi-volume primary rays (k_instances), whose world walk ran in the lean
+// single-volume kernel (k_primary<true, false>).  The same loop from the same state — the
+// later volumes through the TLAS (or linearly), then the shapes — so the same winner, t and
+// counts as find_nearest; the FindNearest call itself was counted by the world pass.
+// Returns whether the record changed (a later volume or a shape won: r.t, r.N, r.mat, *vox).
+template <uint32_t SKIPW = kSkipwNearest, uint32_t MINC = kMincNearest, uint32_t RUN = kRunNearest>
+__device__ __forceinline__ bool find_nearest_rest(const SceneView& sv, Ray& r, Counters& k, int32_t* vox_io) {
+    int32_t vox = *vox_io;
+    const int32_t vox0 = vox;
+    uint32_t hx = 0, hy = 0, hz = 0;
+    auto visit = [&](uint32_t i) {
+        if (misses_volume(sv.vbounds[i], r.O, r.D)) return true;  // Setup3DDDA would fail
+        const vpx_volume& vol = sv.volumes[i];
+        const DevGrid g = sv.grids[vol.grid_id];
+        skip::Walk w;
+        {
+            ORay o;
+            o.O = xform_pos_ssem(r.O, vol.inv_matrix);
+            o.D = xform_vec_ssem(r.D, vol.inv_matrix);
+            o.rD = mk(__fdiv_rn(1.0f, o.D.x), __fdiv_rn(1.0f, o.D.y), __fdiv_rn(1.0f, o.D.z));
+            Dda s;
+            if (!dda_setup(vol, g.n, o, s)) return true;
+            w = to_walk(s);
+        }
+        if (walk_wave<0, SKIPW, MINC, RUN>(grid_view(g), w, r.t, k.cells)) {
+            r.t = w.t;
+            hx = w.X, hy = w.Y, hz = w.Z;
+            vox = (int32_t)i;
+        }
+        return true;
+    };
+    if (sv.tlas_on)
+        for_volumes<true>(sv, r.O, r.D, r.t, visit);
+    else
+        for (uint32_t i = 1; i < sv.num_volumes; ++i) visit(i);
+    bool changed = vox != vox0;
+    if (changed) {
+        const vpx_volume& vol = sv.volumes[vox];
+        const DevGrid g = sv.grids[vol.grid_id];
+        ORay o;
+        o.O = xform_pos_ssem(r.O, vol.inv_matrix);
+        o.D = xform_vec_ssem(r.D, vol.inv_matrix);
+        r.N = normal_voxel(o, r.t, g.n, vol.matrix);
+        r.mat = g.cells[(uint64_t)hx + (uint64_t)hy * g.n + (uint64_t)hz * ((uint64_t)g.n * g.n)];
+    }
+    if (sv.num_spheres | sv.num_triangles) {
+        Ray sh = make_ray(r.O, r.D);
+        for (uint32_t i = 0; i < sv.num_spheres; ++i) sphere_hit(sv.spheres[i], sh);
+        for (uint32_t i = 0; i < sv.num_triangles; ++i) tri_hit(sv.triangles[i], sh);
+        if (r.t > sh.t) {
+            r.t = sh.t;
+            r.mat = sh.mat;
+            r.N = sh.N;
+            r.inside = sh.inside;
+            vox = -1;
+            changed = true;
+        }
+    }
+    *vox_io = vox;
+    return changed;
 }
 
 // Renderer::IsOccluded, renderer.cpp:209-243 (scalar transforms, exact 1/D).  The linear

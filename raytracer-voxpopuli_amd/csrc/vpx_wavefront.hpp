@@ -832,6 +832,63 @@ __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_NEAREST : VPX_WPE_MULTI_
     primary_tile<ONE, SHADE>(sv, f, w, L, ctr);
 }
 
+// Multi-volume primary rays in two launches: the world (volume 0, first in the reference's
+// loop) walked by the lean single-volume head (k_primary<true, false>: 6 waves/SIMD, no
+// spills) writing the hit records to HBM, then this instance pass: per tile, the paths whose
+// ray can still meet a later volume or a shape — the TLAS root box within the ray's segment
+// [0, world t], or every active path when there are shapes, instances outside the tree or no
+// TLAS — compacted into the first waves, Renderer::FindNearest continued from volume 1
+// (find_nearest_rest: the same candidates, order, bounds and counts as the one-launch loop),
+// then level 0's shade for every path of the tile.  The one-launch kernel
+// (k_primary<false, true>) carried the whole volume loop's state through the world walk (112
+// VGPRs, 72 spilled SGPRs, 4 waves/SIMD), and every ray of the frame through the instance
+// loop: C4's primary stage took 1.46 ms against 0.59 ms for the world alone (tools/c4_split.py).
+__global__ __launch_bounds__(256) VPX_WPE(VPX_WPE_MULTI_NEAREST) void k_instances(SceneView sv, FrameArgs f, WaveBufs w,
+                                                                                unsigned long long* __restrict__ ctr) {
+    __shared__ uint32_t sh[4];
+    __shared__ uint32_t lst[256];
+    const uint32_t tb = tile_block() * 256u;
+    const uint32_t p = tb + threadIdx.x;
+    const PathRay pr{w.O, w.D, w.H, w.HM, 0u};
+    Counters k{0u, 0u, 0u};
+    bool go = false;
+    if (p < w.P && (__float_as_uint(w.D[p].w) & kActive)) {
+        go = true;
+        if (sv.tlas_on && !sv.tlas_always && !(sv.num_spheres | sv.num_triangles) && sv.tlas_nodes) {
+            const float4 o = w.O[p], d = w.D[p];
+            const f3 inv = mk(__fdiv_rn(1.0f, d.x), __fdiv_rn(1.0f, d.y), __fdiv_rn(1.0f, d.z));
+            go = tlas_box(sv.tlas[0], mk(o.x, o.y, o.z), inv, w.H[p].x);  // conservative (tlas_box)
+        }
+    }
+    uint32_t total;
+    const uint32_t at = block_scan(go ? 1u : 0u, total, sh);
+    if (go) lst[at] = p;
+    __syncthreads();
+    if (threadIdx.x < total) {
+        const uint32_t q = lst[threadIdx.x];
+        const float4 o = w.O[q], d = w.D[q], h = w.H[q];
+        const uint32_t hm = w.HM[q];
+        Ray r;
+        r.O = mk(o.x, o.y, o.z);
+        r.D = mk(d.x, d.y, d.z);
+        r.t = h.x;
+        r.N = mk(h.y, h.z, h.w);
+        r.mat = hm & 0xffu;
+        r.inside = (hm & 0x80000000u) != 0u;
+        int32_t vox = (int32_t)((hm >> 8) & 0xffffu) - 2;
+        if (find_nearest_rest(sv, r, k, &vox)) {
+            w.H[q] = make_float4(r.t, r.N.x, r.N.y, r.N.z);
+            w.HM[q] = r.mat | ((uint32_t)(vox + 2) << 8) | (r.inside ? 0x80000000u : 0u);
+        }
+    }
+    flush_counters(k, 0u, ctr, VPX_STAGE_INSTANCES);
+    __syncthreads();  // the tile's hit records, as the compacted lanes left them
+    Counters ks{0u, 0u, 0u};
+    const bool cont = shade_path<true>(sv, f, w, pr, p, 0, ks);
+    if (f.max_bounces > 0) put_amask(w, p, cont);
+    flush_counters(ks, 0u, ctr, VPX_STAGE_SHADE);
+}
+
 // Renderer::FindNearest for the active paths of a tile (bounce levels).  Rejected (DESIGN.md
 // §4): grouping a tile's walks by direction octant (C2 4.88 vs 4.82 ms), gathering 2 / 4 / 8
 // tiles per workgroup (C1 2.87 / 3.22 / 4.36 vs 2.70 ms: walk lengths are heavy-tailed, a
@@ -1361,208 +1418,6 @@ __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_SHADOW : VPX_WPE_MULTI_S
     LightSum ls;
     resolve_path(sv, w, p, occ, &ls);
     finish_path<MODE>(f, w, p, accum, rgb8, packed, &ls);
-}
-
-// ------------------------------------------------------------------ the path pool
-// Trace's bounce levels (renderer.cpp:1076-1328 below depth max_bounces) of a single-volume,
-// shape-free frame in ONE persistent launch after the fused head (k_primary<true, true>: the
-// primary walks and level 0's shade, coherent tile by tile).  A lane carries one path through
-// the rest of its chain — level l's shadow walks (Renderer::IsOccluded per slot), its light
-// sum (resolve), the next ray's Renderer::FindNearest walk, level l+1's shade (the material
-// switch), ... — then finishes its pixel (fold + accumulate / packed sample) and takes the
-// next path.  Every step is the per-path function the level kernels run (shade_path,
-// resolve_path, nearest_begin/end_1v, finish_path, the shadow walk of shadow_tile), in the
-// same per-path order (a level's light sum before the next level's shade overwrites SM), so
-// values, RNG streams and counts are the level kernels'.  What goes: the per-level launches
-// and their drains (a level waited for its slowest walk), the tile shadow kernels' sparse
-// waves (a tile's ~40 shadow rays at a bounce level), and the HBM round trips of a level's
-// records between kernels — a lane reads back what it wrote microseconds earlier (L2).
-// Walks of both kinds share the wave: a lane's walk returns when kPoolLeave lanes have
-// finished theirs, the finished lanes advance their paths (the "service": shade / resolve /
-// finish, divergent but short next to the walks) and the walk resumes.  The walk words are
-// the bounce pool's for both kinds (they decide where a lane skips, never what it visits).
-#ifndef VPX_WPE_PATHS
-#define VPX_WPE_PATHS 3
-#endif
-enum PathPhase : int {
-    kPhIdle = 0,      // no path
-    kPhShadowNext,    // start the level's next shadow slot walk, or resolve when none is left
-    kPhResolve,       // the level's light sum, then the next ray or the finish
-    kPhNearest,       // start the next ray's FindNearest walk
-    kPhShade,         // the next level's material switch
-    kPhWalkShadow,    // walking slot s
-    kPhWalkNearest,   // walking the next ray
-};
-// A lane's walk state (skip::Walk without m2, which the octant-plane walk never reads, and
-// the walk's bound) parked in the wave's LDS while the finished lanes advance their paths: the
-// service code (the shade above all, ~90 VGPRs alone) then does not have to share the register
-// file with 64 lanes' live walks (with them in registers the kernel needed 161 VGPRs, or spilled
-// ~650 at 96).  Struct of arrays, one dword per lane per field.
-struct WalkPark {
-    uint32_t u[8][64];  // X, Y, Z, sx, sy, sz, osh, m1 (low word: a skipping lane's cube byte)
-    float f[8][64];     // t, tx, ty, tz, dx, dy, dz, bound
-    __device__ __forceinline__ void put(uint32_t l, const skip::Walk& w, float bound) {
-        u[0][l] = w.X, u[1][l] = w.Y, u[2][l] = w.Z;
-        u[3][l] = (uint32_t)w.sx, u[4][l] = (uint32_t)w.sy, u[5][l] = (uint32_t)w.sz;
-        u[6][l] = w.osh, u[7][l] = (uint32_t)w.m1;
-        f[0][l] = w.t, f[1][l] = w.tx, f[2][l] = w.ty, f[3][l] = w.tz;
-        f[4][l] = w.dx, f[5][l] = w.dy, f[6][l] = w.dz, f[7][l] = bound;
-    }
-    __device__ __forceinline__ void get(uint32_t l, skip::Walk& w, float& bound) const {
-        w.X = u[0][l], w.Y = u[1][l], w.Z = u[2][l];
-        w.sx = (int32_t)u[3][l], w.sy = (int32_t)u[4][l], w.sz = (int32_t)u[5][l];
-        w.osh = u[6][l], w.m1 = u[7][l], w.m2 = 0ull;
-        w.t = f[0][l], w.tx = f[1][l], w.ty = f[2][l], w.tz = f[3][l];
-        w.dx = f[4][l], w.dy = f[5][l], w.dz = f[6][l], bound = f[7][l];
-    }
-};
-
-// The single volume's record as wave-uniform values (scalar registers), read once at kernel
-// start: loads of sv.volumes[0] inside a loop that also stores to global memory cannot be
-// scalar loads (the compiler cannot prove them unclobbered), so every use became a per-lane
-// vector load of the 12-float matrices into VGPRs.
-__device__ __forceinline__ vpx_volume uniform_volume(const vpx_volume* v) {
-    vpx_volume u;
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(v);
-    uint32_t* dst = reinterpret_cast<uint32_t*>(&u);
-#pragma unroll
-    for (uint32_t i = 0; i < sizeof(vpx_volume) / 4u; ++i) dst[i] = __builtin_amdgcn_readfirstlane(src[i]);
-    return u;
-}
-
-template <int MODE>
-__global__ __launch_bounds__(kPoolWg) VPX_WPE(VPX_WPE_PATHS) void k_path_pool(
-    SceneView sv, FrameArgs f, WaveBufs w, unsigned long long* __restrict__ ctr, float4* __restrict__ accum,
-    uint32_t* __restrict__ rgb8, float4* __restrict__ packed) {
-    __shared__ uint32_t lst_wg[kPoolWg / 64][kPoolGrab * 64];
-    __shared__ WalkPark park_wg[kPoolWg / 64];
-    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    uint32_t* lst = lst_wg[wv];
-    WalkPark& park = park_wg[wv];
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t words = (w.P + 63u) >> 6, grabs = (words + kPoolGrab - 1u) / kPoolGrab;
-    const PathRay pr{w.O, w.D, w.H, w.HM, 0u};
-    const vpx_volume vol = uniform_volume(&sv.volumes[0]);
-    const skip::GridView gv = grid_view(sv.grids[vol.grid_id]);
-    Counters k{0u, 0u, 0u};
-    uint32_t q = ~0u;  // the path this lane carries
-    int ph = kPhIdle, mode = kWalkMiss;
-    uint32_t lvl = 0u, rem = 0u, occ = 0u, s = 0u;  // level, slots left, occluded slots, slot walked
-    uint32_t avail = 0u, cur = 0u;
-    bool more = true;
-    {
-        skip::Walk w0;
-        w0.X = w0.Y = w0.Z = 0u, w0.sx = w0.sy = w0.sz = 1, w0.osh = 0u, w0.m1 = w0.m2 = 0ull;
-        w0.t = w0.tx = w0.ty = w0.tz = w0.dx = w0.dy = w0.dz = 0.f;
-        park.put(lane, w0, 0.f);
-    }
-    for (;;) {
-        // service: every lane's path to its next walk (its state parked in LDS meanwhile); idle
-        // lanes take new paths.  A lane that starts a walk parks the new state.
-        for (;;) {
-            if (ph == kPhShade) {
-                ++lvl;
-                (void)shade_path<false>(sv, f, w, pr, q, (int)lvl, k);
-                rem = w.smask[q] & kSlotBits;
-                occ = 0u;
-                ph = kPhShadowNext;
-            }
-            if (ph == kPhShadowNext) {
-                ph = kPhResolve;
-                while (rem) {  // shadow_tile's per-slot IsOccluded in the single volume
-                    s = (uint32_t)__ffs(rem) - 1u;
-                    rem &= rem - 1u;
-                    ++k.shadow;
-                    const uint64_t slot = (uint64_t)s * w.P + q;
-                    const float4 so = w.SO[slot], sd = w.SD[slot];
-                    ORay o;
-                    o.O = xform_pos(mk(so.x, so.y, so.z), vol.inv_matrix);
-                    o.D = xform_vec(mk(sd.x, sd.y, sd.z), vol.inv_matrix);
-                    o.rD = mk(__fdiv_rn(1.0f, o.D.x), __fdiv_rn(1.0f, o.D.y), __fdiv_rn(1.0f, o.D.z));
-                    Dda d;
-                    if (dda_setup(vol, gv.n, o, d)) {
-                        park.put(lane, to_walk(d), so.w);
-                        mode = kWalkStep;
-                        ph = kPhWalkShadow;
-                        break;
-                    }
-                }
-            }
-            if (ph == kPhResolve) {
-                const uint32_t ob = occ;
-                resolve_path_by(sv, w, q, [ob](uint32_t sl, uint64_t) -> bool { return (ob >> sl) & 1u; }, nullptr);
-                // a next ray: the shade wrote an active D (a leaf path's D is inactive; the last
-                // level's shade writes none, hence the level test)
-                ph = (lvl < (uint32_t)f.max_bounces && (__float_as_uint(w.D[q].w) & kActive)) ? kPhNearest : kPhIdle;
-                if (ph == kPhIdle) {  // the chain is complete: fold, accumulate / pack
-                    finish_path<MODE>(f, w, q, accum, rgb8, packed);
-                    q = ~0u;
-                    mode = kWalkMiss;
-                }
-            }
-            if (ph == kPhNearest) {
-                skip::Walk wn;
-                if (nearest_begin_v(vol, gv.n, pr, q, k, wn)) {
-                    park.put(lane, wn, kBig);
-                    mode = kWalkStep;
-                    ph = kPhWalkNearest;
-                } else {  // Setup3DDDA fails: the miss record, shaded at once
-                    nearest_end_v(vol, gv.cells, gv.n, pr, q, wn, false);
-                    ph = kPhShade;
-                }
-            }
-            if (__ballot(ph == kPhShade)) continue;
-            const uint64_t idle = __ballot(ph == kPhIdle);
-            if (!idle || !more) break;
-            if (avail == 0u) {  // the next grab's paths (every path of level 0 goes through the pool)
-                uint32_t gi = 0u;
-                if (lane == 0u) gi = atomicAdd(&w.pool[0], 1u);
-                gi = __builtin_amdgcn_readfirstlane(gi);
-                if (gi >= grabs) {
-                    more = false;
-                    break;
-                }
-                wave_sync();  // the wave's earlier reads of lst are done
-                uint32_t n = 0u;
-#pragma unroll
-                for (uint32_t j = 0; j < kPoolGrab; ++j) {
-                    const uint32_t p0 = (gi * kPoolGrab + j) * 64u;
-                    if (p0 + lane < w.P) lst[n + lane] = p0 + lane;
-                    n += p0 < w.P ? min(64u, w.P - p0) : 0u;
-                }
-                wave_sync();
-                avail = n;
-                cur = 0u;
-                continue;
-            }
-            const uint32_t take = min((uint32_t)__popcll(idle), avail);
-            const uint32_t r = lane_rank(idle);
-            if (ph == kPhIdle && r < take) {  // a path after level 0's shade (k_primary)
-                q = lst[cur + r];
-                lvl = 0u;
-                rem = w.smask[q] & kSlotBits;
-                occ = 0u;
-                ph = kPhShadowNext;
-            }
-            cur += take;
-            avail -= take;
-        }
-        if (!__ballot(q != ~0u)) break;  // the pool is empty and every path is finished
-        skip::Walk wk;
-        float bound;
-        park.get(lane, wk, bound);
-        walk_wave<0, kSkipwBouncePool, kMincBouncePool, kRunBouncePool, true>(gv, wk, bound, k.cells, &mode,
-                                                                              more ? kPoolLeave : 65u);
-        if (ph == kPhWalkShadow && mode >= kWalkMiss) {  // IsOccluded's answer for slot s
-            occ |= (mode == kWalkHit ? 1u : 0u) << s;
-            ph = kPhShadowNext;
-        } else if (ph == kPhWalkNearest && mode >= kWalkMiss) {  // the next ray's hit record
-            nearest_end_v(vol, gv.cells, gv.n, pr, q, wk, mode == kWalkHit);
-            ph = kPhShade;
-        }
-        park.put(lane, wk, bound);
-    }
-    flush_counters(k, 0u, ctr, VPX_STAGE_PATHS);
 }
 
 // The other levels' tail is NOT fused the same way (IsOccluded walks + barrier + resolve as

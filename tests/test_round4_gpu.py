@@ -1,17 +1,14 @@
-"""The path pool (k_path_pool, round 4) and the reference's own scene shape, on the GPU.
+"""Round-4 GPU parity: bounce-level frames, the reference's own scene shape, frames in flight
+that blend in their own tail launch, and the split multi-volume primary stage.
 
-k_path_pool carries each path of a single-volume frame through its bounce levels in one
-persistent launch.  Every frame here is compared bit for bit with the oracle
-(accumulator floats, RGB8 bytes, ray and DDA-cell counts) and with the per-level kernels
-(VPX_PATH_POOL=0 at context creation), over the paths' whole variety: point / area lights
-(1 and several slots per path), glass and smoke interiors (roomGlass, the smoke ball),
-depths 1..14 (the deepest forms word), AA, accumulated frames and frames in flight.
-
-The zone scene (scene.zone_scene: Renderer::SetUpFirstZone's 21 volumes, 10 triangles, point
-+ 5 spot + directional lights, depth 14, sky) runs the multi-volume path.
+Every frame here is compared bit for bit with the oracle (accumulator floats, RGB8 bytes, ray
+and DDA-cell counts): single-volume bounce frames over the paths' variety (point / area lights
+with 1 and several slots per path, glass and smoke interiors, depths 1..14, AA, accumulated
+frames); the zone scene (scene.zone_scene: Renderer::SetUpFirstZone's 21 volumes, 10
+triangles, point + 5 spot + directional lights, depth 14, sky); frames in flight whose tail is
+the shadow pool's k_resolve_finish (the lane blends into the accumulator itself); multi-volume
+primary rays through the world walk + instance pass (k_instances).
 """
-import os
-
 import numpy as np
 import pytest
 
@@ -24,16 +21,8 @@ if not torch.cuda.is_available():
 from cases import bits  # noqa: E402
 
 
-def render(pkg, desc, frames, pool, lanes=0):
-    old = os.environ.get("VPX_PATH_POOL")
-    os.environ["VPX_PATH_POOL"] = "1" if pool else "0"
-    try:
-        ctx = pkg.context.Context(0)
-    finally:
-        if old is None:
-            del os.environ["VPX_PATH_POOL"]
-        else:
-            os.environ["VPX_PATH_POOL"] = old
+def render(pkg, desc, frames, lanes=0):
+    ctx = pkg.context.Context(0)
     s = torch.cuda.Stream()
     ctx.set_stream(s.cuda_stream)
     ctx.load_scene(desc)
@@ -77,37 +66,22 @@ CASES = {
 
 
 @pytest.mark.parametrize("name", sorted(CASES))
-def test_path_pool_bit_exact(pkg, orc, name):
+def test_bounce_frames_bit_exact(pkg, orc, name):
     desc = CASES[name](pkg.scene)
     desc.flags = pkg.abi.VPX_FLAG_AA
     frames = 2
     a_o, r_o, t_o = oracle_frames(orc, pkg, desc, frames)
-    a_p, r_p, t_p = render(pkg, desc, frames, pool=True)
-    assert np.array_equal(a_p, a_o), "path pool accumulator differs from the oracle"
+    a_p, r_p, t_p = render(pkg, desc, frames)
+    assert np.array_equal(a_p, a_o), "accumulator differs from the oracle"
     assert np.array_equal(r_p, r_o)
     assert counts(t_p) == (t_o["primary_rays"], t_o["shadow_rays"], t_o["bounce_rays"], t_o["dda_cells"])
-    a_l, r_l, t_l = render(pkg, desc, frames, pool=False)
-    assert np.array_equal(a_l, a_p) and np.array_equal(r_l, r_p) and counts(t_l) == counts(t_p)
     assert t_p.bounce_rays > 0 and (t_p.shadow_rays > 0 or name.startswith("teapot"))  # the teapot is glass: no light samples
 
 
-@pytest.mark.parametrize("lanes", [2, 3])
-def test_path_pool_frames_in_flight(pkg, orc, lanes):
-    """The pool in the packed-sample mode of frames in flight: 4 AA frames on `lanes` lanes
-    equal the serial frames and the oracle."""
-    sc = pkg.scene
-    desc = sc.city_scene("roomGlass", 128, 96, 64, 4)
-    desc.flags = pkg.abi.VPX_FLAG_AA
-    a_o, r_o, t_o = oracle_frames(orc, pkg, desc, 4)
-    a_p, r_p, t_p = render(pkg, desc, 4, pool=True, lanes=lanes)
-    assert np.array_equal(a_p, a_o) and np.array_equal(r_p, r_o)
-    assert counts(t_p) == (t_o["primary_rays"], t_o["shadow_rays"], t_o["bounce_rays"], t_o["dda_cells"])
-
-
-def test_path_pool_smoke_and_glass_interiors(pkg, orc):
+def test_smoke_and_glass_interiors(pkg, orc):
     """A world of a glass slab and a smoke ball (the interior exit marches of the shade: the
     glass and smoke branches' FindMaterialExit / FindSmokeExit, renderer.cpp:1146-1314) at
-    depth 6 through the pool."""
+    depth 6."""
     sc = pkg.scene
     n = 64
     z, y, x = np.meshgrid(*(np.arange(n),) * 3, indexing="ij")
@@ -122,7 +96,7 @@ def test_path_pool_smoke_and_glass_interiors(pkg, orc):
                      [], [], sc.dir_light((-0.3, -1.0, -0.2), (1.0, 1.0, 1.0)), (0.5, 0.5, -0.8), (0.5, 0.3, 0.5), 72, 56,
                      max_bounces=6)
     a_o, r_o, t_o = oracle_frames(orc, pkg, desc, 1)
-    a_p, r_p, t_p = render(pkg, desc, 1, pool=True)
+    a_p, r_p, t_p = render(pkg, desc, 1)
     assert np.array_equal(a_p, a_o) and np.array_equal(r_p, r_o)
     assert counts(t_p) == (t_o["primary_rays"], t_o["shadow_rays"], t_o["bounce_rays"], t_o["dda_cells"])
 
@@ -134,7 +108,7 @@ def test_zone_scene_bit_exact(pkg, orc, depth):
     desc = pkg.scene.zone_scene(96, 64, depth)
     desc.flags |= pkg.abi.VPX_FLAG_AA
     a_o, r_o, t_o = oracle_frames(orc, pkg, desc, 2)
-    a_g, r_g, t_g = render(pkg, desc, 2, pool=True)
+    a_g, r_g, t_g = render(pkg, desc, 2)
     assert np.array_equal(a_g, a_o) and np.array_equal(r_g, r_o)
     assert counts(t_g) == (t_o["primary_rays"], t_o["shadow_rays"], t_o["bounce_rays"], t_o["dda_cells"])
     assert t_g.bounce_rays > 0
@@ -155,8 +129,8 @@ def test_lane_tail_frames_in_flight(pkg, orc, scene, lanes):
         desc = sc.instanced_scene(n=128, inst_n=32, width=80, height=64, spp=1)
         desc.max_bounces = 2 if scene.endswith("d2") else 0
     desc.flags = pkg.abi.VPX_FLAG_AA
-    a_s, r_s, t_s = render(pkg, desc, 4, pool=True, lanes=0)
-    a_l, r_l, t_l = render(pkg, desc, 4, pool=True, lanes=lanes)
+    a_s, r_s, t_s = render(pkg, desc, 4, lanes=0)
+    a_l, r_l, t_l = render(pkg, desc, 4, lanes=lanes)
     assert np.array_equal(a_l, a_s) and np.array_equal(r_l, r_s) and counts(t_l) == counts(t_s)
     a_o, r_o, t_o = oracle_frames(orc, pkg, desc, 4)
     assert np.array_equal(a_s, a_o) and np.array_equal(r_s, r_o)
