@@ -1234,6 +1234,9 @@ __global__ __launch_bounds__(kPoolWg) VPX_WPE(VPX_WPE_SPOOL) void k_shadow_pool(
 #ifndef VPX_INST_MASK
 #define VPX_INST_MASK 1
 #endif
+#ifndef VPX_INST_CULL
+#define VPX_INST_CULL 1
+#endif
 __device__ __forceinline__ bool occluded_instances(const SceneView& sv, const float4* vb, const Ray& r, Counters& k) {
     const uint32_t nv = sv.num_volumes;
     uint64_t cand = 0ull;
@@ -1271,18 +1274,48 @@ __global__ __launch_bounds__(256) VPX_WPE(VPX_WPE_MULTI_SHADOW) void k_shadow_in
     __shared__ float4 vb[kTlasMaxVolumes];
     extern __shared__ uint32_t lst_dyn[];  // [S * 256]
     if (VPX_INST_MASK && threadIdx.x < sv.num_volumes && threadIdx.x < kTlasMaxVolumes)
-        vb[threadIdx.x] = sv.vbounds[threadIdx.x];  // published by block_scan's barriers
+        vb[threadIdx.x] = sv.vbounds[threadIdx.x];  // published by the barriers below
+    __shared__ uint32_t hist[kLightKeys];
+    if (threadIdx.x < kLightKeys) hist[threadIdx.x] = 0u;
     const uint32_t p = tile_block() * 256u + threadIdx.x;
     Counters k{0u, 0u, 0u};
-    const uint32_t m = p < w.P ? w.smask[p] & kSlotBits : 0u;
+    const uint32_t smv = p < w.P ? w.smask[p] : 0u;
+    const uint32_t m = smv & kSlotBits, key = smv >> 16;
+    // a slot whose segment [0, tmax] misses the instance TLAS's root box meets no instance (the
+    // root box holds every instance's inflated bounding sphere; a cube entered beyond tmax
+    // reads no cell, scene.cpp:1015): it is left unoccluded without a list entry
+    const bool cull = VPX_INST_CULL && sv.tlas_on && !sv.tlas_always && sv.tlas_nodes &&
+                      !(sv.num_spheres | sv.num_triangles);
     uint32_t mine = 0u;
     for (uint32_t b = m; b; b &= b - 1u) {
         const uint32_t sl = (uint32_t)__ffs(b) - 1u;
-        if (!w.occb[(uint64_t)sl * w.P + p]) mine |= 1u << sl;
+        const uint64_t slot = (uint64_t)sl * w.P + p;
+        if (w.occb[slot]) continue;
+        if (cull) {
+            const float4 so = w.SO[slot], sd = w.SD[slot];
+            const f3 inv = mk(__fdiv_rn(1.0f, sd.x), __fdiv_rn(1.0f, sd.y), __fdiv_rn(1.0f, sd.z));
+            if (!tlas_box(sv.tlas[0], mk(so.x, so.y, so.z), inv, so.w)) continue;
+        }
+        mine |= 1u << sl;
     }
-    uint32_t total;
-    uint32_t at = block_scan((uint32_t)__popc(mine), total, sh);
-    for (uint32_t b = mine; b; b &= b - 1u) lst_dyn[at++] = ((uint32_t)__ffs(b) - 1u) << 27 | p;
+    __syncthreads();  // hist zeroed (and vb staged)
+    // the tile's remaining slots grouped by light (shadow_tile's counting sort): a wave's lanes
+    // head the same way and share their candidate instances
+    const uint32_t pos = mine ? atomicAdd(&hist[key], (uint32_t)__popc(mine)) : 0u;
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        const uint32_t v = threadIdx.x < kLightKeys ? hist[threadIdx.x] : 0u;
+        uint32_t t;
+        const uint32_t ex = wave_prefix(v, t);
+        if (threadIdx.x < kLightKeys) hist[threadIdx.x] = ex;
+        if (threadIdx.x == 0) sh[0] = t;
+    }
+    __syncthreads();
+    const uint32_t total = __builtin_amdgcn_readfirstlane(sh[0]);
+    {
+        uint32_t at = mine ? hist[key] + pos : 0u;
+        for (uint32_t b = mine; b; b &= b - 1u) lst_dyn[at++] = ((uint32_t)__ffs(b) - 1u) << 27 | p;
+    }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < total; i += 256u) {
         const uint32_t e = lst_dyn[i];

@@ -15,6 +15,7 @@ b() { tag=$1; cfg=$2; st=$3; shift 3; timeout -k 10 300 env "$@" python bench.py
 for rep in 1 2; do
   b C4_split.$rep C4 3 VPX_LIB=var/lib_base.so
   b C4_nosplit.$rep C4 3 VPX_LIB=var/lib_nosplit.so
+  b C4_nocull.$rep C4 3 VPX_LIB=var/lib_nocull.so
   b Z1_split.$rep Z1 10 VPX_LIB=var/lib_base.so
   b Z1_nosplit.$rep Z1 10 VPX_LIB=var/lib_nosplit.so
 done
