@@ -816,7 +816,9 @@ int launch_render(vpx_ctx* c, hipStream_t s, vpx_ctx::WaveStore& ws, const Scene
     // multi-volume / shape scenes: the world walk in the lean head, then the instance pass
     // (the rest of FindNearest for the rays that can still meet a later volume or a shape, and
     // level 0's shade; k_instances)
-    const bool split = !one && fuse_head && VPX_SPLIT_PRIMARY;
+    // (scenes with analytic shapes test them on every ray, so no ray skips the second pass
+    // there: they keep the one-launch kernel — Z1 2.61-2.62 vs 2.63 ms split, round 4)
+    const bool split = !one && fuse_head && VPX_SPLIT_PRIMARY && !(sv.num_spheres | sv.num_triangles);
     if (split)
         hipLaunchKernelGGL((k_primary<true, false>), grid, block, 0, s, sv, f, w, c->d_ctr);
     else if (fuse_head)

@@ -53,6 +53,9 @@ struct DevGrid {
 // is hit and at `skip` (the node after its subtree) when missed; a leaf holds the bit mask
 // of its volumes (bit k = volume k + 1).
 constexpr uint32_t kTlasMaxVolumes = 65;
+#ifndef VPX_TLAS_SLOAD
+#define VPX_TLAS_SLOAD 1  // the instance pass reads the TLAS and its candidates' records with scalar loads
+#endif
 constexpr uint32_t kTlasMaxNodes = 64;
 struct TlasNode {
     float lo[3];
@@ -86,6 +89,32 @@ struct SceneView {
     float sky_hdr;
     uint32_t sky_tex;
 };
+
+// Read-only scene tables through the constant address space (VPX_CONST_AS): a load at a
+// wave-uniform index becomes a scalar load through the scalar cache.  Through a generic
+// pointer the compiler cannot prove the table unclobbered by the kernel's own global stores,
+// so a uniform read was a vector load (L2 latency) into VGPRs.  Used where a wave walks a
+// chain of uniform loads (the instance TLAS and the candidates' records); applied everywhere
+// it moved the walkers' matrices into SGPRs and spilled them (round 4).  The tables are
+// written only by the host between renders.
+#define VPX_CONST_AS __attribute__((address_space(4)))
+
+// p[i] for a wave-uniform i: a scalar load (VPX_TLAS_SLOAD) or the plain vector load.
+template <class T>
+__device__ __forceinline__ T ldu(const T* p, uint32_t i) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (VPX_TLAS_SLOAD) {
+        static_assert(sizeof(T) % 4 == 0, "ldu: dword-sized records");
+        T v;
+        const VPX_CONST_AS uint32_t* src = (const VPX_CONST_AS uint32_t*)(p + i);
+        uint32_t* dst = reinterpret_cast<uint32_t*>(&v);
+#pragma unroll
+        for (uint32_t k = 0; k < sizeof(T) / 4u; ++k) dst[k] = src[k];
+        return v;
+    }
+#endif
+    return p[i];
+}
 
 struct f3 {
     float x, y, z;
@@ -769,7 +798,7 @@ __device__ __forceinline__ void for_volumes(const SceneView& sv, f3 o, f3 d, con
             any = sv.tlas_always;
             const f3 inv = mk(__fdiv_rn(1.0f, d.x), __fdiv_rn(1.0f, d.y), __fdiv_rn(1.0f, d.z));
             for (uint32_t n = 0; n < sv.tlas_nodes;) {
-                const TlasNode nd = sv.tlas[n];
+                const TlasNode nd = ldu(sv.tlas, n);
                 const bool h = live && tlas_box(nd, o, inv, bound);
                 const bool wave_h = __ballot(h) != 0;
                 if (nd.leaf) {
@@ -857,10 +886,10 @@ __device__ __forceinline__ bool find_nearest_rest(const SceneView& sv, Ray& r, C
     int32_t vox = *vox_io;
     const int32_t vox0 = vox;
     uint32_t hx = 0, hy = 0, hz = 0;
-    auto visit = [&](uint32_t i) {
-        if (misses_volume(sv.vbounds[i], r.O, r.D)) return true;  // Setup3DDDA would fail
-        const vpx_volume& vol = sv.volumes[i];
-        const DevGrid g = sv.grids[vol.grid_id];
+    auto visit = [&](uint32_t i) {  // i is wave-uniform (for_volumes / the linear loop)
+        if (misses_volume(ldu(sv.vbounds, i), r.O, r.D)) return true;
+        const vpx_volume vol = ldu(sv.volumes, i);
+        const DevGrid g = ldu(sv.grids, vol.grid_id);
         skip::Walk w;
         {
             ORay o;

@@ -22,6 +22,8 @@ namespace vpx {
 constexpr int kTileW = 16;
 constexpr int kTilePix = kTileW * kTileW;
 
+
+
 // flags word of a path (stored in D.w)
 constexpr uint32_t kActive = 1u;
 constexpr uint32_t kInside = 2u;
@@ -1234,6 +1236,7 @@ __global__ __launch_bounds__(kPoolWg) VPX_WPE(VPX_WPE_SPOOL) void k_shadow_pool(
 #ifndef VPX_INST_MASK
 #define VPX_INST_MASK 1
 #endif
+
 #ifndef VPX_INST_CULL
 #define VPX_INST_CULL 1
 #endif
@@ -1243,18 +1246,19 @@ __device__ __forceinline__ bool occluded_instances(const SceneView& sv, const fl
     for (uint32_t i = 1; i < nv; ++i)
         cand |= (misses_volume(vb[i], r.O, r.D) ? 0ull : 1ull) << (i - 1u);
     bool occ = false;
+
     // the volumes in increasing index order, wave-uniform (a walk needs one grid per wave); a
     // volume no lane of the wave can reach costs one ballot
     for (uint32_t i = 1; i < nv; ++i) {
         const bool want = !occ && ((cand >> (i - 1u)) & 1ull);
         if (!__ballot(want)) continue;
         if (!want) continue;
-        const vpx_volume& vol = sv.volumes[i];
+        const vpx_volume vol = ldu(sv.volumes, i);  // i is wave-uniform
         ORay o;
         o.O = xform_pos(r.O, vol.inv_matrix);
         o.D = xform_vec(r.D, vol.inv_matrix);
         o.rD = mk(__fdiv_rn(1.0f, o.D.x), __fdiv_rn(1.0f, o.D.y), __fdiv_rn(1.0f, o.D.z));
-        const DevGrid g = sv.grids[vol.grid_id];
+        const DevGrid g = ldu(sv.grids, vol.grid_id);
         Dda s;
         if (!dda_setup(vol, g.n, o, s)) continue;
         skip::Walk wk = to_walk(s);
@@ -1325,8 +1329,9 @@ __global__ __launch_bounds__(256) VPX_WPE(VPX_WPE_MULTI_SHADOW) void k_shadow_in
         r.O = mk(so.x, so.y, so.z);
         r.D = mk(sd.x, sd.y, sd.z);
         r.t = so.w;
-        const bool occ = (VPX_INST_MASK && sv.num_volumes <= kTlasMaxVolumes) ? occluded_instances(sv, vb, r, k)
-                                                                              : is_occluded(sv, r, k, 1u);
+        const bool occ = (VPX_INST_MASK && sv.num_volumes <= kTlasMaxVolumes)
+                             ? occluded_instances(sv, vb, r, k)
+                             : is_occluded(sv, r, k, 1u);
         if (occ) w.occb[slot] = 1u;
     }
     flush_counters(k, 0u, ctr, VPX_STAGE_SHADOW);
