@@ -513,33 +513,28 @@ __device__ __forceinline__ bool walk_wave(const skip::GridView& g, skip::Walk& w
                         mode = kMiss;
                     } else {
                         const int cls = skip::classify_dfp_o<MINC>(w, g, opar);
-                        if (cls == 0) {
-                            ++cells;
-                            mode = kHit;
-                        } else if (cls == 2) {
-                            mode = kSkip;
-                        } else {
+                        // the class's outcome by selects: 0 = the solid cell (visited, hit), 2 =
+                        // skip; 1 / 3 visit the cell and run on in the brick
+                        cells += cls != 2 ? 1u : 0u;
+                        mode = cls == 0 ? kHit : (cls == 2 ? kSkip : mode);
+                        if (cls & 1) {
                             const uint64_t solid = cls == 1 ? w.m1 : 0ull;
-                            ++cells;
 #pragma unroll
                             for (int r = 0; r < kRun; ++r) {
                                 const uint32_t ox = w.X, oy = w.Y, oz = w.Z;
-                                if (!skip::step1<kMin2>(w, g.n)) {
-                                    mode = kMiss;
-                                    break;
-                                }
-                                // left the brick: this step changed a coordinate above its low
-                                // two bits (or the run reached its cap): the next pass loads
-                                if (r + 1 == kRun || ((w.X ^ ox) | (w.Y ^ oy) | (w.Z ^ oz)) > 3u) break;
-                                if (!(w.t < bound)) {
-                                    mode = kMiss;
-                                    break;
-                                }
-                                ++cells;
-                                if ((solid >> ((w.X & 3u) | ((w.Y & 3u) << 2) | ((w.Z & 3u) << 4))) & 1ull) {
-                                    mode = kHit;
-                                    break;
-                                }
+                                // the same outcomes with one exit per cell (fewer exec-mask
+                                // merges): left the grid -> miss; left the brick (or the run's
+                                // cap) -> the next pass loads; bound reached -> miss; else the
+                                // cell is visited, a solid one ends the walk
+                                const bool ing = skip::step1<kMin2>(w, g.n);
+                                const bool inb = r + 1 < kRun && ((w.X ^ ox) | (w.Y ^ oy) | (w.Z ^ oz)) <= 3u;
+                                const bool inbound = w.t < bound;
+                                const bool sol =
+                                    (solid >> ((w.X & 3u) | ((w.Y & 3u) << 2) | ((w.Z & 3u) << 4))) & 1ull;
+                                const bool visit = ing && inb && inbound;
+                                cells += visit ? 1u : 0u;
+                                mode = !ing || (inb && !inbound) ? kMiss : (visit && sol ? kHit : mode);
+                                if (!visit || sol) break;
                             }
                         }
                     }
