@@ -105,15 +105,20 @@ def limiter(pmc, kernel_ms):
         return {"hbm_frac_measured": None, "valu_busy": None, "bound_by": "unknown: no PMC summary for this build"}
     hbm = pmc["hbm_bytes_per_launch"] / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
     vb = pmc.get("valu_busy")
+    wf, st = pmc.get("wait_frac"), pmc.get("issue_stall_frac")
+    fmt = lambda x: "%.2f" % x if x is not None else "n/a"
     if vb is not None and vb >= 0.6 and vb > hbm:
         why = "VALU issue (valu_busy %.2f; real HBM %.3f of peak)" % (vb, hbm)
     elif hbm >= 0.6:
         why = "HBM bandwidth (real HBM %.2f of peak)" % hbm
+    elif wf is not None and st is not None and st > wf:
+        why = ("instruction issue: ready waves not issued, dependency / arbitration stalls %s of wave "
+               "cycles vs %s parked on loads (valu_busy %s, real HBM %.3f of peak)" % (fmt(st), fmt(wf), fmt(vb), hbm))
     else:
-        why = ("load latency: dependent gather chains (real HBM %.3f of peak, valu_busy %s, waves parked %s of cycles)"
-               % (hbm, "%.2f" % vb if vb is not None else "n/a",
-                  "%.2f" % pmc["wait_frac"] if pmc.get("wait_frac") is not None else "n/a"))
-    return {"hbm_frac_measured": round(hbm, 4), "valu_busy": vb, "wait_frac": pmc.get("wait_frac"),
+        why = ("load latency: dependent gather chains (real HBM %.3f of peak, valu_busy %s, waves parked %s "
+               "of cycles, issue-stalled %s)" % (hbm, fmt(vb), fmt(wf), fmt(st)))
+    return {"hbm_frac_measured": round(hbm, 4), "valu_busy": vb, "wait_frac": wf, "issue_stall_frac": st,
+            "issuing_frac": pmc.get("issuing_frac"), "waves_per_simd": pmc.get("waves_per_simd"),
             "l2_hit_rate": pmc.get("l2_hit_rate"), "bound_by": why}
 
 

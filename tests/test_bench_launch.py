@@ -87,6 +87,10 @@ def test_limiter_paths():
     assert lat["bound_by"].startswith("load latency") and lat["valu_busy"] == 0.42
     bw = b.limiter({"hbm_bytes_per_launch": 7e9, "valu_busy": 0.3}, 1.0)
     assert bw["bound_by"].startswith("HBM")
+    # ready waves not issued more than parked -> issue-bound, reported with both fractions
+    iss = b.limiter({"hbm_bytes_per_launch": 1e8, "valu_busy": 0.46, "wait_frac": 0.34,
+                     "issue_stall_frac": 0.36, "issuing_frac": 0.31}, 1.0)
+    assert iss["bound_by"].startswith("instruction issue") and iss["issue_stall_frac"] == 0.36
 
 
 def _rank_summary_worker(rank, world, port, q):

@@ -3,10 +3,10 @@
 # GPU-suite tail, rank shares, PMC traffic and counters.  Runs here, not on the GPU box.
 set -eu
 cd "$(dirname "$0")/.."
-TAG=${TAG:-r03}
+TAG=${TAG:-r04}
 E=gpurun_out/ev
 if [ -f $E/gputests.log ]; then tail -3 $E/gputests.log > profiles/${TAG}_gputests_tail.txt; fi
-for c in C1 C2 C3 C4; do
+for c in C1 C2 C3 C4 Z1; do
   if [ -d $E/prof_$c ]; then
     cp "$(find $E/prof_$c -name run_kernel_stats.csv | head -1)" profiles/${TAG}_kernel_stats_$c.csv
     python tools/trace_busy.py "$(find $E/prof_$c -name run_kernel_trace.csv | head -1)" k_ composite blend \

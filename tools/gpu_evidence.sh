@@ -10,14 +10,14 @@
 set -u
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out/ev
 export TMPDIR=/tmp
-TAG=${TAG:-r03}
+TAG=${TAG:-r04}
 O=gpurun_out/ev
 step() { name=$1; shift; echo "== $name"; timeout -k 10 "$@" > $O/$name.log 2>&1; rc=$?; echo "$name rc=$rc"; grep -v amdgpu.ids $O/$name.log | tail -${TAILN:-2} | cut -c1-300; if [ $rc -ne 0 ]; then exit $rc; fi; }
 sha256sum raytracer-voxpopuli_amd/libvpx_hip.so | tee $O/lib.sha256
 if [ "${PART:-1}" = 1 ]; then
   step gputests 700 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread
   step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-  for c in ${CFGS:-C1 C2 C3 C4}; do
+  for c in ${CFGS:-C1 C2 C3 C4 Z1}; do
     steps=10; [ $c = C4 ] && steps=3
     step prof_$c 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/$O/prof_$c" -o run -- python bench.py --config $c --steps $steps --warmup 2 --no-cpu --no-extra
   done
@@ -25,8 +25,8 @@ if [ "${PART:-1}" = 1 ]; then
     step share_$c 300 env CFG=$c PIPE=3 python tools/rank_share.py
   done
 else
-  declare -A WH=([C1]="1920 1080" [C2]="1920 1080" [C3]="3840 2160" [C4]="3840 2160")
-  for c in ${PMC_CFGS:-C1 C2 C3 C4}; do
+  declare -A WH=([C1]="1920 1080" [C2]="1920 1080" [C3]="3840 2160" [C4]="3840 2160" [Z1]="1920 1080")
+  for c in ${PMC_CFGS:-C1 C2 C3 C4 Z1}; do
     TAG=ev/pmc_$c BENCH_ARGS="--config $c" bash tools/gpu_pmc.sh > $O/pmc_$c.log 2>&1 || { tail -5 $O/pmc_$c.log; exit 1; }
     python tools/pmc_traffic.py $O/pmc_$c profiles/${TAG}_pmc_traffic_$c.json $c ${WH[$c]} > /dev/null
     cp profiles/${TAG}_pmc_traffic_$c.json $O/

@@ -27,15 +27,25 @@ for k, d in vals.items():
     kernels[k] = {"fetch_kib": round(fetch, 1), "write_kib": round(write, 1), "launches_sampled": len(d["FETCH_SIZE"]),
                   "hbm_bytes_per_launch": round((2.0 * fetch + write) * 1024.0)}
     mean = lambda c: sum(d[c]) / len(d[c])
-    if "SQ_ACTIVE_INST_VALU" in d and "GRBM_GUI_ACTIVE" in d:
-        # VALU busy: SQ_ACTIVE_INST_VALU counts quad-cycles summed over the chip's 1024 SIMDs,
-        # GRBM_GUI_ACTIVE cycles summed over its 8 XCDs (MI355X_MICROARCH.md, cycle constants
-        # and DVFS rows): busy = VALU x 4 / 1024 / (GUI_ACTIVE / 8), per (serialised) dispatch
+    if "SQ_INSTS_VALU" in d and "GRBM_GUI_ACTIVE" in d:
+        # VALU busy: the fraction of the chip's 1024 SIMDs' cycles spent issuing VALU, at the
+        # 2 cycles a wave64 VALU instruction holds a SIMD (MI355X_MICROARCH.md, v_fma_f32 row);
+        # GRBM_GUI_ACTIVE is summed over the 8 XCDs (DVFS row) -> /8 = the dispatch's cycles.
+        # (SQ_ACTIVE_INST_VALU counts one per instruction on gfx950 -- measured 1.00-1.04 x
+        # SQ_INSTS_VALU -- so it is an instruction count, not quad-cycles: x4 overstated it 2x.)
         gui = mean("GRBM_GUI_ACTIVE") / 8.0
-        kernels[k]["valu_busy"] = round(mean("SQ_ACTIVE_INST_VALU") * 4.0 / 1024.0 / gui, 4) if gui > 0 else None
+        kernels[k]["valu_busy"] = round(mean("SQ_INSTS_VALU") * 2.0 / 1024.0 / gui, 4) if gui > 0 else None
         kernels[k]["gui_active_cycles"] = round(gui)
+        if "SQ_WAVE_CYCLES" in d and gui > 0:  # quad-cycles, summed over waves
+            kernels[k]["waves_per_simd"] = round(mean("SQ_WAVE_CYCLES") * 4.0 / 1024.0 / gui, 2)
     if "SQ_WAIT_ANY" in d and "SQ_WAVE_CYCLES" in d and mean("SQ_WAVE_CYCLES") > 0:
-        kernels[k]["wait_frac"] = round(mean("SQ_WAIT_ANY") / mean("SQ_WAVE_CYCLES"), 4)
+        # a wave's cycles split three ways (MI355X_MICROARCH.md, PMC slots): parked on
+        # s_waitcnt / barrier, ready but not issued (dependency or arbitration), issuing
+        wc = mean("SQ_WAVE_CYCLES")
+        kernels[k]["wait_frac"] = round(mean("SQ_WAIT_ANY") / wc, 4)
+        if "SQ_WAIT_INST_ANY" in d and "SQ_ACTIVE_INST_ANY" in d:
+            kernels[k]["issue_stall_frac"] = round(mean("SQ_WAIT_INST_ANY") / wc, 4)
+            kernels[k]["issuing_frac"] = round(mean("SQ_ACTIVE_INST_ANY") / wc, 4)
     if "TCC_HIT_sum" in d and "TCC_MISS_sum" in d:
         h, m = mean("TCC_HIT_sum"), mean("TCC_MISS_sum")
         kernels[k]["l2_hit_rate"] = round(h / (h + m), 4) if h + m > 0 else None
