@@ -35,6 +35,9 @@ constexpr int kTile = 16;  // 16x16 pixels per tile / 256-thread workgroup
 #ifndef VPX_LANE_TAIL
 #define VPX_LANE_TAIL 1  // frames in flight blend in their own tail launch where they have one (lane_tail_ok)
 #endif
+#ifndef VPX_LEVEL_FORK
+#define VPX_LEVEL_FORK 1  // launch_render: a level's bounce walks beside its shadow walks
+#endif
 constexpr int kThreads = 256;
 
 // One tile per workgroup.  Several tiles per workgroup with their loads issued together
@@ -477,6 +480,11 @@ struct vpx_ctx {
         void* d = nullptr;
         size_t bytes = 0;
         WaveBufs w{};
+        // the level fork (launch_render): a second stream for the bounce walks, forked after a
+        // level's shade and joined before the next one's, so that they overlap the shadow walks
+        hipStream_t fork = nullptr;
+        hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+        bool fork_dedicated = false;  // on a CU-mask stream, counted in g_lane_queues
     };
     WaveStore wave;
     // frames in flight (vpx_set_pipeline): each lane renders a whole frame on its own library
@@ -742,6 +750,35 @@ int ensure_wave(vpx_ctx* c, vpx_ctx::WaveStore& ws, uint32_t P, uint32_t L, uint
     return VPX_OK;
 }
 
+std::atomic<int> g_lane_queues{0};
+constexpr int kMaxLaneQueues = 16;
+
+// The level fork's stream and events (created on first use): a CU-mask stream of all the
+// device's CUs (a hardware queue of its own) while the process's lane-queue cap allows, else
+// a plain non-blocking stream.  Its work always joins back into the owner's stream within the
+// frame, so synchronising the owner covers it.
+int ensure_fork(vpx_ctx* c, vpx_ctx::WaveStore& ws) {
+    if (ws.fork) return VPX_OK;
+    std::vector<uint32_t> all_cus((c->cus + 31u) / 32u, 0xffffffffu);
+    ws.fork_dedicated = g_lane_queues.fetch_add(1) < kMaxLaneQueues;
+    if (!ws.fork_dedicated) g_lane_queues.fetch_sub(1);
+    const hipError_t se = ws.fork_dedicated
+                              ? hipExtStreamCreateWithCUMask(&ws.fork, (uint32_t)all_cus.size(), all_cus.data())
+                              : hipStreamCreateWithFlags(&ws.fork, hipStreamNonBlocking);
+    if (se != hipSuccess || hipEventCreateWithFlags(&ws.ev_fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&ws.ev_join, hipEventDisableTiming) != hipSuccess)
+        return fail(c, VPX_E_DEVICE, "level fork: stream / event creation failed");
+    return VPX_OK;
+}
+void free_fork(vpx_ctx::WaveStore& ws) {
+    if (ws.fork) (void)hipStreamSynchronize(ws.fork);
+    if (ws.ev_fork) (void)hipEventDestroy(ws.ev_fork);
+    if (ws.ev_join) (void)hipEventDestroy(ws.ev_join);
+    if (ws.fork) (void)hipStreamDestroy(ws.fork);
+    if (ws.fork_dedicated) g_lane_queues.fetch_sub(1);
+    ws.fork = nullptr, ws.ev_fork = ws.ev_join = nullptr, ws.fork_dedicated = false;
+}
+
 // Profile marks: a stage's start (stage >= 0) or end (-1) event on the stream, while the
 // event pool lasts; a start without room for its end is not recorded.
 static void prof_mark(vpx_ctx* c, hipStream_t s, int stage) {
@@ -833,6 +870,23 @@ int launch_render(vpx_ctx* c, hipStream_t s, vpx_ctx::WaveStore& ws, const Scene
         hipLaunchKernelGGL(k_instances, grid, block, 0, s, sv, f, w, c->d_ctr);
         prof_mark(c, s, -1);
     }
+    // FindNearest for the traced rays of the next level: the bounce pool (single volume, no
+    // shapes) or the tile kernel
+    auto bounce = [&](hipStream_t bs, int level) {
+        prof_mark(c, bs, VPX_STAGE_BOUNCE);
+        if (one) {  // the bounce pool: persistent waves, as many as the device keeps resident
+            const uint32_t grabs = (P / 64u + kPoolGrab - 1u) / kPoolGrab;
+            const uint32_t waves = std::min(grabs, c->cus * 4u * (uint32_t)VPX_WPE_BOUNCE);
+            const uint32_t wpb = kPoolWg / 64u;
+            hipLaunchKernelGGL(k_nearest_pool, dim3((waves + wpb - 1u) / wpb), dim3(kPoolWg), 0, bs, sv, w, level,
+                               c->d_ctr);
+        } else {
+            hipLaunchKernelGGL(k_nearest_tile, grid, block, 0, bs, sv, w, c->d_ctr);
+        }
+        prof_mark(c, bs, -1);
+    };
+    const bool fork = VPX_LEVEL_FORK && f.max_bounces > 0 && !rp;
+    if (fork && (rc = ensure_fork(c, ws))) return rc;
     // the last level's shadow -> resolve -> finish as one launch (k_shadow_finish)
     for (int level = 0; level <= f.max_bounces; ++level) {
         if (!(fuse_head && level == 0)) {
@@ -856,6 +910,16 @@ int launch_render(vpx_ctx* c, hipStream_t s, vpx_ctx::WaveStore& ws, const Scene
             }
             break;
         }
+        // the level fork: the next level's bounce walks read only the rays and trace mask
+        // this level's shade wrote and write only the hit records, which the shadow walks and
+        // the light sums do not touch — so they run beside them on the fork stream
+        const bool forked = fork && level < f.max_bounces;
+        if (forked) {
+            VPX_HIP(c, hipEventRecord(ws.ev_fork, s));
+            VPX_HIP(c, hipStreamWaitEvent(ws.fork, ws.ev_fork, 0));
+            bounce(ws.fork, level);
+            VPX_HIP(c, hipEventRecord(ws.ev_join, ws.fork));
+        }
         prof_mark(c, s, VPX_STAGE_SHADOW);
         if (spool)
             shadow_pool(level);
@@ -865,19 +929,10 @@ int launch_render(vpx_ctx* c, hipStream_t s, vpx_ctx::WaveStore& ws, const Scene
         prof_mark(c, s, VPX_STAGE_RESOLVE);
         hipLaunchKernelGGL(k_resolve, grid, block, 0, s, sv, w);
         prof_mark(c, s, -1);
-        if (level < f.max_bounces) {
-            prof_mark(c, s, VPX_STAGE_BOUNCE);
-            if (one) {  // the bounce pool: persistent waves, as many as the device keeps resident
-                const uint32_t grabs = (P / 64u + kPoolGrab - 1u) / kPoolGrab;
-                const uint32_t waves = std::min(grabs, c->cus * 4u * (uint32_t)VPX_WPE_BOUNCE);
-                const uint32_t wpb = kPoolWg / 64u;
-                hipLaunchKernelGGL(k_nearest_pool, dim3((waves + wpb - 1u) / wpb), dim3(kPoolWg), 0, s, sv, w, level,
-                                   c->d_ctr);
-            } else {
-                hipLaunchKernelGGL(k_nearest_tile, grid, block, 0, s, sv, w, c->d_ctr);
-            }
-            prof_mark(c, s, -1);
-        }
+        if (forked)
+            VPX_HIP(c, hipStreamWaitEvent(s, ws.ev_join, 0));
+        else if (level < f.max_bounces)
+            bounce(s, level);
     }
     // (fused tail: k_shadow_finish already finished the frame; max_bounces = -1 runs no
     // level, so the finish folds the zero leaf here)
@@ -938,15 +993,15 @@ int lane_render(vpx_ctx* c, const SceneView& sv, const FrameArgs& f, uint32_t ti
 }
 
 // Lanes on dedicated hardware queues across the process (every context, every device-set
-// member): each takes a queue of its own, so the count is capped (kMaxLaneQueues); lanes past
-// the cap are plain non-blocking streams from the shared pool.
-std::atomic<int> g_lane_queues{0};
-constexpr int kMaxLaneQueues = 16;
+// member; level forks too): each takes a queue of its own, so the count is capped
+// (kMaxLaneQueues, g_lane_queues above); lanes past the cap are plain non-blocking streams
+// from the shared pool.
 
 void free_lanes(vpx_ctx* c) {
     for (auto& L : c->lanes) {
         if (L.dedicated) g_lane_queues.fetch_sub(1);
         if (L.s) (void)hipStreamSynchronize(L.s);
+        free_fork(L.ws);
         if (L.ws.d) (void)hipFree(L.ws.d);
         if (L.packed) (void)hipFree(L.packed);
         if (L.rendered) (void)hipEventDestroy(L.rendered);
@@ -1043,6 +1098,7 @@ int vpx_destroy(vpx_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)sync_all(c);
     free_lanes(c);
+    free_fork(c->wave);
     for (auto& g : c->grids) {
         if (g.ptr) (void)hipFree(g.ptr);
         if (g.l1) (void)hipFree(g.l1);
