@@ -885,7 +885,11 @@ int launch_render(vpx_ctx* c, hipStream_t s, vpx_ctx::WaveStore& ws, const Scene
         }
         prof_mark(c, bs, -1);
     };
-    const bool fork = VPX_LEVEL_FORK && f.max_bounces > 0 && !rp;
+    // Frames rendered on the context's stream only: with frames in flight the lanes already
+    // overlap one frame's levels with the next frame's, and a fork stream per lane measured
+    // slower there (C2 3.37 vs 2.79-2.80 ms per step, Z1 3.48-3.52 vs 2.55-2.57), while a
+    // frame on its own gains (serial C2 3.70-3.74 vs 4.49-4.54 ms, Z1 3.44-3.47 vs 3.89-3.90).
+    const bool fork = VPX_LEVEL_FORK && f.max_bounces > 0 && !rp && &ws == &c->wave;
     if (fork && (rc = ensure_fork(c, ws))) return rc;
     // the last level's shadow -> resolve -> finish as one launch (k_shadow_finish)
     for (int level = 0; level <= f.max_bounces; ++level) {

@@ -258,16 +258,11 @@ struct Walk {
     int32_t sx, sy, sz;
     uint32_t osh;  // 8 x the ray's octant: the shift of its byte in a distance-field word
     uint64_t m1, m2;  // the level words of the current cell's brick / macro (set by classify)
-    // box continuation: bit 31 set while the walk is still inside the empty box of its last
-    // skip (a skip clipped at a binade crossing), bits 0..29 that box's anchor brick
-    // (x | y << 10 | z << 20; m1 still holds its cube) — see skip_on
-    uint32_t anc;
 };
 
 // Reset the level words and set the octant (after X..sz are set).
 VPX_HD void walk_begin(Walk& w) {
     w.m1 = w.m2 = 0ull;
-    w.anc = 0u;
     w.osh = ((w.sx < 0 ? 1u : 0u) | (w.sy < 0 ? 2u : 0u) | (w.sz < 0 ? 4u : 0u)) * 8u;
 }
 
@@ -389,41 +384,6 @@ VPX_HD void df_box(const Walk& w, uint32_t n, uint32_t k, uint32_t lo[3], uint32
         lo[k] = sg[k] > 0 ? c[k] : dn;
         hi[k] = sg[k] > 0 ? (up < n - 1u ? up : n - 1u) : c[k];
     }
-}
-
-// df_box for the cube anchored at brick `ab` (packed as Walk::anc) rather than at the
-// current cell's brick: the box of a skip the walk is still inside (its behind faces at the
-// current cell, as df_box puts them).
-VPX_HD void df_box_at(const Walk& w, uint32_t n, uint32_t k, uint32_t ab, uint32_t lo[3], uint32_t hi[3]) {
-    const uint32_t k4 = k * 4u;
-    const uint32_t c[3] = {w.X, w.Y, w.Z};
-    const uint32_t bb[3] = {(ab & 1023u) << 2, ((ab >> 10) & 1023u) << 2, ((ab >> 20) & 1023u) << 2};
-    const int32_t sg[3] = {w.sx, w.sy, w.sz};
-    for (int k = 0; k < 3; ++k) {
-        const uint32_t b = bb[k];
-        const uint32_t up = b + k4 - 1u, dn = b + 4u > k4 ? b + 4u - k4 : 0u;
-        lo[k] = sg[k] > 0 ? c[k] : dn;
-        hi[k] = sg[k] > 0 ? (up < n - 1u ? up : n - 1u) : c[k];
-    }
-}
-// The anchor word of the current cell's brick.
-VPX_HD uint32_t brick_anchor(const Walk& w) { return (w.X >> 2) | ((w.Y >> 2) << 10) | ((w.Z >> 2) << 20); }
-// Whether the current cell is still inside the box of cube k anchored at brick ab (packed as
-// Walk::anc): short of its far faces along the ray — the step after a skip that was clipped
-// at a binade crossing stays inside, one after a full crossing leaves it.  (The faces are
-// formed again rather than kept live through the skip.)
-VPX_HD bool in_box_at(const Walk& w, uint32_t n, uint32_t k, uint32_t ab) {
-    const uint32_t k4 = k * 4u;
-    const uint32_t c[3] = {w.X, w.Y, w.Z};
-    const uint32_t bb[3] = {(ab & 1023u) << 2, ((ab >> 10) & 1023u) << 2, ((ab >> 20) & 1023u) << 2};
-    const int32_t sg[3] = {w.sx, w.sy, w.sz};
-    bool in = true;
-    for (int k = 0; k < 3; ++k) {
-        const uint32_t b = bb[k];
-        const uint32_t up = b + k4 - 1u, dn = b + 4u > k4 ? b + 4u - k4 : 0u;
-        in &= sg[k] > 0 ? c[k] <= (up < n - 1u ? up : n - 1u) : c[k] >= dn;
-    }
-    return in;
 }
 
 // The chosen axis' cell and head advance (shared by both forms of step1).
@@ -782,23 +742,15 @@ VPX_HD int skip_box_lean(Walk& w, uint32_t lo[3], uint32_t hi[3], float bound, u
 VPX_HD bool walk_skip(const GridView& g, Walk& w, float bound, uint32_t& cells) {
     for (;;) {
         if (!(w.t < bound)) return false;
-        const bool cont = (w.anc >> 31) != 0u;  // still inside the last skip's box: no lookup
-        const int cls = cont ? 2 : classify(w, g);
+        const int cls = classify(w, g);
         if (cls == 0) {
             ++cells;
             return true;
         }
         if (cls == 2) {
-            w.anc = cont ? w.anc & 0x3fffffffu : brick_anchor(w);
             uint32_t lo[3], hi[3];
-            df_box_at(w, g.n, cube_l1(w), w.anc, lo, hi);
-            const int sr = skip_box_lean(w, lo, hi, bound, cells);
-            if (sr == 1) return false;
-            ++cells;  // visit the landing cell (or, refused, the current one), then step
-            const bool ing = step1(w, g.n);
-            w.anc = ing && sr == 0 && in_box_at(w, g.n, cube_l1(w), w.anc) ? w.anc | 0x80000000u : 0u;
-            if (!ing) return false;
-            continue;
+            df_box(w, g.n, cube_l1(w), lo, hi);
+            if (skip_box_lean(w, lo, hi, bound, cells) == 1) return false;
         }
         ++cells;  // visit the (empty) current cell
         if (!step1(w, g.n)) return false;

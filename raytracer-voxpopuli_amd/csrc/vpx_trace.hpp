@@ -453,9 +453,6 @@ constexpr uint32_t kRunShadowPool = VPX_RUN_SHADOW_POOL, kSkipwShadowPool = VPX_
                    kMincShadowPool = VPX_MINC_SHADOW_POOL;
 constexpr uint32_t kRunBouncePool = VPX_RUN_BOUNCE_POOL, kSkipwBouncePool = VPX_SKIPW_BOUNCE_POOL,
                    kMincBouncePool = VPX_MINC_BOUNCE_POOL;
-#ifndef VPX_SKIP_CONT
-#define VPX_SKIP_CONT 1  // walk_wave: skip on through the rest of a box after a clipped skip
-#endif
 #ifdef VPX_ASM_MARKS  // analysis builds only: label the walk phases in the ISA listing
 #define VPX_MARK(s) asm volatile("; MARK " s)
 #else
@@ -554,17 +551,8 @@ __device__ __forceinline__ bool walk_wave(const skip::GridView& g, skip::Walk& w
         VPX_PH(++nk; lk += __popcll(skipping);)
         VPX_MARK("skip phase");
         if (mode == kSkip) {
-#if VPX_SKIP_CONT
-            // a walk still inside its last skip's box (that skip was clipped at a binade
-            // crossing) skips on through the rest of it: the box is known empty, so its brick
-            // is not looked up again (skip::walk_skip has the same sequence)
-            w.anc = (w.anc >> 31) ? w.anc & 0x3fffffffu : skip::brick_anchor(w);
-            uint32_t lo[3], hi[3];
-            skip::df_box_at(w, g.n, skip::cube_dfp(w), w.anc, lo, hi);
-#else
             uint32_t lo[3], hi[3];
             skip::df_box(w, g.n, skip::cube_dfp(w), lo, hi);
-#endif
             const int sr = skip::skip_box_lean<kSeg2Branch>(w, lo, hi, bound, cells);  // 2 (refused): a plain step
             VPX_MARK("skip end");
             VPX_PH(fb += __popcll(__ballot(sr == 2));)
@@ -572,14 +560,7 @@ __device__ __forceinline__ bool walk_wave(const skip::GridView& g, skip::Walk& w
                 mode = kMiss;
             } else {
                 ++cells;  // visit the landing cell, then take the leaving event
-                const bool ing = skip::step1<kMin2>(w, g.n);
-#if VPX_SKIP_CONT
-                const bool on = ing && sr == 0 && w.t < bound && skip::in_box_at(w, g.n, skip::cube_dfp(w), w.anc);
-                w.anc = on ? w.anc | 0x80000000u : 0u;
-                mode = !ing ? kMiss : (on ? kSkip : kStep);
-#else
-                mode = ing ? kStep : kMiss;
-#endif
+                mode = skip::step1<kMin2>(w, g.n) ? kStep : kMiss;
             }
         }
         VPX_PH(ck += __builtin_amdgcn_s_memtime() - t1;)

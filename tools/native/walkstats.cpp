@@ -53,10 +53,6 @@ extern "C" void build_slabs(const uint8_t* bocc, uint32_t nb) {  // bocc[z][y][x
         }
 }
 static uint64_t g_slabskips;
-static uint64_t g_classify, g_contskips;  // brick lookups, and skips that continued a box without one
-extern "C" void cont_out(uint64_t* o) { o[0] = g_classify, o[1] = g_contskips; g_classify = g_contskips = 0; }
-static int g_cont = 1;
-extern "C" void set_cont(int c) { g_cont = c; }
 static uint64_t g_seg2[4];  // skips by the number of axes that need the second closed-form segment
 extern "C" void seg2_out(uint64_t* o) { for (int i = 0; i < 4; ++i) o[i] = g_seg2[i], g_seg2[i] = 0; }
 extern "C" uint64_t slab_out() { const uint64_t v = g_slabskips; g_slabskips = 0; return v; }
@@ -81,9 +77,7 @@ extern "C" void walk_sim(const uint8_t* cells, const uint64_t* l1, const uint64_
         bool hit = false;
         for (;;) {
             if (!(w.t < bound)) break;
-            const bool cont = g_cont && (w.anc >> 31);
-            int cls = cont ? 2 : (++g_classify, classify(w, g));
-            if (cont) ++g_contskips;
+            int cls = classify(w, g);
             if (cls == 0) { ++c; hit = true; break; }
             uint32_t slo[3], shi[3];
             bool slab = false;
@@ -133,8 +127,7 @@ extern "C" void walk_sim(const uint8_t* cells, const uint64_t* l1, const uint64_
             if (cls == 2) {
                 ++skips;
                 uint32_t lo[3], hi[3];
-                w.anc = cont ? w.anc & 0x3fffffffu : brick_anchor(w);
-                df_box_at(w, n, cube_l1(w), w.anc, lo, hi);
+                df_box(w, n, cube_l1(w), lo, hi);
                 if (slab) for (int q = 0; q < 3; ++q) lo[q] = slo[q], hi[q] = shi[q];
                 const uint32_t olo[3] = {lo[0], lo[1], lo[2]}, ohi[3] = {hi[0], hi[1], hi[2]};
                 {
@@ -168,12 +161,11 @@ extern "C" void walk_sim(const uint8_t* cells, const uint64_t* l1, const uint64_
                     }
                     g_cross[worst < 15 ? worst : 15]++;
                 }
-                if (sr == 2) { w.anc = 0; ++c; if (!step1(w, n)) break; continue; }
+                if (sr == 2) { ++c; if (!step1(w, n)) break; continue; }
                 w = t; c += cc;
                 if (sr == 1) break;
                 ++c;
                 if (!step1(w, n)) break;
-                w.anc = in_box_at(w, n, cube_l1(w), w.anc) ? w.anc | 0x80000000u : 0u;
                 continue;
             } else {
                 ++steps;

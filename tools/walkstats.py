@@ -89,8 +89,6 @@ lib.build_slabs(bocc.ctypes.data, nbk)
 lib.set_mode.argtypes = [C.c_int]
 lib.slab_out.restype = C.c_uint64
 modes = [int(x) for x in os.environ.get("MODES", "0").split()]
-lib.set_cont.argtypes = [C.c_int]
-lib.set_cont(int(os.environ.get("CONT", "1")))
 for name, (a, b, bnd), mode in [(nm_, v, md) for nm_, v in sets.items() for md in modes]:
     lib.set_mode(mode)
     R = len(a)
@@ -100,8 +98,6 @@ for name, (a, b, bnd), mode in [(nm_, v, md) for nm_, v in sets.items() for md i
           f"lean-clipped {o[6]/max(o[2],1):.4f} cost {(o[1] + 5.8 * o[2]) / R:.0f}")
     lib.small_out.restype = C.c_uint64
     print(f"   steps in empty bricks with a cube below the skip minimum: {lib.small_out() / R:.1f} per ray")
-    co = np.zeros(2, np.uint64); lib.cont_out.argtypes = [V]; lib.cont_out(co.ctypes.data)
-    print(f"   brick lookups {co[0] / R:.1f} per ray, box-continuing skips {co[1] / R:.1f} per ray")
     cr = np.zeros(16, np.uint64); lib.cross_out.argtypes = [V]; lib.cross_out(cr.ctypes.data)
     print("   clipped boxes by binade crossings of the full box (max over axes):", cr[:10])
     s2 = np.zeros(4, np.uint64); lib.seg2_out.argtypes = [V]; lib.seg2_out(s2.ctypes.data)
