@@ -880,7 +880,9 @@ int launch_render(vpx_ctx* c, hipStream_t s, vpx_ctx::WaveStore& ws, const Scene
             const uint32_t wpb = kPoolWg / 64u;
             hipLaunchKernelGGL(k_nearest_pool, dim3((waves + wpb - 1u) / wpb), dim3(kPoolWg), 0, bs, sv, w, level,
                                c->d_ctr);
-        } else {
+        } else {  // multi-volume / shape scenes (persistent waves without refills, k_nearest_mpool,
+                  // measured slower on Z1: 3.66-3.74 / 4.56-4.67 ms with grabs of 4 / 16 mask
+                  // words vs 2.50-2.54 — DESIGN.md §4)
             hipLaunchKernelGGL(k_nearest_tile, grid, block, 0, bs, sv, w, c->d_ctr);
         }
         prof_mark(c, bs, -1);
