@@ -59,8 +59,10 @@ EXTRA_CONFIGS = ("C2", "C3", "C4", "Z1")
 # from the A/B on one MI355X (ms per step, 2 / 3 / 4 lanes): C1 - / 0.551-0.554 /
 # 0.578-0.594, C4 52.6 / 52.4 / 51.6; with the pools (round 3) C2 2.76-2.77 / 2.50-2.52 /
 # 2.42-2.45 as the process's first config but 2.57-2.69 (3) vs 2.87-2.90 (4) as an extra
-# config after C1 (the line the driver runs), C3 3.70-3.71 / 3.65 / 3.67-3.71.
-PIPELINE = {"C1": 3, "C2": 3, "C3": 3, "C4": 4, "Z1": 3}
+# config after C1 (the line the driver runs), C3 3.70-3.71 / 3.65 / 3.67-3.71.  Round 4: C2's
+# single-volume levels fork their bounce walks beside the shadow walks when at most two lanes
+# run (vpx_kernels.hip launch_render): C2 2.50-2.52 at 2 lanes vs 2.65-2.67 at 3 without forks.
+PIPELINE = {"C1": 3, "C2": 2, "C3": 3, "C4": 4, "Z1": 3}
 STAGE_KERNELS = {"primary": "k_primary", "shade": "k_shade", "shadow": "k_shadow_tile", "resolve": "k_resolve",
                  "bounce": "k_nearest_tile", "finish": "k_finish", "frame": "k_frame0", "instances": "k_instances"}
 

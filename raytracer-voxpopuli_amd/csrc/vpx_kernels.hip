@@ -887,11 +887,14 @@ int launch_render(vpx_ctx* c, hipStream_t s, vpx_ctx::WaveStore& ws, const Scene
         }
         prof_mark(c, bs, -1);
     };
-    // Frames rendered on the context's stream only: with frames in flight the lanes already
-    // overlap one frame's levels with the next frame's, and a fork stream per lane measured
-    // slower there (C2 3.37 vs 2.79-2.80 ms per step, Z1 3.48-3.52 vs 2.55-2.57), while a
-    // frame on its own gains (serial C2 3.70-3.74 vs 4.49-4.54 ms, Z1 3.44-3.47 vs 3.89-3.90).
-    const bool fork = VPX_LEVEL_FORK && f.max_bounces > 0 && !rp && &ws == &c->wave;
+    // Where it pays (ms per step, one MI355X, tools/gpu_r4h/j/k.sh): every frame on the
+    // context's stream (serial C2 3.70-3.74 vs 4.49-4.54, Z1 3.44-3.47 vs 3.89-3.90), and
+    // single-volume frames in flight with at most two lanes (C2 at 2 lanes 2.50-2.52 vs 2.65-2.67
+    // at the 3 lanes without forks).  Not with three or more lanes (C2 3.17-3.28 at 3, 4.0-4.3 at
+    // 4: more dedicated queues than the device runs at once; forks from the shared queue pool
+    // 2.80-2.86), nor for multi-volume / shape frames in flight (Z1 3.20-3.25 at 2 lanes vs
+    // 2.50 at 3 without).
+    const bool fork = VPX_LEVEL_FORK && f.max_bounces > 0 && !rp && (&ws == &c->wave || (one && c->lanes.size() <= 2));
     if (fork && (rc = ensure_fork(c, ws))) return rc;
     // the last level's shadow -> resolve -> finish as one launch (k_shadow_finish)
     for (int level = 0; level <= f.max_bounces; ++level) {
