@@ -234,10 +234,7 @@ int vpx_synchronize(vpx_ctx* ctx);
    reference renders one frame per Tick (renderer.cpp:1646-1891).
    Queues and ordering: each lane takes a hardware queue of its own (D per context, and per
    member of a device set), up to 16 such lanes per process; lanes past that cap are plain
-   non-blocking streams from the process's shared queue pool.  A released lane's stream (on
-   vpx_set_pipeline or vpx_destroy) stays alive in a per-device pool of idle dedicated queues
-   that later lanes of any context in the process reuse first (the runtime keeps a destroyed
-   stream's queue mapped, so new ones would add to them).  Frames with bounce levels also
+   non-blocking streams from the process's shared queue pool.  Frames with bounce levels also
    take one more such queue per path state (the context's own, and each lane's when at most two
    lanes run a single-volume scene): the level fork, a second stream that runs a level's
    bounce walks beside its shadow walks and joins back within the frame.  Dedicated-queue lanes are

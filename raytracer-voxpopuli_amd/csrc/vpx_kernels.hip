@@ -19,9 +19,6 @@
 #include <cstring>
 #include <string>
 #include <array>
-#include <mutex>
-#include <utility>
-#include <vector>
 #include <atomic>
 #include <vector>
 
@@ -487,7 +484,7 @@ struct vpx_ctx {
         // level's shade and joined before the next one's, so that they overlap the shadow walks
         hipStream_t fork = nullptr;
         hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-        bool fork_dedicated = false;  // a dedicated queue (take_queue / give_queue)
+        bool fork_dedicated = false;  // on a CU-mask stream, counted in g_lane_queues
     };
     WaveStore wave;
     // frames in flight (vpx_set_pipeline): each lane renders a whole frame on its own library
@@ -502,7 +499,7 @@ struct vpx_ctx {
         hipEvent_t rendered = nullptr, consumed = nullptr;
         hipEvent_t caller = nullptr;  // the caller's stream at the frame's vpx_render (lane_tail_ok frames)
         bool used = false;
-        bool dedicated = false;  // on a dedicated hardware queue (take_queue / give_queue)
+        bool dedicated = false;  // on a CU-mask stream (its own hardware queue), counted in g_lane_queues
     };
     std::vector<Lane> lanes;
     uint32_t lane_next = 0;
@@ -756,74 +753,29 @@ int ensure_wave(vpx_ctx* c, vpx_ctx::WaveStore& ws, uint32_t P, uint32_t L, uint
 std::atomic<int> g_lane_queues{0};
 constexpr int kMaxLaneQueues = 16;
 
-// Dedicated hardware queues are a process resource: a stream with an explicit CU mask (every
-// CU) gets a queue of its own, and the runtime keeps a destroyed stream's queue mapped, so a
-// later context's lanes would add queues beyond the ones an earlier context left idle (C2's
-// lanes ran 2.70 ms per step after C1's context vs 2.50 as the process's first).  Idle
-// dedicated streams therefore go back to a per-device pool and the next lane or fork takes
-// one from there before creating another; at most kMaxLaneQueues are ever created, past that
-// lanes and forks are plain non-blocking streams from the process's shared queue pool.
-std::mutex g_queue_mu;
-std::vector<std::pair<int, hipStream_t>> g_idle_queues;  // (device, stream)
-hipError_t take_queue(int device, hipStream_t* s, bool* dedicated) {
-    {
-        std::lock_guard<std::mutex> lk(g_queue_mu);
-        for (size_t i = 0; i < g_idle_queues.size(); ++i)
-            if (g_idle_queues[i].first == device) {
-                *s = g_idle_queues[i].second;
-                g_idle_queues.erase(g_idle_queues.begin() + (long)i);
-                *dedicated = true;
-                return hipSuccess;
-            }
-    }
-    *dedicated = g_lane_queues.fetch_add(1) < kMaxLaneQueues;
-    if (!*dedicated) {
-        g_lane_queues.fetch_sub(1);
-        return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
-    }
-    int n_cu = 0;
-    hipError_t e = hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device);
-    if (e != hipSuccess) {
-        g_lane_queues.fetch_sub(1);
-        *dedicated = false;
-        return e;
-    }
-    std::vector<uint32_t> all_cus(((uint32_t)n_cu + 31u) / 32u, 0xffffffffu);
-    // CU-mask streams are blocking streams (no flags argument): they synchronise with the
-    // legacy null stream like any default-flag stream (documented in vpx.h)
-    e = hipExtStreamCreateWithCUMask(s, (uint32_t)all_cus.size(), all_cus.data());
-    if (e != hipSuccess) {
-        g_lane_queues.fetch_sub(1);
-        *dedicated = false;
-    }
-    return e;
-}
-void give_queue(int device, hipStream_t s, bool dedicated) {
-    if (!s) return;
-    (void)hipStreamSynchronize(s);
-    if (!dedicated) {
-        (void)hipStreamDestroy(s);
-        return;
-    }
-    std::lock_guard<std::mutex> lk(g_queue_mu);
-    g_idle_queues.emplace_back(device, s);
-}
-
-// The level fork's stream and events (created on first use), from the dedicated-queue pool.
-// Its work always joins back into the owner's stream within the frame, so synchronising the
-// owner covers it.
+// The level fork's stream and events (created on first use): a CU-mask stream of all the
+// device's CUs (a hardware queue of its own) while the process's lane-queue cap allows, else
+// a plain non-blocking stream.  Its work always joins back into the owner's stream within the
+// frame, so synchronising the owner covers it.
 int ensure_fork(vpx_ctx* c, vpx_ctx::WaveStore& ws) {
     if (ws.fork) return VPX_OK;
-    const hipError_t se = take_queue(c->device, &ws.fork, &ws.fork_dedicated);
+    std::vector<uint32_t> all_cus((c->cus + 31u) / 32u, 0xffffffffu);
+    ws.fork_dedicated = g_lane_queues.fetch_add(1) < kMaxLaneQueues;
+    if (!ws.fork_dedicated) g_lane_queues.fetch_sub(1);
+    const hipError_t se = ws.fork_dedicated
+                              ? hipExtStreamCreateWithCUMask(&ws.fork, (uint32_t)all_cus.size(), all_cus.data())
+                              : hipStreamCreateWithFlags(&ws.fork, hipStreamNonBlocking);
     if (se != hipSuccess || hipEventCreateWithFlags(&ws.ev_fork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&ws.ev_join, hipEventDisableTiming) != hipSuccess)
         return fail(c, VPX_E_DEVICE, "level fork: stream / event creation failed");
     return VPX_OK;
 }
-void free_fork(int device, vpx_ctx::WaveStore& ws) {
-    give_queue(device, ws.fork, ws.fork_dedicated);
+void free_fork(vpx_ctx::WaveStore& ws) {
+    if (ws.fork) (void)hipStreamSynchronize(ws.fork);
     if (ws.ev_fork) (void)hipEventDestroy(ws.ev_fork);
     if (ws.ev_join) (void)hipEventDestroy(ws.ev_join);
+    if (ws.fork) (void)hipStreamDestroy(ws.fork);
+    if (ws.fork_dedicated) g_lane_queues.fetch_sub(1);
     ws.fork = nullptr, ws.ev_fork = ws.ev_join = nullptr, ws.fork_dedicated = false;
 }
 
@@ -1049,19 +1001,22 @@ int lane_render(vpx_ctx* c, const SceneView& sv, const FrameArgs& f, uint32_t ti
     return VPX_OK;
 }
 
-// A context's lanes: their streams go back to the process's dedicated-queue pool
-// (give_queue), their buffers and events are freed.
+// Lanes on dedicated hardware queues across the process (every context, every device-set
+// member; level forks too): each takes a queue of its own, so the count is capped
+// (kMaxLaneQueues, g_lane_queues above); lanes past the cap are plain non-blocking streams
+// from the shared pool.
 
 void free_lanes(vpx_ctx* c) {
     for (auto& L : c->lanes) {
+        if (L.dedicated) g_lane_queues.fetch_sub(1);
         if (L.s) (void)hipStreamSynchronize(L.s);
-        free_fork(c->device, L.ws);
+        free_fork(L.ws);
         if (L.ws.d) (void)hipFree(L.ws.d);
         if (L.packed) (void)hipFree(L.packed);
         if (L.rendered) (void)hipEventDestroy(L.rendered);
         if (L.consumed) (void)hipEventDestroy(L.consumed);
         if (L.caller) (void)hipEventDestroy(L.caller);
-        give_queue(c->device, L.s, L.dedicated);
+        if (L.s) (void)hipStreamDestroy(L.s);
     }
     c->lanes.clear();
     c->lane_next = 0;
@@ -1152,7 +1107,7 @@ int vpx_destroy(vpx_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)sync_all(c);
     free_lanes(c);
-    free_fork(c->device, c->wave);
+    free_fork(c->wave);
     for (auto& g : c->grids) {
         if (g.ptr) (void)hipFree(g.ptr);
         if (g.l1) (void)hipFree(g.l1);
@@ -1201,9 +1156,17 @@ int vpx_set_pipeline(vpx_ctx* c, uint32_t depth) {
     // stream with an explicit CU mask (here: every CU) gets a dedicated queue.  Measured on
     // one box (C1 ms, two processes x two contexts, 20 frames): 3 lanes 0.551-0.554 vs
     // 0.578-0.598 on pooled streams (4 pooled lanes 0.567-0.572, 4 dedicated 0.578-0.594).
-    // (take_queue: a dedicated queue from the process's pool, or a new CU-mask stream)
+    int n_cu = 0;
+    VPX_HIP(c, hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, c->device));
+    std::vector<uint32_t> all_cus(((uint32_t)n_cu + 31u) / 32u, 0xffffffffu);
+    // CU-mask streams are blocking streams (no flags argument): they synchronise with the
+    // legacy null stream like any default-flag stream (documented in vpx.h).
     for (auto& L : c->lanes) {
-        const hipError_t se = take_queue(c->device, &L.s, &L.dedicated);
+        L.dedicated = g_lane_queues.fetch_add(1) < kMaxLaneQueues;
+        if (!L.dedicated) g_lane_queues.fetch_sub(1);
+        const hipError_t se = L.dedicated
+                                  ? hipExtStreamCreateWithCUMask(&L.s, (uint32_t)all_cus.size(), all_cus.data())
+                                  : hipStreamCreateWithFlags(&L.s, hipStreamNonBlocking);
         if (se != hipSuccess ||
             hipEventCreateWithFlags(&L.rendered, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&L.consumed, hipEventDisableTiming) != hipSuccess ||

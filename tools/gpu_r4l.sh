@@ -1,4 +1,4 @@
-# Round 4: the level-fork policy build with the process-wide dedicated-queue pool (context stream,
+# Round 4: the level-fork policy build (context stream, or single-volume frames with <= 2
 # lanes; C2 at 2 lanes) — GPU suite, then two full bench lines (C1 + extras, as the driver runs).
 set -u
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out/r4l
