@@ -61,8 +61,10 @@ EXTRA_CONFIGS = ("C2", "C3", "C4", "Z1")
 # 2.42-2.45 as the process's first config but 2.57-2.69 (3) vs 2.87-2.90 (4) as an extra
 # config after C1 (the line the driver runs), C3 3.70-3.71 / 3.65 / 3.67-3.71.  Round 4: C2's
 # single-volume levels fork their bounce walks beside the shadow walks when at most two lanes
-# run (vpx_kernels.hip launch_render): C2 2.50-2.52 at 2 lanes vs 2.65-2.67 at 3 without forks.
-PIPELINE = {"C1": 3, "C2": 2, "C3": 3, "C4": 4, "Z1": 3}
+# run (vpx_kernels.hip launch_render): C2 2.50-2.52 at 2 lanes vs 2.65-2.67 at 3 without forks
+# as the first config (2.70 either way as an extra after C1).  Round-4 build (tools/gpu_r4m.sh,
+# 2 / 3 / 4 lanes): C1 0.553-0.557 / 0.555-0.556 / 0.586-0.587, C4 45.0-45.1 / 43.2-43.5 / 44.5-44.8.
+PIPELINE = {"C1": 3, "C2": 2, "C3": 3, "C4": 3, "Z1": 3}
 STAGE_KERNELS = {"primary": "k_primary", "shade": "k_shade", "shadow": "k_shadow_tile", "resolve": "k_resolve",
                  "bounce": "k_nearest_tile", "finish": "k_finish", "frame": "k_frame0", "instances": "k_instances"}
 
