@@ -619,8 +619,12 @@ __global__ __launch_bounds__(256) void k_resolve(SceneView sv, WaveBufs w) {
 #ifndef VPX_WPE_MULTI_NEAREST
 #define VPX_WPE_MULTI_NEAREST 4
 #endif
+// The multi-volume shadow kernels (k_shadow_inst, k_shadow_tile<false>, k_shadow_finish<false>)
+// at 6 (80 VGPRs, 15-18 spilled): C4 42.91 / 42.60 / 42.84 vs 43.18 / 42.94 / 44.99 ms at 5,
+// Z1 within noise (round 4, tools/gpu_r4n.sh); k_nearest_tile at 5 (49 spilled VGPRs): Z1
+// 2.66 vs 2.50-2.52.
 #ifndef VPX_WPE_MULTI_SHADOW
-#define VPX_WPE_MULTI_SHADOW 5
+#define VPX_WPE_MULTI_SHADOW 6
 #endif
 
 #define VPX_WPE(n) __attribute__((amdgpu_waves_per_eu(n)))
