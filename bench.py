@@ -96,10 +96,27 @@ def pmc_summary(kernel, config, W, H, sha):
             d = json.load(open(f))
         except (OSError, ValueError):
             continue
+        ks = d.get("kernels", {})
+        parts = kernel.split("+")  # a stage of two launches (e.g. k_shadow_pool+k_shadow_inst)
         if (d.get("config") == config and d.get("width") == W and d.get("height") == H
-                and d.get("lib_sha256") == sha and kernel in d.get("kernels", {})):
-            best, src = d["kernels"][kernel], os.path.relpath(f, REPO)
+                and d.get("lib_sha256") == sha and all(k in ks for k in parts)):
+            best, src = combine_pmc([ks[k] for k in parts]), os.path.relpath(f, REPO)
     return best, src
+
+
+def combine_pmc(ps):
+    """One stage's PMC summary from its launches' (each launched once per frame): bytes add,
+    the cycle fractions are averaged weighted by each launch's GRBM_GUI_ACTIVE cycles."""
+    if len(ps) == 1:
+        return ps[0]
+    out = {"hbm_bytes_per_launch": sum(p["hbm_bytes_per_launch"] for p in ps)}
+    wts = [p.get("gui_active_cycles") or 0 for p in ps]
+    for key in ("valu_busy", "wait_frac", "issue_stall_frac", "issuing_frac", "waves_per_simd", "l2_hit_rate"):
+        vals = [p.get(key) for p in ps]
+        if all(v is not None for v in vals) and sum(wts) > 0:
+            out[key] = round(sum(v * w for v, w in zip(vals, wts)) / sum(wts), 4)
+    out["gui_active_cycles"] = sum(wts)
+    return out
 
 
 def limiter(pmc, kernel_ms):

@@ -93,6 +93,17 @@ def test_limiter_paths():
     assert iss["bound_by"].startswith("instruction issue") and iss["issue_stall_frac"] == 0.36
 
 
+def test_combine_pmc_two_launch_stage():
+    b = _bench()
+    one = {"hbm_bytes_per_launch": 5.0, "valu_busy": 0.5}
+    assert b.combine_pmc([one]) is one
+    c = b.combine_pmc([{"hbm_bytes_per_launch": 100, "valu_busy": 0.2, "wait_frac": 0.6, "gui_active_cycles": 3},
+                       {"hbm_bytes_per_launch": 50, "valu_busy": 0.6, "wait_frac": 0.2, "gui_active_cycles": 1}])
+    assert c["hbm_bytes_per_launch"] == 150 and c["gui_active_cycles"] == 4
+    assert abs(c["valu_busy"] - 0.3) < 1e-9 and abs(c["wait_frac"] - 0.5) < 1e-9
+    assert "l2_hit_rate" not in c  # missing in a part -> left out
+
+
 def _rank_summary_worker(rank, world, port, q):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
