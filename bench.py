@@ -496,7 +496,10 @@ def main():
                       serial_frames=args.steps)
     extra, weak = {}, None
     if not args.no_extra:
-        xs = max(3, args.steps // 4)
+        # the extras time as many steps as the headline: with frames in flight the timed region
+        # includes one pipeline fill and drain, which 5 steps (the earlier K / 4) charged at
+        # ~0.2 ms per step to C2 (2.70 vs 2.50 ms per step at 10 steps, same build and box)
+        xs = max(3, args.steps)
         for cfg in EXTRA_CONFIGS:
             if cfg != args.config:
                 r = run_config(pkg, env, cfg, xs, min(args.warmup, 2), sha=sha, pipeline=args.pipeline,
