@@ -135,3 +135,20 @@ def test_lane_tail_frames_in_flight(pkg, orc, scene, lanes):
     a_o, r_o, t_o = oracle_frames(orc, pkg, desc, 4)
     assert np.array_equal(a_s, a_o) and np.array_equal(r_s, r_o)
     assert counts(t_s) == (t_o["primary_rays"], t_o["shadow_rays"], t_o["bounce_rays"], t_o["dda_cells"])
+
+
+@pytest.mark.parametrize("scene", ["roomGlass-d4-points", "monu3-d3-areas"])
+def test_level_fork_frames_bit_exact(pkg, orc, scene):
+    """The level fork (a level's bounce walks on a second stream beside its shadow walks,
+    joined before the next shade): frames on the context's stream (fork), 2 lanes (fork on
+    each lane, single-volume scenes) and 3 lanes (no fork) equal each other and the oracle,
+    with the tile shadow kernels (point lights) and the shadow pool (area lights)."""
+    desc = CASES[scene](pkg.scene)
+    desc.flags = pkg.abi.VPX_FLAG_AA
+    frames = 3
+    a_o, r_o, t_o = oracle_frames(orc, pkg, desc, frames)
+    for lanes in (0, 2, 3):
+        a_p, r_p, t_p = render(pkg, desc, frames, lanes=lanes)
+        assert np.array_equal(a_p, a_o), f"{lanes} lanes: accumulator differs from the oracle"
+        assert np.array_equal(r_p, r_o), f"{lanes} lanes: RGB8 differs"
+        assert counts(t_p) == (t_o["primary_rays"], t_o["shadow_rays"], t_o["bounce_rays"], t_o["dda_cells"])
