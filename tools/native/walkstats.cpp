@@ -25,6 +25,8 @@ extern "C" void cross_out(uint64_t* o) {
 static std::vector<uint8_t> g_slab;
 static uint32_t g_nb = 0;
 static int g_mode = 0;
+static int g_full = 0;
+extern "C" void set_full(int f) { g_full = f; }
 extern "C" void set_mode(int m) { g_mode = m; }
 extern "C" void build_slabs(const uint8_t* bocc, uint32_t nb) {  // bocc[z][y][x] != 0: occupied
     g_nb = nb;
@@ -144,7 +146,11 @@ extern "C" void walk_sim(const uint8_t* cells, const uint64_t* l1, const uint64_
                 }
                 Walk t = w;
                 uint32_t cc = 0;
-                const int sr = skip_box_lean(t, lo, hi, bound, cc);
+                // g_full: the exact multi-binade tier (skip_box: every box whole, any number of
+                // binade crossings) instead of the lean two-segment tier — what a lean tier with
+                // more segments could reach
+                int sr = g_full ? skip_box(t, lo, hi, bound, cc) : skip_box_lean(t, lo, hi, bound, cc);
+                if (g_full && sr == 2) sr = skip_box_lean(t, lo, hi, bound, cc);
                 bool clipped = false;
                 for (int k = 0; k < 3; ++k) clipped |= lo[k] != olo[k] || hi[k] != ohi[k];
                 if (sr == 2 || clipped) {

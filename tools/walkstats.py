@@ -89,6 +89,8 @@ lib.build_slabs(bocc.ctypes.data, nbk)
 lib.set_mode.argtypes = [C.c_int]
 lib.slab_out.restype = C.c_uint64
 modes = [int(x) for x in os.environ.get("MODES", "0").split()]
+lib.set_full.argtypes = [C.c_int]
+lib.set_full(int(os.environ.get("FULL", "0")))  # 1: whole boxes (the exact multi-binade tier)
 for name, (a, b, bnd), mode in [(nm_, v, md) for nm_, v in sets.items() for md in modes]:
     lib.set_mode(mode)
     R = len(a)
