@@ -193,9 +193,10 @@ class Env:
         return f"tile-shard x{self.n}, accumulator sharded, RCCL gather of RGB8 to rank 0 (overlapped)"
 
 
-def run_config(pkg, env, cfg, steps, warmup, weak=False, sha=None, pipeline=None, serial_frames=0):
+def run_config(pkg, env, cfg, steps, warmup, weak=False, sha=None, pipeline=None, serial_frames=0, arith=0):
     """Load `cfg` on this rank, run warmup + `steps` timed steps, return the result dict
-    (rank 0; None elsewhere).  Frees the world before returning."""
+    (rank 0; None elsewhere).  Frees the world before returning.  arith: vpx_set_arithmetic
+    mode (0 exact, the default; 1 the reference's x86 rcpps / rsqrtps from this host)."""
     desc = pkg.scene.CONFIGS[cfg]()
     if weak:  # N x the pixels at the same field of view (the base frame's camera)
         desc = desc.with_resolution(*weak_size(env.n, (desc.width, desc.height)))
@@ -203,6 +204,8 @@ def run_config(pkg, env, cfg, steps, warmup, weak=False, sha=None, pipeline=None
     ctx = pkg.context.Context(env.dev)
     ctx.set_stream(env.stream.cuda_stream)
     ctx.load_scene(desc)
+    if arith:
+        ctx.set_arithmetic(arith)
     if pipeline is None:
         pipeline = PIPELINE.get(cfg, 0)
     ctx.set_pipeline(pipeline)
@@ -356,8 +359,10 @@ def run_config(pkg, env, cfg, steps, warmup, weak=False, sha=None, pipeline=None
             torch.cuda.synchronize()
         if out is not None:
             out["serial_ms_per_frame"] = round((time.perf_counter() - t1) * 1000.0 / serial_frames, 4)
+            out["serial_ms_per_step"] = round(out["serial_ms_per_frame"] * spp, 4)
             out["serial_def"] = (f"{serial_frames} frames at --pipeline 0 with a host synchronize after each "
-                                 "(a per-frame-synchronous Tick); ms_per_step / launch_ms are the frames-in-flight figures")
+                                 f"(a per-frame-synchronous Tick); a step is {spp} frame(s), so serial_ms_per_step = "
+                                 "serial_ms_per_frame x spp compares with ms_per_step, the frames-in-flight figure")
     del acc, rgb, sharded
     ctx.close()
     torch.cuda.synchronize()
@@ -473,6 +478,9 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip extra_configs / weak_scaling")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--arith", choices=("exact", "x86"), default="exact",
+                    help="vpx_set_arithmetic of the headline config (x86: the reference's rcpps+NR / rsqrtps, "
+                         "this host's tables); the N=1 line also reports C1 in the x86 mode as reference_arithmetic")
     ap.add_argument("--pipeline", type=int, default=None,
                     help="frames in flight per GPU (vpx_set_pipeline lanes; 0 = serial frames); default: "
                          "per config, PIPELINE")
@@ -492,8 +500,19 @@ def main():
     pkg = entry.load_package()
     env = Env(args.gpus)
     sha = lib_sha256(pkg)
+    arith = 1 if args.arith == "x86" else 0
     head = run_config(pkg, env, args.config, args.steps, args.warmup, sha=sha, pipeline=args.pipeline,
-                      serial_frames=args.steps)
+                      serial_frames=args.steps, arith=arith)
+    ref_arith = None
+    if env.n == 1 and not args.no_extra and not arith and os.uname().machine == "x86_64":
+        # the same workload in the reference-arithmetic mode (VPX_ARITH_X86_HOST: FindNearest's
+        # FastReciprocal and the primary rsqrtps as this host computes them, bit-identical to the
+        # oracle's x86 mode, tests/test_x86_arith.py)
+        r = run_config(pkg, env, args.config, args.steps, args.warmup, sha=sha, pipeline=args.pipeline, arith=1)
+        if r is not None:
+            ref_arith = {"mode": "VPX_ARITH_X86_HOST", "ms_per_step": r["ms_per_step"], "value": r["value"],
+                         "exact_ms_per_step": head["ms_per_step"],
+                         "cost": round(r["ms_per_step"] / head["ms_per_step"] - 1.0, 4)}
     extra, weak = {}, None
     if not args.no_extra:
         # the extras time as many steps as the headline: with frames in flight the timed region
@@ -503,7 +522,7 @@ def main():
         for cfg in EXTRA_CONFIGS:
             if cfg != args.config:
                 r = run_config(pkg, env, cfg, xs, min(args.warmup, 2), sha=sha, pipeline=args.pipeline,
-                               serial_frames=xs)
+                               serial_frames=xs, arith=arith)
                 if r is not None:
                     extra[cfg] = r
         if env.n > 1:
@@ -519,7 +538,11 @@ def main():
                           "parallelism": env.parallelism(), "frames_in_flight": head["pipeline"], "lib_sha256": sha},
                "rays_per_step": head["rays_per_step"], "mpix_per_s": head["mpix_per_s"],
                "total_mray_s": head["total_mray_s"], "roofline": head["roofline"], "cpu_baseline": None}
-        for k in ("serial_ms_per_frame", "serial_def", "ranks"):
+        if ref_arith is not None:
+            out["reference_arithmetic"] = ref_arith
+        if arith:
+            out["config"]["arithmetic"] = "VPX_ARITH_X86_HOST"
+        for k in ("serial_ms_per_frame", "serial_ms_per_step", "serial_def", "ranks"):
             if k in head:
                 out[k] = head[k]
         if extra:

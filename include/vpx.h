@@ -287,6 +287,31 @@ int vpx_set_camera(vpx_ctx* ctx, const vpx_camera* camera);
 int vpx_set_sky(vpx_ctx* ctx, const float* rgb, uint32_t width, uint32_t height,
                 float hdr_contribution);
 
+/* ---- arithmetic mode ----------------------------------------------------------------
+   VPX_ARITH_EXACT (the default): exact 1/x and 1/sqrtf where the reference uses x86
+   approximations.  VPX_ARITH_X86_HOST: the reference's own arithmetic,
+   bit for bit as THIS host's CPU computes it — FastReciprocal (rcpps + one Newton step,
+   renderer.cpp:929-934) for every Renderer::FindNearest volume visit (:969), and
+   normalize(__m128) = v * rsqrtps(dpps(v, v, 0x7F)) (template/tmpl8math.h:2356-2360) for the
+   primary directions of Renderer::Update (:1735-1765).  rcpps / rsqrtps differ between CPU
+   vendors, so the call captures the host's tables (vpx_x86_arith_tables) and uploads them;
+   VPX_E_STATE when the host is not x86 or its instructions do not follow the table model.
+   The static-camera path's primary rays (GetPrimaryRayNoDOF, the Ray constructor) stay exact,
+   as in the reference. */
+#define VPX_ARITH_EXACT 0u
+#define VPX_ARITH_X86_HOST 1u
+int vpx_set_arithmetic(vpx_ctx* ctx, uint32_t mode);
+/* Host only (no device): capture this CPU's rcpss / rsqrtss tables under FTZ | DAZ and
+   spot-check the model (vpx_x86.hpp) against the instructions.  info = {rcp key shift, rsqrt
+   key shift, first rsqrt entry, entries}; out (may be NULL: sizes only) receives the entries
+   (cap >= info[3]).  VPX_E_STATE: not x86, or the spot check failed. */
+int vpx_x86_arith_tables(uint32_t* out, uint64_t cap, uint32_t info[4]);
+/* Host only: the model against this CPU's rcpss and rsqrtss for every input bit pattern in
+   [lo, hi] (0, 0xffffffff = all 2^32) on `threads` threads; mismatches[0] / [1] count rcp /
+   rsqrt disagreements, first_bad[] the first input of each. */
+int vpx_x86_arith_verify(uint32_t lo, uint32_t hi, uint32_t threads, uint64_t mismatches[2],
+                         uint32_t first_bad[2]);
+
 /* ---- display interop ---------------------------------------------
    Replaces the per-frame host upload of Surface::pixels in GLTexture::CopyFrom
    (template/opengl.cpp:144-149, called from template/template.cpp:305).  The host creates a

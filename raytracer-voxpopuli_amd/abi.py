@@ -17,6 +17,7 @@ VPX_E_INVALID, VPX_E_DEVICE, VPX_E_NOMEM, VPX_E_STATE = -1, -2, -3, -4  # includ
 VPX_FLAG_AA = 0x1
 VPX_FLAG_DOF = 0x2
 VPX_FLAG_NO_TONEMAP = 0x4
+VPX_ARITH_EXACT, VPX_ARITH_X86_HOST = 0, 1  # vpx_set_arithmetic modes
 VPX_FLAG_SKY = 0x8  # activateSky: misses sample the vpx_set_sky texture (renderer.cpp:2308-2326)
 MAT_NONE = 255
 SKY_DEFAULT = (0.392, 0.584, 0.829)  # SampleSky with activateSky == false, renderer.cpp:2310-2313
@@ -190,6 +191,10 @@ SIGNATURES = {
                                      C.POINTER(C.c_uint32)]),
     "vpx_bvh_random_tris": (C.c_int, [C.POINTER(C.c_uint32), C.POINTER(BvhTri)]),
     "vpx_bvh_depth": (C.c_uint32, [C.POINTER(BvhNode), C.c_uint32]),
+    "vpx_set_arithmetic": (C.c_int, [C.c_void_p, C.c_uint32]),
+    "vpx_x86_arith_tables": (C.c_int, [C.c_void_p, C.c_uint64, C.POINTER(C.c_uint32)]),
+    "vpx_x86_arith_verify": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint64),
+                                       C.POINTER(C.c_uint32)]),
     "vpx_vox_decode": (C.c_int, [C.c_void_p, C.c_uint64, C.POINTER(C.c_uint32), C.c_void_p, C.c_uint64, C.c_void_p]),
 }
 

@@ -60,6 +60,11 @@ class Context:
         """Frames in flight (vpx_set_pipeline): 0 / 1 off, 2..4 lanes."""
         self._chk(self.lib.vpx_set_pipeline(self.h, int(depth)), "vpx_set_pipeline")
 
+    def set_arithmetic(self, mode):
+        """vpx_set_arithmetic: abi.VPX_ARITH_EXACT (default) or abi.VPX_ARITH_X86_HOST (the
+        reference's rcpps+NR / rsqrtps as this host's CPU computes them)."""
+        self._chk(self.lib.vpx_set_arithmetic(self.h, int(mode)), "vpx_set_arithmetic")
+
     # ------------------------------------------------------------------- scene
     def load_scene(self, desc, upload_grids=True):
         if upload_grids:

@@ -464,6 +464,9 @@ struct vpx_ctx {
     float* d_sky = nullptr;
     uint32_t sky_w = 0, sky_h = 0;
     float sky_hdr = 1.0f;
+    // reference arithmetic (vpx_set_arithmetic): the host's captured rcpss / rsqrtss tables
+    uint32_t* d_x86 = nullptr;
+    X86Arith x86{nullptr, 0u, 0u, 0u, 0u};
     unsigned long long* d_ctr = nullptr;  // striped work counters (vpx_wavefront.hpp flush_counters)
     // per-stage profile: event pairs around stage launches while enabled
     std::vector<hipEvent_t> prof_ev;
@@ -664,6 +667,7 @@ SceneView view_of(const vpx_ctx* c, const float sky[3], int32_t area_samples, bo
     sv.sky_w = c->sky_w, sv.sky_h = c->sky_h;
     sv.sky_hdr = c->sky_hdr;
     sv.sky_tex = (sky_tex && c->d_sky) ? 1u : 0u;
+    sv.x86 = c->x86;
     return sv;
 }
 
@@ -1115,7 +1119,7 @@ int vpx_destroy(vpx_ctx* c) {
         if (g.dfp) (void)hipFree(g.dfp);
     }
     void* ptrs[] = {c->d_grids, c->d_volumes, c->d_vbounds, c->d_tlas, c->d_bvh, c->d_materials, c->d_points, c->d_spots, c->d_areas,
-                    c->d_spheres, c->d_triangles, c->d_ctr, c->d_sum, c->d_scratch, c->wave.d, c->d_sky};
+                    c->d_spheres, c->d_triangles, c->d_ctr, c->d_sum, c->d_scratch, c->wave.d, c->d_sky, c->d_x86};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (hipEvent_t e : c->prof_ev) (void)hipEventDestroy(e);
@@ -1637,6 +1641,27 @@ int vpx_set_sky(vpx_ctx* c, const float* rgb, uint32_t width, uint32_t height, f
     VPX_HIP(c, sync_all(c));
     c->sky_w = width, c->sky_h = height;
     c->sky_hdr = hdr_contribution;
+    return VPX_OK;
+}
+
+int vpx_set_arithmetic(vpx_ctx* c, uint32_t mode) {
+    VPX_GROUP_ALL(c, vpx_set_arithmetic(m_, mode));
+    if (!c) return VPX_E_INVALID;
+    if (mode != VPX_ARITH_EXACT && mode != VPX_ARITH_X86_HOST) return fail(c, VPX_E_INVALID, "unknown arithmetic mode");
+    VPX_HIP(c, hipSetDevice(c->device));
+    VPX_HIP(c, sync_all(c));  // frames in flight read the tables
+    if (c->d_x86) (void)hipFree(c->d_x86);
+    c->d_x86 = nullptr;
+    c->x86 = X86Arith{nullptr, 0u, 0u, 0u, 0u};
+    if (mode == VPX_ARITH_EXACT) return VPX_OK;
+    uint32_t info[4];
+    if (vpx_x86_arith_tables(nullptr, 0, info) != VPX_OK)
+        return fail(c, VPX_E_STATE, "the host's rcpss / rsqrtss do not follow the table model (or the host is not x86)");
+    std::vector<uint32_t> tab(info[3]);
+    if (vpx_x86_arith_tables(tab.data(), tab.size(), info) != VPX_OK) return fail(c, VPX_E_STATE, "table capture failed");
+    VPX_HIP(c, hipMalloc(&c->d_x86, sizeof(uint32_t) * tab.size()));
+    VPX_HIP(c, hipMemcpy(c->d_x86, tab.data(), sizeof(uint32_t) * tab.size(), hipMemcpyHostToDevice));
+    c->x86 = X86Arith{c->d_x86, info[0], info[1], info[2], 0u};
     return VPX_OK;
 }
 

@@ -20,6 +20,7 @@
 
 #include "../../include/vpx.h"
 #include "vpx_skip.hpp"
+#include "vpx_x86.hpp"
 
 namespace vpx {
 
@@ -88,6 +89,9 @@ struct SceneView {
     uint32_t sky_w, sky_h;
     float sky_hdr;
     uint32_t sky_tex;
+    // reference arithmetic (vpx_set_arithmetic): the host's rcpss / rsqrtss tables, or a null
+    // tab for the exact 1/x and 1/sqrtf of the default mode
+    X86Arith x86;
 };
 
 // Read-only scene tables through the constant address space (VPX_CONST_AS): a load at a
@@ -300,6 +304,20 @@ __device__ __forceinline__ f3 ray_point(const Ray& r) { return r.O + r.D * r.t; 
 struct ORay {
     f3 O, D, rD;
 };
+
+// rD of a Renderer::FindNearest volume visit.  Default: exact 1/D.  Reference arithmetic
+// (xa.tab set, wave-uniform): FastReciprocal = rcpps + one Newton step, (r + r) - D * (r * r)
+// (renderer.cpp:929-934, :969), rcpps from the host's captured table (vpx_x86.hpp) — a zero
+// component gives inf * 0 = NaN there, as on the host.
+__device__ __forceinline__ float fast_reciprocal1(float x, const X86Arith& xa) {
+    const float r = __uint_as_float(x86_rcp_bits(__float_as_uint(x), xa.tab, xa.rcp_shift));
+    const float muls = x * (r * r);
+    return (r + r) - muls;
+}
+__device__ __forceinline__ f3 nearest_rd(f3 d, const X86Arith& xa) {
+    if (xa.tab) return mk(fast_reciprocal1(d.x, xa), fast_reciprocal1(d.y, xa), fast_reciprocal1(d.z, xa));
+    return mk(__fdiv_rn(1.0f, d.x), __fdiv_rn(1.0f, d.y), __fdiv_rn(1.0f, d.z));
+}
 
 // ------------------------------------------------------------------------ the DDA
 struct Dda {
@@ -827,7 +845,7 @@ __device__ __forceinline__ int32_t find_nearest(const SceneView& sv, Ray& r, Cou
             ORay o;
             o.O = xform_pos_ssem(r.O, vol.inv_matrix);
             o.D = xform_vec_ssem(r.D, vol.inv_matrix);
-            o.rD = mk(__fdiv_rn(1.0f, o.D.x), __fdiv_rn(1.0f, o.D.y), __fdiv_rn(1.0f, o.D.z));
+            o.rD = nearest_rd(o.D, sv.x86);
             Dda s;
             if (!dda_setup(vol, g.n, o, s)) return true;
             w = to_walk(s);
@@ -890,7 +908,7 @@ __device__ __forceinline__ bool find_nearest_rest(const SceneView& sv, Ray& r, C
             ORay o;
             o.O = xform_pos_ssem(r.O, vol.inv_matrix);
             o.D = xform_vec_ssem(r.D, vol.inv_matrix);
-            o.rD = mk(__fdiv_rn(1.0f, o.D.x), __fdiv_rn(1.0f, o.D.y), __fdiv_rn(1.0f, o.D.z));
+            o.rD = nearest_rd(o.D, sv.x86);
             Dda s;
             if (!dda_setup(vol, g.n, o, s)) return true;
             w = to_walk(s);

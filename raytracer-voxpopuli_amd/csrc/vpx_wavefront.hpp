@@ -107,7 +107,20 @@ struct WaveBufs {
 // ------------------------------------------------------------------ primary rays
 // Camera::GetPrimaryRayNoDOF (camera.h:103-110) / GetPrimaryRay + thin lens (:68-83);
 // AA jitter as the AVX path: fma(rand, aa, x) (renderer.cpp:1699-1708).
-__device__ __forceinline__ Ray primary_ray(const FrameArgs& f, uint32_t x, uint32_t y, Rng& g) {
+// Reference arithmetic (xa.tab set, not the static-camera path, whose GetPrimaryRayNoDOF goes
+// through the Ray constructor): the AVX loop's normalize(__m128) = v * rsqrtps(dpps(v, v,
+// 0x7F)) (tmpl8math.h:2356-2360, renderer.cpp:1735-1765), the dot product summed
+// (x*x + y*y) + z*z as dpps does, rsqrtps from the host's captured table (vpx_x86.hpp).
+__device__ __forceinline__ Ray primary_make_ray(f3 o, f3 dir, const X86Arith& xa, bool x86) {
+    if (!x86) return make_ray(o, dir);
+    Ray r = make_ray(o, dir);
+    const float dp = (dir.x * dir.x + dir.y * dir.y) + dir.z * dir.z;
+    const float inv = __uint_as_float(x86_rsq_bits(__float_as_uint(dp), xa.tab + xa.rsq_off, xa.rsq_shift));
+    r.D = dir * inv;
+    return r;
+}
+__device__ __forceinline__ Ray primary_ray(const FrameArgs& f, uint32_t x, uint32_t y, Rng& g, const X86Arith& xa) {
+    const bool x86 = xa.tab && !(f.flags & kFlagReproject);
     float fx = (float)x, fy = (float)y;
     if (f.flags & VPX_FLAG_AA) {
         const float rx = g.next(), ry = g.next();
@@ -129,9 +142,9 @@ __device__ __forceinline__ Ray primary_ray(const FrameArgs& f, uint32_t x, uint3
         const float jy = (cy * f.cam.defocus_jitter) / (float)f.width;
         const f3 focal = cp + normalize(P - cp) * f.cam.focal_distance;
         const f3 o = (cp + ld3(f.cam.right) * jx) + ld3(f.cam.up) * jy;
-        return make_ray(o, focal - o);
+        return primary_make_ray(o, focal - o, xa, x86);
     }
-    return make_ray(cp, P - cp);
+    return primary_make_ray(cp, P - cp, xa, x86);
 }
 
 // Lane -> pixel inside a 16x16 tile: the tile's four waves take its four 8x8 quadrants
@@ -667,12 +680,13 @@ __device__ __forceinline__ void nearest_record(SceneView sv, const PathRay& pr, 
 }
 
 // Object-space ray of path p in the single volume (FindNearest's SSE transforms).
-__device__ __forceinline__ ORay path_oray(const vpx_volume& vol, const PathRay& pr, uint32_t p) {
+__device__ __forceinline__ ORay path_oray(const vpx_volume& vol, const PathRay& pr, uint32_t p,
+                                          const X86Arith& xa = X86Arith{}) {
     const float4 o = pr.O[pr.at(p)], d = pr.D[pr.at(p)];
     ORay r;
     r.O = xform_pos_ssem(mk(o.x, o.y, o.z), vol.inv_matrix);
     r.D = xform_vec_ssem(mk(d.x, d.y, d.z), vol.inv_matrix);
-    r.rD = mk(__fdiv_rn(1.0f, r.D.x), __fdiv_rn(1.0f, r.D.y), __fdiv_rn(1.0f, r.D.z));
+    r.rD = nearest_rd(r.D, xa);
     return r;
 }
 
@@ -683,9 +697,9 @@ __device__ __forceinline__ ORay path_oray(const vpx_volume& vol, const PathRay& 
 // Its two halves (walk continuations, k_nearest_tile): the walk state of path p's ray
 // (false: Setup3DDDA fails, no cell is read) and the hit record from the finished walk.
 __device__ __forceinline__ bool nearest_begin_v(const vpx_volume& vol, uint32_t n, const PathRay& w, uint32_t p,
-                                                Counters& k, skip::Walk& wk) {
+                                                Counters& k, skip::Walk& wk, const X86Arith& xa) {
     ++k.nearest;
-    const ORay o = path_oray(vol, w, p);
+    const ORay o = path_oray(vol, w, p, xa);
     Dda s;
     if (!dda_setup(vol, n, o, s)) return false;
     wk = to_walk(s);
@@ -694,7 +708,7 @@ __device__ __forceinline__ bool nearest_begin_v(const vpx_volume& vol, uint32_t 
 __device__ __forceinline__ bool nearest_begin_1v(const SceneView& sv, const PathRay& w, uint32_t p, Counters& k,
                                                  skip::Walk& wk) {
     const vpx_volume* vol = uni_ptr(&sv.volumes[0]);
-    return nearest_begin_v(*vol, sv.grids[vol->grid_id].n, w, p, k, wk);
+    return nearest_begin_v(*vol, sv.grids[vol->grid_id].n, w, p, k, wk, sv.x86);
 }
 __device__ __forceinline__ void nearest_end_v(const vpx_volume& vol, const uint8_t* cells, uint32_t n, const PathRay& w,
                                               uint32_t p, const skip::Walk& wk, bool hit);
@@ -773,7 +787,7 @@ __device__ __forceinline__ void primary_tile(const SceneView& sv, const FrameArg
         uint32_t rng = 0, flags = 0;
         if (go) {
             Rng g{pixel_seed(f.seed_base, f.frame_index, f.width, f.height, x, y)};
-            r = primary_ray(f, x, y, g);
+            r = primary_ray(f, x, y, g, sv.x86);
             rng = g.s;
             prim = 1;
             flags = kActive;
@@ -793,7 +807,7 @@ __device__ __forceinline__ void primary_tile(const SceneView& sv, const FrameArg
                 ORay o;
                 o.O = xform_pos_ssem(r.O, vol.inv_matrix);
                 o.D = xform_vec_ssem(r.D, vol.inv_matrix);
-                o.rD = mk(1.0f / o.D.x, 1.0f / o.D.y, 1.0f / o.D.z);
+                o.rD = nearest_rd(o.D, sv.x86);
                 Dda s;
                 if (!dda_setup(vol, sv.grids[vol.grid_id].n, o, s)) {
                     walk = false;
