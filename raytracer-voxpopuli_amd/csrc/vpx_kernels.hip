@@ -713,8 +713,7 @@ int validate_frame(vpx_ctx* c, const vpx_frame_params* p) {
 int ensure_wave(vpx_ctx* c, vpx_ctx::WaveStore& ws, uint32_t P, uint32_t L, uint32_t S) {
     const size_t f4 = sizeof(float4);
     const size_t bytes = (size_t)P * (f4 * (5 + 2 * (size_t)L + 3 * (size_t)S + 1) + 3 * sizeof(uint32_t)) +
-                         sizeof(uint32_t) * (size_t)P + (size_t)P / 8 + sizeof(uint32_t) * 2 * kMaxLevels +
-                         (size_t)P * S + 19 * 256;
+                         sizeof(uint32_t) * (size_t)P * 3 + sizeof(uint32_t) * kPoolWords + (size_t)P * S + 20 * 256;
     if (bytes > ws.bytes) {
         if (ws.d) {
             VPX_HIP(c, sync_all(c));
@@ -748,8 +747,9 @@ int ensure_wave(vpx_ctx* c, vpx_ctx::WaveStore& ws, uint32_t P, uint32_t L, uint
     w.depth = (int32_t*)take(4 * (size_t)P);
     w.forms = (uint32_t*)take(4 * (size_t)P);
     w.smask = (uint32_t*)take(4 * (size_t)P);
-    w.amask = (uint64_t*)take((size_t)P / 8);  // P is a multiple of 256
-    w.pool = (uint32_t*)take(sizeof(uint32_t) * 2 * kMaxLevels);
+    w.live0 = (uint32_t*)take(4 * (size_t)P);
+    w.live1 = (uint32_t*)take(4 * (size_t)P);
+    w.pool = (uint32_t*)take(sizeof(uint32_t) * kPoolWords);
     w.occb = (uint8_t*)take((size_t)P * S);
     return VPX_OK;
 }
@@ -761,17 +761,22 @@ constexpr int kMaxLaneQueues = 16;
 // device's CUs (a hardware queue of its own) while the process's lane-queue cap allows, else
 // a plain non-blocking stream.  Its work always joins back into the owner's stream within the
 // frame, so synchronising the owner covers it.
+void free_fork(vpx_ctx::WaveStore& ws);
 int ensure_fork(vpx_ctx* c, vpx_ctx::WaveStore& ws) {
-    if (ws.fork) return VPX_OK;
+    if (ws.fork && ws.ev_fork && ws.ev_join) return VPX_OK;
+    free_fork(ws);  // a partly created fork (an earlier failure): start clean
     std::vector<uint32_t> all_cus((c->cus + 31u) / 32u, 0xffffffffu);
     ws.fork_dedicated = g_lane_queues.fetch_add(1) < kMaxLaneQueues;
     if (!ws.fork_dedicated) g_lane_queues.fetch_sub(1);
     const hipError_t se = ws.fork_dedicated
                               ? hipExtStreamCreateWithCUMask(&ws.fork, (uint32_t)all_cus.size(), all_cus.data())
                               : hipStreamCreateWithFlags(&ws.fork, hipStreamNonBlocking);
+    if (se != hipSuccess) ws.fork = nullptr;
     if (se != hipSuccess || hipEventCreateWithFlags(&ws.ev_fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&ws.ev_join, hipEventDisableTiming) != hipSuccess)
+        hipEventCreateWithFlags(&ws.ev_join, hipEventDisableTiming) != hipSuccess) {
+        free_fork(ws);  // releases the counted queue and whatever was created
         return fail(c, VPX_E_DEVICE, "level fork: stream / event creation failed");
+    }
     return VPX_OK;
 }
 void free_fork(vpx_ctx::WaveStore& ws) {
@@ -835,13 +840,18 @@ int launch_render(vpx_ctx* c, hipStream_t s, vpx_ctx::WaveStore& ws, const Scene
     const bool spool = !rp && S > 1;
     if (!spool) w.occb = nullptr;  // k_resolve reads the slots' SD flags
     const uint32_t sgrab = std::max(1u, std::min(4u, kShadowList / (64u * S)));
+    // persistent launches over a level's live list (its length is on the device): as many
+    // workgroups as the device keeps resident, capped by the frame's tiles
+    auto resident = [&](uint32_t waves_per_simd) { return dim3(std::min(tiles, c->cus * waves_per_simd)); };
     auto shadow_pool = [&](int level) {
         const uint32_t grabs = (P / 64u + sgrab - 1u) / sgrab;
         const uint32_t waves = std::min(grabs, c->cus * 4u * (uint32_t)VPX_WPE_SPOOL);
         const uint32_t wpb = kPoolWg / 64u;
         hipLaunchKernelGGL(k_shadow_pool, dim3((waves + wpb - 1u) / wpb), dim3(kPoolWg), 0, s, sv, w, level, sgrab,
                            c->d_ctr);
-        if (!one) hipLaunchKernelGGL(k_shadow_inst, grid, block, slds, s, sv, w, c->d_ctr);
+        if (!one)
+            hipLaunchKernelGGL(level ? k_shadow_inst<false> : k_shadow_inst<true>,
+                               level ? resident(VPX_WPE_MULTI_SHADOW) : grid, block, slds, s, sv, w, level, c->d_ctr);
     };
     if (one && fuse_tail && f.max_bounces == 0 && tiles <= kFuseFrameTiles && S == 1) {
         // the whole depth-0 frame in one launch (k_frame0), its path state and one shadow slot
@@ -852,6 +862,9 @@ int launch_render(vpx_ctx* c, hipStream_t s, vpx_ctx::WaveStore& ws, const Scene
         VPX_HIP(c, hipGetLastError());
         return VPX_OK;
     }
+    // the frame's level counters (grabs, live-list lengths; kPool*): zeroed before the head,
+    // whose level-0 shade appends level 1's list
+    VPX_HIP(c, hipMemsetAsync(w.pool, 0, sizeof(uint32_t) * kPoolWords, s));
     prof_mark(c, s, VPX_STAGE_PRIMARY);
     const bool fuse_head = f.max_bounces >= 0;  // level 0's shade at the end of k_primary
     // multi-volume / shape scenes: the world walk in the lean head, then the instance pass
@@ -879,15 +892,13 @@ int launch_render(vpx_ctx* c, hipStream_t s, vpx_ctx::WaveStore& ws, const Scene
     auto bounce = [&](hipStream_t bs, int level) {
         prof_mark(c, bs, VPX_STAGE_BOUNCE);
         if (one) {  // the bounce pool: persistent waves, as many as the device keeps resident
-            const uint32_t grabs = (P / 64u + kPoolGrab - 1u) / kPoolGrab;
-            const uint32_t waves = std::min(grabs, c->cus * 4u * (uint32_t)VPX_WPE_BOUNCE);
+            const uint32_t chunks = (P + kPoolChunk - 1u) / kPoolChunk;
+            const uint32_t waves = std::min(chunks, c->cus * 4u * (uint32_t)VPX_WPE_BOUNCE);
             const uint32_t wpb = kPoolWg / 64u;
             hipLaunchKernelGGL(k_nearest_pool, dim3((waves + wpb - 1u) / wpb), dim3(kPoolWg), 0, bs, sv, w, level,
                                c->d_ctr);
-        } else {  // multi-volume / shape scenes (persistent waves without refills, k_nearest_mpool,
-                  // measured slower on Z1: 3.66-3.74 / 4.56-4.67 ms with grabs of 4 / 16 mask
-                  // words vs 2.50-2.54 — DESIGN.md §4)
-            hipLaunchKernelGGL(k_nearest_tile, grid, block, 0, bs, sv, w, c->d_ctr);
+        } else {  // multi-volume / shape scenes: persistent waves over the live list, 64 rays a grab
+            hipLaunchKernelGGL(k_nearest_tile, resident(VPX_WPE_MULTI_NEAREST), block, 0, bs, sv, w, level, c->d_ctr);
         }
         prof_mark(c, bs, -1);
     };
@@ -902,7 +913,7 @@ int launch_render(vpx_ctx* c, hipStream_t s, vpx_ctx::WaveStore& ws, const Scene
     if (fork && (rc = ensure_fork(c, ws))) return rc;
     // the last level's shadow -> resolve -> finish as one launch (k_shadow_finish)
     for (int level = 0; level <= f.max_bounces; ++level) {
-        if (!(fuse_head && level == 0)) {
+        if (!(fuse_head && level == 0)) {  // (level >= 1: the head shades level 0)
             prof_mark(c, s, VPX_STAGE_SHADE);
             hipLaunchKernelGGL(k_shade, grid, block, 0, s, sv, f, w, level, c->d_ctr);
             prof_mark(c, s, -1);
@@ -936,11 +947,15 @@ int launch_render(vpx_ctx* c, hipStream_t s, vpx_ctx::WaveStore& ws, const Scene
         prof_mark(c, s, VPX_STAGE_SHADOW);
         if (spool)
             shadow_pool(level);
-        else
+        else if (level == 0)
             hipLaunchKernelGGL(one ? k_shadow_tile<true> : k_shadow_tile<false>, grid, block, slds, s, sv, w, c->d_ctr);
+        else
+            hipLaunchKernelGGL(one ? k_shadow_list<true> : k_shadow_list<false>,
+                               resident(one ? VPX_WPE_SHADOW : VPX_WPE_MULTI_SHADOW), block, slds, s, sv, w, level,
+                               c->d_ctr);
         prof_mark(c, s, -1);
         prof_mark(c, s, VPX_STAGE_RESOLVE);
-        hipLaunchKernelGGL(k_resolve, grid, block, 0, s, sv, w);
+        hipLaunchKernelGGL(k_resolve, level ? resident(8) : grid, block, 0, s, sv, w, level);
         prof_mark(c, s, -1);
         if (forked)
             VPX_HIP(c, hipStreamWaitEvent(s, ws.ev_join, 0));
@@ -1153,6 +1168,9 @@ int vpx_set_pipeline(vpx_ctx* c, uint32_t depth) {
     VPX_HIP(c, sync_all(c));
     free_lanes(c);
     if (depth < 2) return VPX_OK;
+    // the context's own level fork (taken by a depth > 0 frame on the context's stream) gives
+    // its dedicated queue back: the lanes need them, and it is recreated if such a frame comes
+    free_fork(c->wave);
     c->lanes.resize(depth);
     // Each lane on a hardware queue of its own.  Plain streams share the process's pool of
     // GPU_MAX_HW_QUEUES (4) queues: a kernel trace shows two of three lanes on one queue and
@@ -1561,6 +1579,10 @@ int vpx_set_volumes(vpx_ctx* c, const vpx_volume* v, uint32_t count) {
         VPX_HIP(c, hipMalloc(&c->d_vbounds, sizeof(float4) * count));
         c->d_volumes_cap = count;
     }
+    // Invariant: d_volumes, d_vbounds and the TLAS (d_tlas) describe the same volumes.  The
+    // instance kernels cull by the TLAS root box and the bounding spheres (FindNearest's
+    // candidates, k_shadow_inst's slot cull), so a volume update that skipped build_tlas would
+    // silently drop instance hits and shadows: every writer of d_volumes goes through here.
     c->volumes.assign(v, v + count);
     std::vector<float4> bounds(count);
     for (uint32_t i = 0; i < count; ++i) bounds[i] = volume_bounds(v[i]);

@@ -95,14 +95,34 @@ struct WaveBufs {
     float4* SL;    // [S][P] unoccluded contribution of the slot
     float4* SM;    // [P] pending light: xyz = kd (area), w = bits(kind | discard<<3 | count<<4 | level<<8 | lc<<16)
     uint32_t* smask;  // [P] shadow slots emitted this level (bit s = slot s, s < 15) | light key << 16
-    uint64_t* amask;  // [P/64] bit p & 63 of word p >> 6: path p traces a next ray (the shades write it)
-    uint32_t* pool;   // [2 * kMaxLevels] the pools' grab counters: bounce walks of level l at [l], shadow walks
-                      // at [kMaxLevels + l] (k_primary zeroes them)
+    uint32_t* live0;  // [P] live-path lists: the paths that trace a ray at level l (l >= 1) are
+    uint32_t* live1;  //     live{l & 1}[0 .. pool[kPoolLive + l]) (appended by level l - 1's shade)
+    uint32_t* pool;   // [kPoolWords] the level counters (kPool*), zeroed at the start of every frame that
+                      // uses them (launch_render)
     uint8_t* occb;    // [S][P] the shadow pool's result per slot: 1 = occluded (valid slots only)
     float4* RD;    // [W*H] reprojection: level-0 intersection point, w = material bits (image order)
     uint32_t P;    // paths (pixels) this call
     uint32_t S;    // shadow slots per path
 };
+
+// Level counters in WaveBufs::pool: chunk grabs of the bounce walks / the shadow walks / the
+// multi-volume shadow pass of level l, and the length of level l's live-path list.
+constexpr uint32_t kPoolBounce = 0, kPoolShadow = kMaxLevels, kPoolLive = 2 * kMaxLevels,
+                   kPoolShadow2 = 3 * kMaxLevels, kPoolWords = 4 * kMaxLevels;
+
+// Level l's paths: level 0 is every path of the launch (p = i); a later level's are the paths
+// that trace a ray there, listed by the previous level's shade (put_live).  Every kernel after
+// level 0's head walks / shades / resolves the list, so a level costs its live paths — Z1's
+// deep levels hold a few thousand of the frame's two million.
+__device__ __forceinline__ const uint32_t* live_list(const WaveBufs& w, int level) {
+    return (level & 1) ? w.live1 : w.live0;
+}
+__device__ __forceinline__ uint32_t live_count(const WaveBufs& w, int level) {
+    return level ? __builtin_amdgcn_readfirstlane(w.pool[kPoolLive + level]) : w.P;
+}
+__device__ __forceinline__ uint32_t live_path(const WaveBufs& w, int level, uint32_t i) {
+    return level ? live_list(w, level)[i] : i;
+}
 
 // ------------------------------------------------------------------ primary rays
 // Camera::GetPrimaryRayNoDOF (camera.h:103-110) / GetPrimaryRay + thin lens (:68-83);
@@ -534,17 +554,34 @@ __device__ __forceinline__ bool shade_path(const SceneView& sv, const FrameArgs&
     return cont;
 }
 
-// The bounce pool's mask word of this wave's 64 paths (p = the wave's first path + lane).
-__device__ __forceinline__ void put_amask(const WaveBufs& w, uint32_t p, bool cont) {
+// Append the wave's continuing paths to the next level's list (one atomic per wave; the
+// order of the waves' runs is whatever the atomics give — each path's work is independent of
+// its place, so results and counts are too).  Called by the whole wave.
+__device__ __forceinline__ uint32_t lane_rank(uint64_t m) {  // set bits of m below this lane
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+__device__ __forceinline__ void put_live(const WaveBufs& w, uint32_t p, bool cont, int next) {
     const uint64_t b = __ballot(cont);
-    if ((threadIdx.x & 63u) == 0 && p < w.P) w.amask[p >> 6] = b;
+    if (!b) return;
+    uint32_t base = 0u;
+    if ((threadIdx.x & 63u) == (uint32_t)__ffsll((unsigned long long)b) - 1u)
+        base = atomicAdd(&w.pool[kPoolLive + next], (uint32_t)__popcll(b));
+    base = __builtin_amdgcn_readlane(base, __ffsll((unsigned long long)b) - 1);
+    if (cont) ((next & 1) ? w.live1 : w.live0)[base + lane_rank(b)] = p;
 }
 
+// Level l >= 1's material switch over its live list: the launch is sized for the largest list
+// (the count is on the device), workgroups past the list's end return at once (a grid-stride
+// loop kept more registers live: 113 VGPRs and scratch instead of 90).
 __global__ __launch_bounds__(256) void k_shade(SceneView sv, FrameArgs f, WaveBufs w, int level,
                                                unsigned long long* ctr) {
     Counters k{0u, 0u, 0u};
-    const uint32_t p = blockIdx.x * 256u + threadIdx.x;
-    put_amask(w, p, shade_path(sv, f, w, PathRay{w.O, w.D, w.H, w.HM, 0u}, p, level, k));
+    const uint32_t n = live_count(w, level);
+    if (blockIdx.x * 256u >= n) return;
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    const uint32_t p = i < n ? live_path(w, level, i) : ~0u;  // ~0u: shade_path does nothing
+    const bool cont = shade_path(sv, f, w, PathRay{w.O, w.D, w.H, w.HM, 0u}, p, level, k);
+    if (level < f.max_bounces) put_live(w, p, cont, level + 1);
     flush_counters(k, 0u, ctr, VPX_STAGE_SHADE);
 }
 
@@ -605,8 +642,10 @@ __device__ __forceinline__ void resolve_path(const SceneView& sv, const WaveBufs
         out);
 }
 
-__global__ __launch_bounds__(256) void k_resolve(SceneView sv, WaveBufs w) {
-    resolve_path(sv, w, blockIdx.x * 256u + threadIdx.x);
+__global__ __launch_bounds__(256) void k_resolve(SceneView sv, WaveBufs w, int level) {
+    const uint32_t n = live_count(w, level);
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u)
+        resolve_path(sv, w, live_path(w, level, i));
 }
 
 // ------------------------------------------------------------ tile kernels
@@ -774,7 +813,6 @@ __device__ __forceinline__ void primary_tile(const SceneView& sv, const FrameArg
     Counters k{0u, 0u, 0u};
     uint32_t prim = 0;
     bool walk = false;
-    if (blockIdx.x == 0 && threadIdx.x < 2u * kMaxLevels && w.pool) w.pool[threadIdx.x] = 0u;  // the frame's pools
     if (p < w.P) {
         uint32_t x, y;
         bool go = path_pixel(f, p, x, y);
@@ -840,7 +878,7 @@ __device__ __forceinline__ void primary_tile(const SceneView& sv, const FrameArg
         __syncthreads();  // the tile's hit records, written by the compacted walkers
         Counters ks{0u, 0u, 0u};
         const bool cont = shade_path<true>(sv, f, w, pr, p, 0, ks);
-        if (f.max_bounces > 0) put_amask(w, p, cont);
+        if (f.max_bounces > 0) put_live(w, p, cont, 1);
         flush_counters(ks, 0u, ctr, VPX_STAGE_SHADE);
     }
 }
@@ -905,7 +943,7 @@ __global__ __launch_bounds__(256) VPX_WPE(VPX_WPE_MULTI_NEAREST) void k_instance
     __syncthreads();  // the tile's hit records, as the compacted lanes left them
     Counters ks{0u, 0u, 0u};
     const bool cont = shade_path<true>(sv, f, w, pr, p, 0, ks);
-    if (f.max_bounces > 0) put_amask(w, p, cont);
+    if (f.max_bounces > 0) put_live(w, p, cont, 1);
     flush_counters(ks, 0u, ctr, VPX_STAGE_SHADE);
 }
 
@@ -917,27 +955,31 @@ __global__ __launch_bounds__(256) VPX_WPE(VPX_WPE_MULTI_NEAREST) void k_instance
 // order of a counting sort by (direction octant, Morton index of the origin's 16^3-cell
 // region): the sorted walker took 553 vs 541 us per level on C2 and the sort 350 us more —
 // coherent starts do not shorten the walks, whose cost is their length and step latency.
-// Multi-volume / shape scenes (the single-volume scenes walk their bounces in the pool below).
-__global__ __launch_bounds__(256) VPX_WPE(VPX_WPE_MULTI_NEAREST) void k_nearest_tile(SceneView sv, WaveBufs w,
+// Multi-volume / shape scenes (the single-volume scenes walk their bounces in the pool below):
+// the next level's live list in chunks of 64 entries, one per wave grab (persistent waves, no
+// barriers), so every wave is full — a tile's compaction left a deep level's few rays spread
+// one or two per wave over the frame's 8100 tiles (Z1: 14 levels, 2 M paths at level 1, 4 k at
+// level 14, each launch scanning all 2 M).  `level` is the shade level whose rays it walks.
+__global__ __launch_bounds__(256) VPX_WPE(VPX_WPE_MULTI_NEAREST) void k_nearest_tile(SceneView sv, WaveBufs w, int level,
                                                                                     unsigned long long* __restrict__ ctr) {
-    __shared__ uint32_t sh[4];
-    __shared__ uint32_t lst[256];
-    const uint32_t base = tile_block() * 256u;
     Counters k{0u, 0u, 0u};
-    uint32_t total;
-    const uint32_t p = base + threadIdx.x;
-    const uint32_t cnt = (p < w.P && (__float_as_uint(w.D[p].w) & kActive)) ? 1u : 0u;
-    const uint32_t at = block_scan(cnt, total, sh);
-    if (cnt) lst[at] = p;
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < total; i += 256u) {
-        const uint32_t q = lst[i];
-        const float4 o = w.O[q], d = w.D[q];
-        Ray r;
-        r.O = mk(o.x, o.y, o.z);
-        r.D = mk(d.x, d.y, d.z);
-        r.inside = (__float_as_uint(d.w) & kInside) != 0u;
-        nearest_record<kSkipwBounce, kMincBounce, kRunBounce>(sv, PathRay{w.O, w.D, w.H, w.HM, 0u}, q, r, k);
+    const uint32_t n = live_count(w, level + 1);
+    const uint32_t lane = threadIdx.x & 63u;
+    for (;;) {
+        uint32_t g = 0u;
+        if (lane == 0u) g = atomicAdd(&w.pool[kPoolBounce + level], 1u);
+        g = __builtin_amdgcn_readfirstlane(g);
+        if (g * 64u >= n) break;
+        const uint32_t i = g * 64u + lane;
+        if (i < n) {
+            const uint32_t q = live_path(w, level + 1, i);
+            const float4 o = w.O[q], d = w.D[q];
+            Ray r;
+            r.O = mk(o.x, o.y, o.z);
+            r.D = mk(d.x, d.y, d.z);
+            r.inside = (__float_as_uint(d.w) & kInside) != 0u;
+            nearest_record<kSkipwBounce, kMincBounce, kRunBounce>(sv, PathRay{w.O, w.D, w.H, w.HM, 0u}, q, r, k);
+        }
     }
     flush_counters(k, 0u, ctr, VPX_STAGE_BOUNCE);
 }
@@ -946,8 +988,9 @@ __global__ __launch_bounds__(256) VPX_WPE(VPX_WPE_MULTI_NEAREST) void k_nearest_
 // walked by persistent waves that refill their finished lanes.  A tile's bounce walks are
 // heavy-tailed (C2: of a walk iteration's 64 lanes 16 step, 9 wait to skip and 39 are already
 // done), and a tile's ~90 bounce rays leave its second wave mostly empty; here each wave takes
-// the next kPoolGrab x 64 paths at a time (one global atomic), lists the traced ones of them in
-// its LDS (their bits in the shades' amask words), and hands them to its lanes as lanes free up:
+// the next kPoolChunk entries of the level's live list at a time (one global atomic; every
+// entry traces a ray — until round 4 a grab was 4 words of a per-path trace mask, ~90 traced
+// rays of 256 paths), and hands them to its lanes as lanes free up:
 // the walk returns once kPoolLeave lanes have finished, their hit records are written, and new
 // rays start in their place while the others keep their walk state.  Every ray is walked by
 // exactly the per-lane sequence of nearest_record_1v (same cells, same counts, same records);
@@ -956,8 +999,8 @@ __global__ __launch_bounds__(256) VPX_WPE(VPX_WPE_MULTI_NEAREST) void k_nearest_
 // pool 2.72 / 2.68 / 2.70; 64-thread workgroups 2.83 / 2.82 / 2.77; leave at 8 finished lanes
 // 2.75 / 2.73 / 2.74, at 32 2.71 / 2.72 / 2.65; grabs of 2 words 2.84 / 2.77 / 2.82, of 8
 // 2.79 / 2.79 / 2.71.
-#ifndef VPX_POOL_GRAB
-#define VPX_POOL_GRAB 4
+#ifndef VPX_POOL_CHUNK
+#define VPX_POOL_CHUNK 128
 #endif
 #ifndef VPX_POOL_LEAVE
 #define VPX_POOL_LEAVE 16
@@ -965,26 +1008,22 @@ __global__ __launch_bounds__(256) VPX_WPE(VPX_WPE_MULTI_NEAREST) void k_nearest_
 #ifndef VPX_POOL_WG
 #define VPX_POOL_WG 256
 #endif
-constexpr uint32_t kPoolGrab = VPX_POOL_GRAB;    // mask words (x 64 paths) per grab
+constexpr uint32_t kPoolChunk = VPX_POOL_CHUNK;  // list entries (traced rays) per grab
 constexpr uint32_t kPoolLeave = VPX_POOL_LEAVE;  // finished lanes that end a walk while rays are left
 constexpr uint32_t kPoolWg = VPX_POOL_WG;        // threads per workgroup (its waves are independent)
-__device__ __forceinline__ uint32_t lane_rank(uint64_t m) {  // set bits of m below this lane
-    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-}
 __global__ __launch_bounds__(kPoolWg) VPX_WPE(VPX_WPE_BOUNCE) void k_nearest_pool(SceneView sv, WaveBufs w, int level,
                                                                                unsigned long long* __restrict__ ctr) {
-    __shared__ uint32_t lst_wg[kPoolWg / 64][kPoolGrab * 64];
-    uint32_t* lst = lst_wg[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)];
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t words = (w.P + 63u) >> 6, grabs = (words + kPoolGrab - 1u) / kPoolGrab;
+    const uint32_t n = live_count(w, level + 1);  // the rays level `level`'s shade traced
+    const uint32_t* L = live_list(w, level + 1);
     const PathRay pr{w.O, w.D, w.H, w.HM, 0u};
     const skip::GridView gv = grid_view(sv.grids[uni_ptr(&sv.volumes[0])->grid_id]);
     Counters k{0u, 0u, 0u};
     skip::Walk wk;
     uint32_t q = ~0u;     // the path this lane walks (~0u: none)
     int mode = kWalkMiss;
-    uint32_t avail = 0u, cur = 0u;  // listed paths not yet handed out, and where they start
-    bool more = true;               // paths may be left in the pool
+    uint32_t avail = 0u, cur = 0u;  // grabbed list entries not yet handed out, and where they start
+    bool more = true;               // entries may be left in the list
     for (;;) {
         if (q != ~0u && mode >= kWalkMiss) {  // finished: its hit record
             nearest_end_1v(sv, pr, q, wk, mode == kWalkHit);
@@ -993,38 +1032,28 @@ __global__ __launch_bounds__(kPoolWg) VPX_WPE(VPX_WPE_BOUNCE) void k_nearest_poo
         while (more) {
             const uint64_t idle = __ballot(q == ~0u);
             if (!idle) break;
-            if (avail == 0u) {  // take the next paths from the pool and list the traced ones
+            if (avail == 0u) {  // the next chunk of the list (every entry traces a ray)
                 uint32_t g = 0u;
-                if (lane == 0u) g = atomicAdd(&w.pool[level], 1u);
+                if (lane == 0u) g = atomicAdd(&w.pool[kPoolBounce + level], 1u);
                 g = __builtin_amdgcn_readfirstlane(g);
-                if (g >= grabs) {
+                if (g * kPoolChunk >= n) {
                     more = false;
                     break;
                 }
-                wave_sync();  // the wave's earlier reads of lst are done
-                uint32_t n = 0u;
-#pragma unroll
-                for (uint32_t j = 0; j < kPoolGrab; ++j) {
-                    const uint32_t wi = g * kPoolGrab + j;
-                    const uint64_t m = wi < words ? w.amask[wi] : 0ull;
-                    if ((m >> lane) & 1ull) lst[n + lane_rank(m)] = wi * 64u + lane;
-                    n += (uint32_t)__popcll(m);
-                }
-                wave_sync();
-                avail = n;
-                cur = 0u;
+                cur = g * kPoolChunk;
+                avail = min(kPoolChunk, n - cur);
                 continue;
             }
             const uint32_t take = min((uint32_t)__popcll(idle), avail);
             const uint32_t r = lane_rank(idle);
             if (q == ~0u && r < take) {
-                q = lst[cur + r];
+                q = L[cur + r];
                 mode = nearest_begin_1v(sv, pr, q, k, wk) ? kWalkStep : kWalkMiss;
             }
             cur += take;
             avail -= take;
         }
-        if (!__ballot(q != ~0u)) break;  // the pool is empty and every lane is done
+        if (!__ballot(q != ~0u)) break;  // the list is done and every lane is done
         walk_wave<0, kSkipwBouncePool, kMincBouncePool, kRunBouncePool, true>(gv, wk, kBig, k.cells, &mode,
                                                                    more ? kPoolLeave : 65u);
     }
@@ -1051,14 +1080,14 @@ __device__ __forceinline__ void mark_occluded(const WaveBufs& w, uint64_t slot, 
 // keep kRunShadow: the two-compare step (5 spilled VGPRs instead of 3) measured C1
 // 0.5824-0.5839 vs 0.5833-0.5859 ms and runs of 4 cells 0.5843-0.5873 (round 3, three
 // interleaved runs each: noise / slower).
+// p: this thread's path (the tile's, or a live-list entry; >= w.P: none).
 template <bool ONE, uint32_t RUN = kRunShadow>
 __device__ __forceinline__ void shadow_tile(const SceneView& sv, const WaveBufs& w, unsigned long long* __restrict__ ctr,
-                                            uint32_t* occ = nullptr) {
+                                            uint32_t* occ, uint32_t p) {
     __shared__ uint32_t sh[4];
     if (occ)
         for (uint32_t i = threadIdx.x; i < w.S * 8u; i += 256u) occ[i] = 0u;  // published by the barriers below
     extern __shared__ uint32_t lst_dyn[];  // [S * 256]
-    const uint32_t base = tile_block() * 256u;
     Counters k{0u, 0u, 0u};
     // counting sort of the tile's slots by light key: LDS histogram (the order inside a
     // bucket is whatever the atomics give — it only orders independent walks), bucket
@@ -1066,7 +1095,6 @@ __device__ __forceinline__ void shadow_tile(const SceneView& sv, const WaveBufs&
     __shared__ uint32_t hist[kLightKeys];
     if (threadIdx.x < kLightKeys) hist[threadIdx.x] = 0u;
     __syncthreads();
-    const uint32_t p = base + threadIdx.x;
     const uint32_t sm = p < w.P ? w.smask[p] : 0u;
     const uint32_t m = sm & kSlotBits, key = sm >> 16;
     const uint32_t pos = m ? atomicAdd(&hist[key], (uint32_t)__popc(m)) : 0u;
@@ -1124,7 +1152,26 @@ __device__ __forceinline__ void shadow_tile(const SceneView& sv, const WaveBufs&
 
 template <bool ONE>
 __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_SHADOW : VPX_WPE_MULTI_SHADOW) void k_shadow_tile(SceneView sv, WaveBufs w, unsigned long long* __restrict__ ctr) {
-    shadow_tile<ONE>(sv, w, ctr);
+    shadow_tile<ONE>(sv, w, ctr, nullptr, tile_block() * 256u + threadIdx.x);
+}
+
+// Level l's shadow walks over its live list: persistent workgroups take 256 entries at a time
+// (one atomic per grab) and walk those paths' slots as shadow_tile walks a tile's (counting-
+// sorted by light).  Level 0 (every path) takes the tiles in order.
+template <bool ONE>
+__global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_SHADOW : VPX_WPE_MULTI_SHADOW) void k_shadow_list(SceneView sv, WaveBufs w, int level,
+                                                                                                       unsigned long long* __restrict__ ctr) {
+    __shared__ uint32_t chunk;
+    const uint32_t n = live_count(w, level);
+    for (;;) {
+        if (threadIdx.x == 0) chunk = atomicAdd(&w.pool[kPoolShadow + level], 1u);
+        __syncthreads();
+        const uint32_t c = chunk;
+        __syncthreads();  // every thread has read it before the next grab
+        if (c * 256u >= n) break;
+        const uint32_t i = c * 256u + threadIdx.x;
+        shadow_tile<ONE>(sv, w, ctr, nullptr, i < n ? live_path(w, level, i) : ~0u);
+    }
 }
 
 // The shadow pool (single-volume scenes): Renderer::IsOccluded for a level's shadow slots,
@@ -1149,7 +1196,8 @@ __global__ __launch_bounds__(kPoolWg) VPX_WPE(VPX_WPE_SPOOL) void k_shadow_pool(
     uint32_t* lst = lst_wg[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)];
     uint32_t* hist = hist_wg[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)];
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t words = (w.P + 63u) >> 6, grabs = (words + grab - 1u) / grab;
+    const uint32_t n = live_count(w, level);  // level 0: every path; later: the level's live list
+    const uint32_t grabs = (n + 64u * grab - 1u) / (64u * grab);
     const vpx_volume* vol = uni_ptr(&sv.volumes[0]);
     const DevGrid g = sv.grids[vol->grid_id];
     const skip::GridView gv = grid_view(g);
@@ -1185,8 +1233,8 @@ __global__ __launch_bounds__(kPoolWg) VPX_WPE(VPX_WPE_SPOOL) void k_shadow_pool(
                 uint32_t smv[4], pos[4];
 #pragma unroll
                 for (uint32_t j = 0; j < 4; ++j) {
-                    const uint32_t p = (gi * grab + j) * 64u + lane;
-                    smv[j] = (j < grab && p < w.P) ? w.smask[p] : 0u;
+                    const uint32_t i = (gi * grab + j) * 64u + lane;
+                    smv[j] = (j < grab && i < n) ? w.smask[live_path(w, level, i)] : 0u;
                     const uint32_t m = smv[j] & kSlotBits;
                     pos[j] = m ? atomicAdd(&hist[smv[j] >> 16], (uint32_t)__popc(m)) : 0u;
                 }
@@ -1200,7 +1248,7 @@ __global__ __launch_bounds__(kPoolWg) VPX_WPE(VPX_WPE_SPOOL) void k_shadow_pool(
                 for (uint32_t j = 0; j < 4; ++j) {
                     const uint32_t m = smv[j] & kSlotBits;
                     if (m) {
-                        const uint32_t p = (gi * grab + j) * 64u + lane;
+                        const uint32_t p = live_path(w, level, (gi * grab + j) * 64u + lane);
                         uint32_t at = hist[smv[j] >> 16] + pos[j];
                         for (uint32_t b = m; b; b &= b - 1u) lst[at++] = ((uint32_t)__ffs(b) - 1u) << 27 | p;
                     }
@@ -1290,16 +1338,13 @@ __device__ __forceinline__ bool occluded_instances(const SceneView& sv, const fl
     return false;
 }
 
-__global__ __launch_bounds__(256) VPX_WPE(VPX_WPE_MULTI_SHADOW) void k_shadow_inst(SceneView sv, WaveBufs w,
-                                                                                  unsigned long long* __restrict__ ctr) {
+// One tile's (or 256 live-list entries') remaining slots: p = this thread's path (>= P: none).
+__device__ __forceinline__ void shadow_inst_chunk(const SceneView& sv, const WaveBufs& w, unsigned long long* __restrict__ ctr,
+                                                  const float4* vb, uint32_t p) {
     __shared__ uint32_t sh[4];
-    __shared__ float4 vb[kTlasMaxVolumes];
     extern __shared__ uint32_t lst_dyn[];  // [S * 256]
-    if (VPX_INST_MASK && threadIdx.x < sv.num_volumes && threadIdx.x < kTlasMaxVolumes)
-        vb[threadIdx.x] = sv.vbounds[threadIdx.x];  // published by the barriers below
     __shared__ uint32_t hist[kLightKeys];
     if (threadIdx.x < kLightKeys) hist[threadIdx.x] = 0u;
-    const uint32_t p = tile_block() * 256u + threadIdx.x;
     Counters k{0u, 0u, 0u};
     const uint32_t smv = p < w.P ? w.smask[p] : 0u;
     const uint32_t m = smv & kSlotBits, key = smv >> 16;
@@ -1353,6 +1398,30 @@ __global__ __launch_bounds__(256) VPX_WPE(VPX_WPE_MULTI_SHADOW) void k_shadow_in
         if (occ) w.occb[slot] = 1u;
     }
     flush_counters(k, 0u, ctr, VPX_STAGE_SHADOW);
+}
+
+// L0 (level 0): one tile per workgroup; later levels: the live list, 256 entries per grab.
+template <bool L0>
+__global__ __launch_bounds__(256) VPX_WPE(VPX_WPE_MULTI_SHADOW) void k_shadow_inst(SceneView sv, WaveBufs w, int level,
+                                                                                  unsigned long long* __restrict__ ctr) {
+    __shared__ float4 vb[kTlasMaxVolumes];
+    if (VPX_INST_MASK && threadIdx.x < sv.num_volumes && threadIdx.x < kTlasMaxVolumes)
+        vb[threadIdx.x] = sv.vbounds[threadIdx.x];  // published by the barriers in the chunk
+    if (L0) {
+        shadow_inst_chunk(sv, w, ctr, vb, tile_block() * 256u + threadIdx.x);
+        return;
+    }
+    __shared__ uint32_t chunk;
+    const uint32_t n = live_count(w, level);
+    for (;;) {
+        if (threadIdx.x == 0) chunk = atomicAdd(&w.pool[kPoolShadow2 + level], 1u);
+        __syncthreads();
+        const uint32_t c = chunk;
+        __syncthreads();
+        if (c * 256u >= n) break;
+        const uint32_t i = c * 256u + threadIdx.x;
+        shadow_inst_chunk(sv, w, ctr, vb, i < n ? live_path(w, level, i) : ~0u);
+    }
 }
 
 // ------------------------------------------------------------------- stage 4
@@ -1468,9 +1537,10 @@ __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_SHADOW : VPX_WPE_MULTI_S
     SceneView sv, FrameArgs f, WaveBufs w, unsigned long long* __restrict__ ctr, float4* __restrict__ accum,
     uint32_t* __restrict__ rgb8, float4* __restrict__ packed) {
     __shared__ uint32_t occ[kOccWords];
-    shadow_tile<ONE>(sv, w, ctr, occ);
+    shadow_tile<ONE>(sv, w, ctr, occ, tile_block() * 256u + threadIdx.x);
     __syncthreads();
-    const uint32_t p = tile_block() * 256u + threadIdx.x;
+    uint32_t p = tile_block() * 256u + threadIdx.x;  // re-derived after the walks, not kept live across them
+    asm volatile("" : "+v"(p));
     LightSum ls;
     resolve_path(sv, w, p, occ, &ls);
     finish_path<MODE>(f, w, p, accum, rgb8, packed, &ls);
@@ -1536,7 +1606,9 @@ __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_FRAME : VPX_WPE_MULTI_NE
     wl.SL = L.ray + 512 - tb;
     primary_tile<ONE, true>(sv, f, wl, L, ctr);
     __syncthreads();
-    shadow_tile<ONE, kRunShadow>(sv, wl, ctr, occ);
+    uint32_t ps = p;  // re-derived, not kept live across the head (as pt below)
+    asm volatile("" : "+v"(ps));
+    shadow_tile<ONE, kRunShadow>(sv, wl, ctr, occ, ps);
     __syncthreads();
     // the tail's own copy of p: the shade's per-lane LDS addresses are re-derived here
     // instead of being kept live (spilled) across the shadow walks
