@@ -713,7 +713,8 @@ int validate_frame(vpx_ctx* c, const vpx_frame_params* p) {
 int ensure_wave(vpx_ctx* c, vpx_ctx::WaveStore& ws, uint32_t P, uint32_t L, uint32_t S) {
     const size_t f4 = sizeof(float4);
     const size_t bytes = (size_t)P * (f4 * (5 + 2 * (size_t)L + 3 * (size_t)S + 1) + 3 * sizeof(uint32_t)) +
-                         sizeof(uint32_t) * (size_t)P * 3 + sizeof(uint32_t) * kPoolWords + (size_t)P * S + 20 * 256;
+                         sizeof(uint32_t) * (size_t)P * 3 + (size_t)P / 8 + sizeof(uint32_t) * kPoolWords +
+                         (size_t)P * S + 21 * 256;
     if (bytes > ws.bytes) {
         if (ws.d) {
             VPX_HIP(c, sync_all(c));
@@ -749,6 +750,7 @@ int ensure_wave(vpx_ctx* c, vpx_ctx::WaveStore& ws, uint32_t P, uint32_t L, uint
     w.smask = (uint32_t*)take(4 * (size_t)P);
     w.live0 = (uint32_t*)take(4 * (size_t)P);
     w.live1 = (uint32_t*)take(4 * (size_t)P);
+    w.amask = (uint64_t*)take((size_t)P / 8);  // P is a multiple of 256
     w.pool = (uint32_t*)take(sizeof(uint32_t) * kPoolWords);
     w.occb = (uint8_t*)take((size_t)P * S);
     return VPX_OK;
@@ -934,9 +936,12 @@ int launch_render(vpx_ctx* c, hipStream_t s, vpx_ctx::WaveStore& ws, const Scene
             }
             break;
         }
-        // the level fork: the next level's bounce walks read only the rays and trace mask
-        // this level's shade wrote and write only the hit records, which the shadow walks and
-        // the light sums do not touch — so they run beside them on the fork stream
+        // the next level's live list from this level's shade bits
+        if (level < f.max_bounces)
+            hipLaunchKernelGGL(k_compact, dim3((P / 64u + 255u) / 256u), block, 0, s, w, level);
+        // the level fork: the next level's bounce walks read only the rays and live list this
+        // level's shade and k_compact wrote and write only the hit records, which the shadow
+        // walks and the light sums do not touch — so they run beside them on the fork stream
         const bool forked = fork && level < f.max_bounces;
         if (forked) {
             VPX_HIP(c, hipEventRecord(ws.ev_fork, s));

@@ -101,6 +101,8 @@ int Renderer::SetSky(const float* rgb, uint32_t width, uint32_t height, float hd
     return status_ ? status_ : vpx_set_sky(ctx_, rgb, width, height, hdr_contribution);
 }
 
+int Renderer::SetArithmetic(uint32_t mode) { return status_ ? status_ : vpx_set_arithmetic(ctx_, mode); }
+
 int Renderer::CopyToPrevCamera() {
     if (status_) return status_;
     const int rc = vpx_prev_camera_look_at(camPos_, camTarget_, width_, height_, &prevCamera);

@@ -47,6 +47,9 @@ public:
     int SetSky(const float* rgb, uint32_t width, uint32_t height, float hdr_contribution);
     // prevCamera = the current camera (CopyToPrevCamera, renderer.cpp:1893-1902).
     int CopyToPrevCamera();
+    // The reference's own x86 arithmetic (FastReciprocal in FindNearest, rsqrtps for the
+    // primary rays) as this host computes it: VPX_ARITH_X86_HOST; VPX_ARITH_EXACT (default).
+    int SetArithmetic(uint32_t mode);
 
     // --- per frame -----------------------------------------------------------------------
     void ResetAccumulator() { numRenderedFrames = 0; }  // renderer.cpp:343-346

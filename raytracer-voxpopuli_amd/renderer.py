@@ -46,6 +46,12 @@ class Renderer:
         self._sky_uploaded = (self.skyPixels, self.HDRLightContribution)
         return self
 
+    def SetArithmetic(self, mode):
+        """abi.VPX_ARITH_X86_HOST: the reference's FastReciprocal / rsqrtps as this host computes
+        them (vpx_set_arithmetic); abi.VPX_ARITH_EXACT: exact 1/x, 1/sqrtf (default)."""
+        self.ctx.set_arithmetic(mode)
+        return self
+
     def _frame_params(self):
         p = self.scene.frame_params(frame_index=self.numRenderedFrames)
         p.max_bounces = self.maxBounces
