@@ -852,8 +852,8 @@ int launch_render(vpx_ctx* c, hipStream_t s, vpx_ctx::WaveStore& ws, const Scene
         hipLaunchKernelGGL(k_shadow_pool, dim3((waves + wpb - 1u) / wpb), dim3(kPoolWg), 0, s, sv, w, level, sgrab,
                            c->d_ctr);
         if (!one)
-            hipLaunchKernelGGL(level ? k_shadow_inst<false> : k_shadow_inst<true>,
-                               level ? resident(VPX_WPE_MULTI_SHADOW) : grid, block, slds, s, sv, w, level, c->d_ctr);
+            hipLaunchKernelGGL(level ? k_shadow_inst<false> : k_shadow_inst<true>, grid, block, slds, s, sv, w, level,
+                               c->d_ctr);
     };
     if (one && fuse_tail && f.max_bounces == 0 && tiles <= kFuseFrameTiles && S == 1) {
         // the whole depth-0 frame in one launch (k_frame0), its path state and one shadow slot
@@ -900,7 +900,7 @@ int launch_render(vpx_ctx* c, hipStream_t s, vpx_ctx::WaveStore& ws, const Scene
             hipLaunchKernelGGL(k_nearest_pool, dim3((waves + wpb - 1u) / wpb), dim3(kPoolWg), 0, bs, sv, w, level,
                                c->d_ctr);
         } else {  // multi-volume / shape scenes: persistent waves over the live list, 64 rays a grab
-            hipLaunchKernelGGL(k_nearest_tile, resident(VPX_WPE_MULTI_NEAREST), block, 0, bs, sv, w, level, c->d_ctr);
+            hipLaunchKernelGGL(k_nearest_tile, grid, block, 0, bs, sv, w, level, c->d_ctr);
         }
         prof_mark(c, bs, -1);
     };
@@ -955,8 +955,7 @@ int launch_render(vpx_ctx* c, hipStream_t s, vpx_ctx::WaveStore& ws, const Scene
         else if (level == 0)
             hipLaunchKernelGGL(one ? k_shadow_tile<true> : k_shadow_tile<false>, grid, block, slds, s, sv, w, c->d_ctr);
         else
-            hipLaunchKernelGGL(one ? k_shadow_list<true> : k_shadow_list<false>,
-                               resident(one ? VPX_WPE_SHADOW : VPX_WPE_MULTI_SHADOW), block, slds, s, sv, w, level,
+            hipLaunchKernelGGL(one ? k_shadow_list<true> : k_shadow_list<false>, grid, block, slds, s, sv, w, level,
                                c->d_ctr);
         prof_mark(c, s, -1);
         prof_mark(c, s, VPX_STAGE_RESOLVE);

@@ -107,10 +107,13 @@ struct WaveBufs {
     uint32_t S;    // shadow slots per path
 };
 
-// Level counters in WaveBufs::pool: chunk grabs of the bounce walks / the shadow walks / the
-// multi-volume shadow pass of level l, and the length of level l's live-path list.
-constexpr uint32_t kPoolBounce = 0, kPoolShadow = kMaxLevels, kPoolLive = 2 * kMaxLevels,
-                   kPoolShadow2 = 3 * kMaxLevels, kPoolWords = 4 * kMaxLevels;
+// Level counters in WaveBufs::pool: the length of level l's live-path list, and the pools'
+// chunk grabs (kGrabStripes counters per level) of its shadow walks and its bounce walks.
+// (Spreading the pools' grabs over 16 counters per level — stripe s dealing chunks s, s + 16,
+// ... — measured much slower: C2 5.64 vs 2.54 ms, C3 3.93 vs 3.65, C4 49.7 vs 43.1.  The
+// counters share a cache line, so the L2 still serialises them, the tail takes up to 16 atomics
+// per wave, and the frame is no longer swept in order, so the waves' lines are spread further.)
+constexpr uint32_t kPoolLive = 0, kPoolShadow = kMaxLevels, kPoolBounce = 2 * kMaxLevels, kPoolWords = 3 * kMaxLevels;
 
 // Level l's paths: level 0 is every path of the launch (p = i); a later level's are the paths
 // that trace a ray there, listed by the previous level's shade (put_live).  Every kernel after
@@ -988,8 +991,8 @@ __global__ __launch_bounds__(256) void k_compact(WaveBufs w, int level) {
 // region): the sorted walker took 553 vs 541 us per level on C2 and the sort 350 us more —
 // coherent starts do not shorten the walks, whose cost is their length and step latency.
 // Multi-volume / shape scenes (the single-volume scenes walk their bounces in the pool below):
-// the next level's live list in chunks of 64 entries, one per wave grab (persistent waves, no
-// barriers), so every wave is full — a tile's compaction left a deep level's few rays spread
+// the next level's live list in chunks of 64 entries (persistent waves, no barriers), so
+// every wave is full — a tile's compaction left a deep level's few rays spread
 // one or two per wave over the frame's 8100 tiles (Z1: 14 levels, 2 M paths at level 1, 4 k at
 // level 14, each launch scanning all 2 M).  `level` is the shade level whose rays it walks.
 __global__ __launch_bounds__(256) VPX_WPE(VPX_WPE_MULTI_NEAREST) void k_nearest_tile(SceneView sv, WaveBufs w, int level,
@@ -997,11 +1000,13 @@ __global__ __launch_bounds__(256) VPX_WPE(VPX_WPE_MULTI_NEAREST) void k_nearest_
     Counters k{0u, 0u, 0u};
     const uint32_t n = live_count(w, level + 1);
     const uint32_t lane = threadIdx.x & 63u;
-    for (;;) {
-        uint32_t g = 0u;
-        if (lane == 0u) g = atomicAdd(&w.pool[kPoolBounce + level], 1u);
-        g = __builtin_amdgcn_readfirstlane(g);
-        if (g * 64u >= n) break;
+    // one chunk per wave, the launch sized for the longest list (waves past its end return at
+    // once): the hardware deals the workgroups as slots free up.  Dynamic grabs from one shared
+    // counter serialised (Z1's bounce stage 0.134 -> 0.183 ms); chunks dealt statically to
+    // persistent waves balanced the heavy-tailed walks worse (Z1 serial 3.64 vs 3.41 ms).
+    {
+        const uint32_t g = blockIdx.x * 4u + (threadIdx.x >> 6);
+        if (g * 64u >= n) return;
         const uint32_t i = g * 64u + lane;
         if (i < n) {
             const uint32_t q = live_path(w, level + 1, i);
@@ -1187,23 +1192,15 @@ __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_SHADOW : VPX_WPE_MULTI_S
     shadow_tile<ONE>(sv, w, ctr, nullptr, tile_block() * 256u + threadIdx.x);
 }
 
-// Level l's shadow walks over its live list: persistent workgroups take 256 entries at a time
-// (one atomic per grab) and walk those paths' slots as shadow_tile walks a tile's (counting-
-// sorted by light).  Level 0 (every path) takes the tiles in order.
+// Level l >= 1's shadow walks over its live list: a workgroup takes 256 entries and walks
+// those paths' slots as shadow_tile walks a tile's (counting-sorted by light).
 template <bool ONE>
 __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_SHADOW : VPX_WPE_MULTI_SHADOW) void k_shadow_list(SceneView sv, WaveBufs w, int level,
                                                                                                        unsigned long long* __restrict__ ctr) {
-    __shared__ uint32_t chunk;
     const uint32_t n = live_count(w, level);
-    for (;;) {
-        if (threadIdx.x == 0) chunk = atomicAdd(&w.pool[kPoolShadow + level], 1u);
-        __syncthreads();
-        const uint32_t c = chunk;
-        __syncthreads();  // every thread has read it before the next grab
-        if (c * 256u >= n) break;
-        const uint32_t i = c * 256u + threadIdx.x;
-        shadow_tile<ONE>(sv, w, ctr, nullptr, i < n ? live_path(w, level, i) : ~0u);
-    }
+    if (blockIdx.x * 256u >= n) return;  // one chunk per workgroup (k_nearest_tile)
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    shadow_tile<ONE>(sv, w, ctr, nullptr, i < n ? live_path(w, level, i) : ~0u);
 }
 
 // The shadow pool (single-volume scenes): Renderer::IsOccluded for a level's shadow slots,
@@ -1251,7 +1248,7 @@ __global__ __launch_bounds__(kPoolWg) VPX_WPE(VPX_WPE_SPOOL) void k_shadow_pool(
             if (!idle) break;
             if (avail == 0u) {
                 uint32_t gi = 0u;
-                if (lane == 0u) gi = atomicAdd(&w.pool[kMaxLevels + level], 1u);
+                if (lane == 0u) gi = atomicAdd(&w.pool[kPoolShadow + level], 1u);
                 gi = __builtin_amdgcn_readfirstlane(gi);
                 if (gi >= grabs) {
                     more = false;
@@ -1443,17 +1440,10 @@ __global__ __launch_bounds__(256) VPX_WPE(VPX_WPE_MULTI_SHADOW) void k_shadow_in
         shadow_inst_chunk(sv, w, ctr, vb, tile_block() * 256u + threadIdx.x);
         return;
     }
-    __shared__ uint32_t chunk;
     const uint32_t n = live_count(w, level);
-    for (;;) {
-        if (threadIdx.x == 0) chunk = atomicAdd(&w.pool[kPoolShadow2 + level], 1u);
-        __syncthreads();
-        const uint32_t c = chunk;
-        __syncthreads();
-        if (c * 256u >= n) break;
-        const uint32_t i = c * 256u + threadIdx.x;
-        shadow_inst_chunk(sv, w, ctr, vb, i < n ? live_path(w, level, i) : ~0u);
-    }
+    if (blockIdx.x * 256u >= n) return;  // one chunk per workgroup (k_nearest_tile)
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    shadow_inst_chunk(sv, w, ctr, vb, i < n ? live_path(w, level, i) : ~0u);
 }
 
 // ------------------------------------------------------------------- stage 4

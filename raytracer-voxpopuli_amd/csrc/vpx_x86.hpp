@@ -19,9 +19,9 @@
 #include <stdint.h>
 
 #if defined(__HIPCC__)
-#define VPX_HD __host__ __device__ inline __attribute__((always_inline))
+#define VPX_HDX __host__ __device__ inline __attribute__((always_inline))
 #else
-#define VPX_HD inline
+#define VPX_HDX inline
 #endif
 
 namespace vpx {
@@ -38,7 +38,7 @@ struct X86Arith {
 // rcpss(x) as bits: the table holds rcp(1.m) for the key's mantissas; the exponent moves the
 // result by 2^-(e - 127).  Zero / denormal -> signed infinity, infinity -> signed zero, NaN ->
 // the quieted NaN, results below the normal range -> signed zero (flush).
-VPX_HD uint32_t x86_rcp_bits(uint32_t u, const uint32_t* tab, uint32_t shift) {
+VPX_HDX uint32_t x86_rcp_bits(uint32_t u, const uint32_t* tab, uint32_t shift) {
     const uint32_t s = u & 0x80000000u, e = (u >> 23) & 0xffu, m = u & 0x7fffffu;
     if (e == 0u) return s | 0x7f800000u;
     if (e == 255u) return m ? (u | 0x400000u) : s;
@@ -50,7 +50,7 @@ VPX_HD uint32_t x86_rcp_bits(uint32_t u, const uint32_t* tab, uint32_t shift) {
 // rsqrtss(x) as bits: the table holds rsqrt of [1, 4) (parity 1 = [2, 4)); an even exponent
 // step 2q moves the result by 2^-q.  +-0 / denormals -> signed infinity, negative -> the
 // default NaN, +inf -> +0, NaN -> the quieted NaN.
-VPX_HD uint32_t x86_rsq_bits(uint32_t u, const uint32_t* tab, uint32_t shift) {
+VPX_HDX uint32_t x86_rsq_bits(uint32_t u, const uint32_t* tab, uint32_t shift) {
     const uint32_t e = (u >> 23) & 0xffu, m = u & 0x7fffffu;
     if (e == 0u) return (u & 0x80000000u) | 0x7f800000u;
     if (e == 255u && m) return u | 0x400000u;
