@@ -859,7 +859,11 @@ int launch_render(vpx_ctx* c, hipStream_t s, vpx_ctx::WaveStore& ws, const Scene
         // the whole depth-0 frame in one launch (k_frame0), its path state and one shadow slot
         // per path in LDS; with area lights the frame splits to use the shadow pool
         prof_mark(c, s, VPX_STAGE_FRAME);
-        hipLaunchKernelGGL((k_frame0<true, MODE>), grid, block, slds, s, sv, f, w, c->d_ctr, accum, rgb8, packed);
+#ifndef VPX_FRAME_EXTRA_LDS
+#define VPX_FRAME_EXTRA_LDS 0  // A/B hook: bytes of unused LDS added per k_frame0 workgroup (occupancy sensitivity)
+#endif
+        hipLaunchKernelGGL((k_frame0<true, MODE>), grid, block, slds + VPX_FRAME_EXTRA_LDS, s, sv, f, w, c->d_ctr, accum,
+                           rgb8, packed);
         prof_mark(c, s, -1);
         VPX_HIP(c, hipGetLastError());
         return VPX_OK;

@@ -113,7 +113,46 @@ struct WaveBufs {
 // ... — measured much slower: C2 5.64 vs 2.54 ms, C3 3.93 vs 3.65, C4 49.7 vs 43.1.  The
 // counters share a cache line, so the L2 still serialises them, the tail takes up to 16 atomics
 // per wave, and the frame is no longer swept in order, so the waves' lines are spread further.)
-constexpr uint32_t kPoolLive = 0, kPoolShadow = kMaxLevels, kPoolBounce = 2 * kMaxLevels, kPoolWords = 3 * kMaxLevels;
+// The pools' grab counters: kGrabLines counters per level, each on its own 128-byte line (the
+// L2 serialises atomics per line), counter k dealing chunks k, k + kGrabLines, ...; a wave
+// starts on its own counter and moves to the next when it runs dry, and an exhausted counter
+// sets its bit in the level's mask word (its own line) so that later waves skip it.
+#ifndef VPX_GRAB_LINES
+#define VPX_GRAB_LINES 1
+#endif
+constexpr uint32_t kGrabLines = VPX_GRAB_LINES, kLineWords = 32;
+constexpr uint32_t kGrabBlock = (kGrabLines + 1u) * kLineWords;  // per level: the counters, then the mask
+constexpr uint32_t kPoolLive = 0, kPoolShadow = kLineWords, kPoolBounce = kPoolShadow + kMaxLevels * kGrabBlock,
+                   kPoolWords = kPoolBounce + kMaxLevels * kGrabBlock;
+
+// The next of `chunks` chunks for this wave (wave-uniform; lane 0 takes it), ~0u when none is
+// left.  blk: the level's grab block; line: the wave's current counter (wave-uniform).
+__device__ __forceinline__ uint32_t pool_grab(uint32_t* blk, uint32_t chunks, uint32_t& line) {
+    const bool lead = (threadIdx.x & 63u) == 0u;
+    if (kGrabLines == 1u) {
+        uint32_t g = 0u;
+        if (lead) g = atomicAdd(blk, 1u);
+        g = __builtin_amdgcn_readfirstlane(g);
+        return g < chunks ? g : ~0u;
+    }
+    for (uint32_t t = 0; t < kGrabLines; ++t) {
+        const uint32_t done = __builtin_amdgcn_readfirstlane(
+            __hip_atomic_load(blk + kGrabLines * kLineWords, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        if (!((done >> line) & 1u)) {
+            uint32_t k = 0u;
+            if (lead) k = atomicAdd(blk + line * kLineWords, 1u);
+            k = __builtin_amdgcn_readfirstlane(k);
+            const uint32_t c = line + k * kGrabLines;
+            if (c < chunks) return c;
+            if (lead) atomicOr(blk + kGrabLines * kLineWords, 1u << line);
+        }
+        line = line + 1u == kGrabLines ? 0u : line + 1u;
+    }
+    return ~0u;
+}
+__device__ __forceinline__ uint32_t pool_line0() {
+    return __builtin_amdgcn_readfirstlane((blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) % kGrabLines);
+}
 
 // Level l's paths: level 0 is every path of the launch (p = i); a later level's are the paths
 // that trace a ray there, listed by the previous level's shade (put_live).  Every kernel after
@@ -919,6 +958,9 @@ __global__ __launch_bounds__(256) VPX_WPE(VPX_WPE_MULTI_NEAREST) void k_instance
             const f3 inv = mk(__fdiv_rn(1.0f, d.x), __fdiv_rn(1.0f, d.y), __fdiv_rn(1.0f, d.z));
             go = tlas_box(sv.tlas[0], mk(o.x, o.y, o.z), inv, w.H[p].x);  // conservative (tlas_box)
         }
+#ifdef VPX_DEBUG_NO_INST_WALK
+        go = false;  // timing probe only (wrong images): the pass without its instance walks
+#endif
     }
     uint32_t total;
     const uint32_t at = block_scan(go ? 1u : 0u, total, sh);
@@ -1050,8 +1092,7 @@ constexpr uint32_t kPoolLeave = VPX_POOL_LEAVE;  // finished lanes that end a wa
 constexpr uint32_t kPoolWg = VPX_POOL_WG;        // threads per workgroup (its waves are independent)
 __global__ __launch_bounds__(kPoolWg) VPX_WPE(VPX_WPE_BOUNCE) void k_nearest_pool(SceneView sv, WaveBufs w, int level,
                                                                                unsigned long long* __restrict__ ctr) {
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t n = live_count(w, level + 1);  // the rays level `level`'s shade traced
+        const uint32_t n = live_count(w, level + 1);  // the rays level `level`'s shade traced
     const uint32_t* L = live_list(w, level + 1);
     const PathRay pr{w.O, w.D, w.H, w.HM, 0u};
     const skip::GridView gv = grid_view(sv.grids[uni_ptr(&sv.volumes[0])->grid_id]);
@@ -1061,6 +1102,7 @@ __global__ __launch_bounds__(kPoolWg) VPX_WPE(VPX_WPE_BOUNCE) void k_nearest_poo
     int mode = kWalkMiss;
     uint32_t avail = 0u, cur = 0u;  // grabbed list entries not yet handed out, and where they start
     bool more = true;               // entries may be left in the list
+    uint32_t line = pool_line0();
     for (;;) {
         if (q != ~0u && mode >= kWalkMiss) {  // finished: its hit record
             nearest_end_1v(sv, pr, q, wk, mode == kWalkHit);
@@ -1070,10 +1112,8 @@ __global__ __launch_bounds__(kPoolWg) VPX_WPE(VPX_WPE_BOUNCE) void k_nearest_poo
             const uint64_t idle = __ballot(q == ~0u);
             if (!idle) break;
             if (avail == 0u) {  // the next chunk of the list (every entry traces a ray)
-                uint32_t g = 0u;
-                if (lane == 0u) g = atomicAdd(&w.pool[kPoolBounce + level], 1u);
-                g = __builtin_amdgcn_readfirstlane(g);
-                if (g * kPoolChunk >= n) {
+                const uint32_t g = pool_grab(w.pool + kPoolBounce + level * kGrabBlock, (n + kPoolChunk - 1u) / kPoolChunk, line);
+                if (g == ~0u) {
                     more = false;
                     break;
                 }
@@ -1238,6 +1278,7 @@ __global__ __launch_bounds__(kPoolWg) VPX_WPE(VPX_WPE_SPOOL) void k_shadow_pool(
     int mode = kWalkMiss;
     uint32_t avail = 0u, cur = 0u;
     bool more = true;
+    uint32_t line = pool_line0();
     for (;;) {
         if (e != ~0u && mode >= kWalkMiss) {
             w.occb[(uint64_t)(e >> 27) * w.P + (e & 0x07ffffffu)] = mode == kWalkHit ? 1u : 0u;
@@ -1247,10 +1288,8 @@ __global__ __launch_bounds__(kPoolWg) VPX_WPE(VPX_WPE_SPOOL) void k_shadow_pool(
             const uint64_t idle = __ballot(e == ~0u);
             if (!idle) break;
             if (avail == 0u) {
-                uint32_t gi = 0u;
-                if (lane == 0u) gi = atomicAdd(&w.pool[kPoolShadow + level], 1u);
-                gi = __builtin_amdgcn_readfirstlane(gi);
-                if (gi >= grabs) {
+                const uint32_t gi = pool_grab(w.pool + kPoolShadow + level * kGrabBlock, grabs, line);
+                if (gi == ~0u) {
                     more = false;
                     break;
                 }

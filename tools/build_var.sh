@@ -8,5 +8,5 @@ out=var/lib_$name.so; [ "$name" = ph ] && out=var/ph.so
 mkdir -p var
 C=raytracer-voxpopuli_amd/csrc
 hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fgpu-flush-denormals-to-zero -Wall "$@" \
-  -shared -o $out $C/vpx_kernels.hip $C/vpx_host.cpp -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+  -shared -o $out $C/vpx_kernels.hip $C/vpx_host.cpp $C/vpx_x86_host.cpp -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 echo "built $out"
