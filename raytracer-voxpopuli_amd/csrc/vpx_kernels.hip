@@ -38,6 +38,14 @@ constexpr int kTile = 16;  // 16x16 pixels per tile / 256-thread workgroup
 #ifndef VPX_LEVEL_FORK
 #define VPX_LEVEL_FORK 1  // launch_render: a level's bounce walks beside its shadow walks
 #endif
+// k_tail: frames of at least VPX_TAIL_MIN_DEPTH bounces run their levels from VPX_TAIL_LEVEL on
+// in one launch (0: off).
+#ifndef VPX_TAIL_LEVEL
+#define VPX_TAIL_LEVEL 7
+#endif
+#ifndef VPX_TAIL_MIN_DEPTH
+#define VPX_TAIL_MIN_DEPTH 8
+#endif
 constexpr int kThreads = 256;
 
 // One tile per workgroup.  Several tiles per workgroup with their loads issued together
@@ -917,6 +925,9 @@ int launch_render(vpx_ctx* c, hipStream_t s, vpx_ctx::WaveStore& ws, const Scene
     // 2.50 at 3 without).
     const bool fork = VPX_LEVEL_FORK && f.max_bounces > 0 && !rp && (&ws == &c->wave || (one && c->lanes.size() <= 2));
     if (fork && (rc = ensure_fork(c, ws))) return rc;
+    // deep frames: the levels from tail_from on in one launch (k_tail), then k_finish
+    const int tail_from = (VPX_TAIL_LEVEL > 0 && f.max_bounces >= VPX_TAIL_MIN_DEPTH && !rp) ? VPX_TAIL_LEVEL : -1;
+    bool tailed = false;
     // the last level's shadow -> resolve -> finish as one launch (k_shadow_finish)
     for (int level = 0; level <= f.max_bounces; ++level) {
         if (!(fuse_head && level == 0)) {  // (level >= 1: the head shades level 0)
@@ -946,7 +957,8 @@ int launch_render(vpx_ctx* c, hipStream_t s, vpx_ctx::WaveStore& ws, const Scene
         // the level fork: the next level's bounce walks read only the rays and live list this
         // level's shade and k_compact wrote and write only the hit records, which the shadow
         // walks and the light sums do not touch — so they run beside them on the fork stream
-        const bool forked = fork && level < f.max_bounces;
+        const bool tail_next = level + 1 == tail_from;  // the next levels run in k_tail
+        const bool forked = fork && level < f.max_bounces && !tail_next;
         if (forked) {
             VPX_HIP(c, hipEventRecord(ws.ev_fork, s));
             VPX_HIP(c, hipStreamWaitEvent(ws.fork, ws.ev_fork, 0));
@@ -967,12 +979,21 @@ int launch_render(vpx_ctx* c, hipStream_t s, vpx_ctx::WaveStore& ws, const Scene
         prof_mark(c, s, -1);
         if (forked)
             VPX_HIP(c, hipStreamWaitEvent(s, ws.ev_join, 0));
-        else if (level < f.max_bounces)
+        else if (level < f.max_bounces && !tail_next)
             bounce(s, level);
+        if (tail_next) {
+            WaveBufs wt = w;
+            wt.occb = nullptr;  // k_tail marks occluded slots in their SD words, as the tile kernels do
+            prof_mark(c, s, VPX_STAGE_BOUNCE);
+            hipLaunchKernelGGL(k_tail, grid, block, 0, s, sv, f, wt, level + 1, c->d_ctr);
+            prof_mark(c, s, -1);
+            tailed = true;
+            break;
+        }
     }
     // (fused tail: k_shadow_finish already finished the frame; max_bounces = -1 runs no
     // level, so the finish folds the zero leaf here)
-    const bool finished = fuse_tail && f.max_bounces >= 0;
+    const bool finished = fuse_tail && f.max_bounces >= 0 && !tailed;
     if (!finished) prof_mark(c, s, VPX_STAGE_FINISH);
     if (!rp) {
         if (!finished) hipLaunchKernelGGL((k_finish<MODE>), grid, block, 0, s, f, w, accum, rgb8, packed);

@@ -1587,6 +1587,51 @@ __global__ __launch_bounds__(256) void k_resolve_finish(SceneView sv, FrameArgs 
     finish_path<MODE>(f, w, p, accum, rgb8, packed, &ls);
 }
 
+// The deep levels in one launch (k_tail): from level `level` on, each lane carries one path of
+// the level's live list through every remaining level — its FindNearest, the material switch,
+// IsOccluded for the level's shadow slots, the light sum — until the path ends; k_finish then
+// folds every path.  The same per-path operations as the level kernels (nearest_record,
+// shade_path, shadow, resolve_path), so the same values, RNG order and counts; the levels stop
+// costing a launch, a compaction and the longest walk of each level.  Deep levels hold few
+// paths (Z1 at 1920x1080: 192 k at level 5, 3.7 k at level 14), so the kernel's registers (the
+// whole chain inlined) and low occupancy cost little, while each of those levels cost ~0.2 ms
+// of launches and latency chains in the per-level kernels.
+__global__ __launch_bounds__(256) VPX_WPE(2) void k_tail(SceneView sv, FrameArgs f, WaveBufs w, int level,
+                                                      unsigned long long* __restrict__ ctr) {
+    Counters kn{0u, 0u, 0u}, ks{0u, 0u, 0u}, kh{0u, 0u, 0u};
+    const uint32_t n = live_count(w, level);
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (blockIdx.x * 256u >= n) return;
+    const uint32_t p = i < n ? live_path(w, level, i) : ~0u;
+    const PathRay pr{w.O, w.D, w.H, w.HM, 0u};
+    for (int l = level; p != ~0u; ++l) {
+        {  // Renderer::FindNearest for the ray the previous level's shade traced
+            const float4 o = w.O[p], d = w.D[p];
+            Ray r;
+            r.O = mk(o.x, o.y, o.z);
+            r.D = mk(d.x, d.y, d.z);
+            r.inside = (__float_as_uint(d.w) & kInside) != 0u;
+            nearest_record<kSkipwBounce, kMincBounce, kRunBounce>(sv, pr, p, r, kn);
+        }
+        const bool cont = shade_path(sv, f, w, pr, p, l, kh);
+        const uint32_t slots = w.smask[p] & kSlotBits;
+        for (uint32_t b = slots; b; b &= b - 1u) {  // IsOccluded of each of the level's shadow rays
+            const uint64_t slot = (uint64_t)((uint32_t)__ffs(b) - 1u) * w.P + p;
+            const float4 so = w.SO[slot], sd = w.SD[slot];
+            Ray r;
+            r.O = mk(so.x, so.y, so.z);
+            r.D = mk(sd.x, sd.y, sd.z);
+            r.t = so.w;
+            if (shadow(sv, r, ks)) w.SD[slot].w = __uint_as_float(__float_as_uint(sd.w) | 4u /* kSlotOcc */);
+        }
+        resolve_path(sv, w, p);  // the level's light sum into LB (the slots' SD flags)
+        if (!cont || l >= f.max_bounces) break;
+    }
+    flush_counters(kn, 0u, ctr, VPX_STAGE_BOUNCE);
+    flush_counters(ks, 0u, ctr, VPX_STAGE_SHADOW);
+    flush_counters(kh, 0u, ctr, VPX_STAGE_SHADE);
+}
+
 // The last level's tail in one launch: IsOccluded for the tile's shadow slots, then (after
 // the workgroup barrier, which makes the slots' occluded flags visible to the whole tile)
 // each thread resolves and finishes its own path.  The same per-path operations as
