@@ -214,7 +214,10 @@ def load_library(path=None):
     if not os.path.exists(p):
         raise VpxError(f"{p} is missing: run __graft_entry__.build() (hipcc --offload-arch=gfx950)")
     lib = C.CDLL(p)
+    old_ok = os.environ.get("VPX_LIB_OLD") == "1"  # A/B runs against an earlier build (tools/gpu_ab.sh)
     for name, (res, args) in SIGNATURES.items():
+        if old_ok and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)  # AttributeError = the library does not export the ABI
         fn.restype = res
         fn.argtypes = args

@@ -837,6 +837,7 @@ int launch_render(vpx_ctx* c, hipStream_t s, vpx_ctx::WaveStore& ws, const Scene
     const size_t slds = sizeof(uint32_t) * S * kThreads;
     // single volume, no analytic shapes: the DDA kernels' lean instances
     const bool one = sv.num_volumes == 1 && !(sv.num_spheres | sv.num_triangles);
+    const bool x86 = sv.x86.tab != nullptr;  // the reference-arithmetic instances of the hot kernels
     // the last level's shadow -> resolve -> finish as one launch (k_shadow_finish), except
     // on the static-camera path, whose tail is the reprojection
     const bool fuse_tail = !rp;
@@ -871,8 +872,8 @@ int launch_render(vpx_ctx* c, hipStream_t s, vpx_ctx::WaveStore& ws, const Scene
 #ifndef VPX_FRAME_EXTRA_LDS
 #define VPX_FRAME_EXTRA_LDS 0  // A/B hook: bytes of unused LDS added per k_frame0 workgroup (occupancy sensitivity)
 #endif
-        hipLaunchKernelGGL((k_frame0<true, MODE>), grid, block, slds + VPX_FRAME_EXTRA_LDS, s, sv, f, w, c->d_ctr, accum,
-                           rgb8, packed);
+        hipLaunchKernelGGL((x86 ? k_frame0<true, MODE, true> : k_frame0<true, MODE, false>), grid, block,
+                           slds + VPX_FRAME_EXTRA_LDS, s, sv, f, w, c->d_ctr, accum, rgb8, packed);
         prof_mark(c, s, -1);
         VPX_HIP(c, hipGetLastError());
         return VPX_OK;
@@ -889,12 +890,17 @@ int launch_render(vpx_ctx* c, hipStream_t s, vpx_ctx::WaveStore& ws, const Scene
     // there: they keep the one-launch kernel — Z1 2.61-2.62 vs 2.63 ms split, round 4)
     const bool split = !one && fuse_head && VPX_SPLIT_PRIMARY && !(sv.num_spheres | sv.num_triangles);
     if (split)
-        hipLaunchKernelGGL((k_primary<true, true, true>), grid, block, 0, s, sv, f, w, c->d_ctr);
+        hipLaunchKernelGGL((x86 ? k_primary<true, true, true, true> : k_primary<true, true, true, false>), grid, block, 0, s,
+                           sv, f, w, c->d_ctr);
     else if (fuse_head)
-        hipLaunchKernelGGL((one ? k_primary<true, true> : k_primary<false, true>), grid, block, 0, s, sv, f, w,
+        hipLaunchKernelGGL((one ? (x86 ? k_primary<true, true, false, true> : k_primary<true, true, false, false>)
+                                : (x86 ? k_primary<false, true, false, true> : k_primary<false, true, false, false>)),
+                           grid, block, 0, s, sv, f, w,
                            c->d_ctr);
     else
-        hipLaunchKernelGGL((one ? k_primary<true, false> : k_primary<false, false>), grid, block, 0, s, sv, f,
+        hipLaunchKernelGGL((one ? (x86 ? k_primary<true, false, false, true> : k_primary<true, false, false, false>)
+                                : (x86 ? k_primary<false, false, false, true> : k_primary<false, false, false, false>)),
+                           grid, block, 0, s, sv, f,
                            w, c->d_ctr);
     prof_mark(c, s, -1);
     if (split) {
@@ -911,7 +917,8 @@ int launch_render(vpx_ctx* c, hipStream_t s, vpx_ctx::WaveStore& ws, const Scene
             const uint32_t chunks = (P + kPoolChunk - 1u) / kPoolChunk;
             const uint32_t waves = std::min(chunks, c->cus * 4u * (uint32_t)VPX_WPE_BOUNCE);
             const uint32_t wpb = kPoolWg / 64u;
-            hipLaunchKernelGGL(k_nearest_pool, dim3((waves + wpb - 1u) / wpb), dim3(kPoolWg), 0, bs, sv, w, level,
+            hipLaunchKernelGGL(x86 ? k_nearest_pool<true> : k_nearest_pool<false>, dim3((waves + wpb - 1u) / wpb),
+                               dim3(kPoolWg), 0, bs, sv, w, level,
                                c->d_ctr);
         } else {  // multi-volume / shape scenes: persistent waves over the live list, 64 rays a grab
             hipLaunchKernelGGL(k_nearest_tile, grid, block, 0, bs, sv, w, level, c->d_ctr);

@@ -315,7 +315,9 @@ __device__ __forceinline__ float fast_reciprocal1(float x, const X86Arith& xa) {
     return (r + r) - muls;
 }
 __device__ __forceinline__ f3 nearest_rd(f3 d, const X86Arith& xa) {
+#ifndef VPX_NO_X86
     if (xa.tab) return mk(fast_reciprocal1(d.x, xa), fast_reciprocal1(d.y, xa), fast_reciprocal1(d.z, xa));
+#endif
     return mk(__fdiv_rn(1.0f, d.x), __fdiv_rn(1.0f, d.y), __fdiv_rn(1.0f, d.z));
 }
 

@@ -156,6 +156,16 @@ __device__ __forceinline__ uint32_t pool_line0() {
     return __builtin_amdgcn_readfirstlane((blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) % kGrabLines);
 }
 
+// The scene view a kernel instance works with: X86 = false drops the reference-arithmetic
+// tables (a constant null tab, so the exact arithmetic is inlined without its runtime branch:
+// the branch cost C1 1.2 %, 0.5527-0.5563 vs 0.5445-0.5477 ms); X86 = true keeps them.
+template <bool X86>
+__device__ __forceinline__ SceneView arith_view(const SceneView& sv) {
+    SceneView v = sv;
+    if (!X86) v.x86.tab = nullptr;
+    return v;
+}
+
 // Level l's paths: level 0 is every path of the launch (p = i); a later level's are the paths
 // that trace a ray there, listed by the previous level's shade (put_live).  Every kernel after
 // level 0's head walks / shades / resolves the list, so a level costs its live paths — Z1's
@@ -186,7 +196,11 @@ __device__ __forceinline__ Ray primary_make_ray(f3 o, f3 dir, const X86Arith& xa
     return r;
 }
 __device__ __forceinline__ Ray primary_ray(const FrameArgs& f, uint32_t x, uint32_t y, Rng& g, const X86Arith& xa) {
+#ifndef VPX_NO_X86
     const bool x86 = xa.tab && !(f.flags & kFlagReproject);
+#else
+    const bool x86 = false;
+#endif
     float fx = (float)x, fy = (float)y;
     if (f.flags & VPX_FLAG_AA) {
         const float rx = g.next(), ry = g.next();
@@ -954,11 +968,11 @@ __device__ __forceinline__ void primary_tile(const SceneView& sv, const FrameArg
     }
 }
 
-template <bool ONE, bool SHADE = false, bool SPLIT = false>
+template <bool ONE, bool SHADE = false, bool SPLIT = false, bool X86 = false>
 __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_NEAREST : VPX_WPE_MULTI_NEAREST) void k_primary(SceneView sv, FrameArgs f, WaveBufs w,
                                                  unsigned long long* __restrict__ ctr) {
     __shared__ HeadLds<SHADE> L;
-    primary_tile<ONE, SHADE, SPLIT>(sv, f, w, L, ctr);
+    primary_tile<ONE, SHADE, SPLIT>(arith_view<X86>(sv), f, w, L, ctr);
 }
 
 // Multi-volume primary rays in two launches: the world (volume 0, first in the reference's
@@ -1128,8 +1142,10 @@ __global__ __launch_bounds__(256) VPX_WPE(VPX_WPE_MULTI_NEAREST) void k_nearest_
 constexpr uint32_t kPoolChunk = VPX_POOL_CHUNK;  // list entries (traced rays) per grab
 constexpr uint32_t kPoolLeave = VPX_POOL_LEAVE;  // finished lanes that end a walk while rays are left
 constexpr uint32_t kPoolWg = VPX_POOL_WG;        // threads per workgroup (its waves are independent)
-__global__ __launch_bounds__(kPoolWg) VPX_WPE(VPX_WPE_BOUNCE) void k_nearest_pool(SceneView sv, WaveBufs w, int level,
+template <bool X86>
+__global__ __launch_bounds__(kPoolWg) VPX_WPE(VPX_WPE_BOUNCE) void k_nearest_pool(SceneView sv_, WaveBufs w, int level,
                                                                                unsigned long long* __restrict__ ctr) {
+    const SceneView sv = arith_view<X86>(sv_);
         const uint32_t n = live_count(w, level + 1);  // the rays level `level`'s shade traced
     const uint32_t* L = live_list(w, level + 1);
     const PathRay pr{w.O, w.D, w.H, w.HM, 0u};
@@ -1729,10 +1745,11 @@ constexpr uint32_t kFuseFrameTiles = VPX_FUSE_FRAME_TILES;
 // records, forms the walker list (dead after the walks' barrier).  The tile's WaveBufs view
 // points those arrays at LDS, shifted by the tile's first path so that path p indexes them
 // as p (level 0 and slot 0 only: every index is p).  HBM sees the accumulator / screen.
-template <bool ONE, int MODE>
+template <bool ONE, int MODE, bool X86 = false>
 __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_FRAME : VPX_WPE_MULTI_NEAREST) void k_frame0(
-    SceneView sv, FrameArgs f, WaveBufs w, unsigned long long* __restrict__ ctr, float4* __restrict__ accum,
+    SceneView sv_, FrameArgs f, WaveBufs w, unsigned long long* __restrict__ ctr, float4* __restrict__ accum,
     uint32_t* __restrict__ rgb8, float4* __restrict__ packed) {
+    const SceneView sv = arith_view<X86>(sv_);
     __shared__ HeadLds<true> L;
     __shared__ float4 s_val[256];  // LA (a) or leaf of the path's one level
     __shared__ float4 s_sm[256];   // SM: the pending light
@@ -1750,9 +1767,13 @@ __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_FRAME : VPX_WPE_MULTI_NE
     wl.SL = L.ray + 512 - tb;
     primary_tile<ONE, true>(sv, f, wl, L, ctr);
     __syncthreads();
+#ifdef VPX_FRAME_P_TILE
+    shadow_tile<ONE, kRunShadow>(sv, wl, ctr, occ, tile_block() * 256u + threadIdx.x);
+#else
     uint32_t ps = p;  // re-derived, not kept live across the head (as pt below)
     asm volatile("" : "+v"(ps));
     shadow_tile<ONE, kRunShadow>(sv, wl, ctr, occ, ps);
+#endif
     __syncthreads();
     // the tail's own copy of p: the shade's per-lane LDS addresses are re-derived here
     // instead of being kept live (spilled) across the shadow walks

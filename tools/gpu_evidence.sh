@@ -10,7 +10,7 @@
 set -u
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out/ev
 export TMPDIR=/tmp
-TAG=${TAG:-r04}
+TAG=${TAG:-r05}
 O=gpurun_out/ev
 step() { name=$1; shift; echo "== $name"; timeout -k 10 "$@" > $O/$name.log 2>&1; rc=$?; echo "$name rc=$rc"; grep -v amdgpu.ids $O/$name.log | tail -${TAILN:-2} | cut -c1-300; if [ $rc -ne 0 ]; then exit $rc; fi; }
 sha256sum raytracer-voxpopuli_amd/libvpx_hip.so | tee $O/lib.sha256
