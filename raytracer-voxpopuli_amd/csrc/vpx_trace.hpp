@@ -422,7 +422,10 @@ __device__ __forceinline__ skip::Walk to_walk(const Dda& s) {
 constexpr uint32_t kSkipwNearest = 1, kSkipwBounce = 2, kSkipwShadow = 4;
 // Smallest distance-field cube worth a skip per walk kind (C1, ms: FindNearest 0.430 with
 // 2 / 0.435 with 1; IsOccluded 0.383 with 2 / 0.354 with 1).
-constexpr uint32_t kMincNearest = 2, kMincBounce = 2, kMincShadow = 1;
+#ifndef VPX_MINC_NEAREST
+#define VPX_MINC_NEAREST 2
+#endif
+constexpr uint32_t kMincNearest = VPX_MINC_NEAREST, kMincBounce = 2, kMincShadow = 1;
 // Brick runs per walk kind, the RUN word: cap | passes << 8 | seg2 << 17 | min2 << 18.
 // After its octant-plane byte (and, in an occupied brick, its cell mask) loads, a lane
 // steps up to `cap` cells inside its 4^3 brick on the register copy; `passes` brick loads
@@ -442,9 +445,24 @@ constexpr uint32_t kMincNearest = 2, kMincBounce = 2, kMincShadow = 1;
 // words instead of the octant plane, a branch-free select-committed step, loading two
 // cells' words per round trip, prefetching the exit brick's byte, speculative cell-mask
 // loads after an occupied brick, walk continuations with a step budget.
-constexpr uint32_t kRunNearest = 3u | 2u << 8 | 1u << 17 | 1u << 18;
+#ifndef VPX_RUN_NEAREST
+#define VPX_RUN_NEAREST (3u | 3u << 8 | 1u << 17 | 1u << 18)
+#endif
+constexpr uint32_t kRunNearest = VPX_RUN_NEAREST;
 constexpr uint32_t kRunBounce = 4u | 1u << 8 | 0u << 17 | 1u << 18;
-constexpr uint32_t kRunShadow = 3u | 1u << 8 | 1u << 17 | 0u << 18;
+#ifndef VPX_RUN_SHADOW
+#define VPX_RUN_SHADOW (3u | 1u << 8 | 1u << 17 | 0u << 18)
+#endif
+constexpr uint32_t kRunShadow = VPX_RUN_SHADOW;
+// Round 5 (ms per step, three interleaved runs, tools/gpu_ab.sh): FindNearest runs of 3 cells in
+// three passes instead of two, C1 0.5419-0.5446 vs 0.5491-0.5496, C3 3.57 either way (four
+// passes 0.5424-0.5459; runs of 4 in three passes 0.5462-0.5497); k_frame0's shadow walks in two
+// passes on top, C1 0.5413-0.5431 (its own word: the other shadow walkers with two passes, C2
+// 2.466-2.480 vs 2.427-2.452).
+#ifndef VPX_RUN_FRAME_SHADOW
+#define VPX_RUN_FRAME_SHADOW (3u | 2u << 8 | 1u << 17 | 0u << 18)
+#endif
+constexpr uint32_t kRunFrameShadow = VPX_RUN_FRAME_SHADOW;
 // The pools' walks (k_nearest_pool, k_shadow_pool: 96 VGPRs at 5 waves/SIMD) have their own
 // words (A/B overrides: VPX_*_POOL).  With the pool's registers the shadow walks take the
 // two-compare step without spilling: C3 3.684-3.719 vs 3.724-3.756 ms (three interleaved runs,

@@ -1768,11 +1768,11 @@ __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_FRAME : VPX_WPE_MULTI_NE
     primary_tile<ONE, true>(sv, f, wl, L, ctr);
     __syncthreads();
 #ifdef VPX_FRAME_P_TILE
-    shadow_tile<ONE, kRunShadow>(sv, wl, ctr, occ, tile_block() * 256u + threadIdx.x);
+    shadow_tile<ONE, kRunFrameShadow>(sv, wl, ctr, occ, tile_block() * 256u + threadIdx.x);
 #else
     uint32_t ps = p;  // re-derived, not kept live across the head (as pt below)
     asm volatile("" : "+v"(ps));
-    shadow_tile<ONE, kRunShadow>(sv, wl, ctr, occ, ps);
+    shadow_tile<ONE, kRunFrameShadow>(sv, wl, ctr, occ, ps);
 #endif
     __syncthreads();
     // the tail's own copy of p: the shade's per-lane LDS addresses are re-derived here
