@@ -40,6 +40,9 @@ constexpr int kTile = 16;  // 16x16 pixels per tile / 256-thread workgroup
 #endif
 // k_tail: frames of at least VPX_TAIL_MIN_DEPTH bounces run their levels from VPX_TAIL_LEVEL on
 // in one launch (0: off).
+#ifndef VPX_LANE_DOUBLE
+#define VPX_LANE_DOUBLE 1  // frames in flight: two sample buffers per lane (lane_render)
+#endif
 #ifndef VPX_TAIL_LEVEL
 #define VPX_TAIL_LEVEL 7
 #endif
@@ -506,8 +509,13 @@ struct vpx_ctx {
         hipStream_t s = nullptr;
         WaveStore ws;
         float4* packed = nullptr;  // the lane's frame: one float4 sample per path (tile order)
+        float4* packed2 = nullptr; // its second buffer (frames alternate: VPX_LANE_DOUBLE)
         size_t packed_len = 0;
-        hipEvent_t rendered = nullptr, consumed = nullptr;
+        hipEvent_t rendered = nullptr, consumed = nullptr, consumed2 = nullptr;
+        bool used2 = false;
+        uint32_t flip = 0;
+        float4* cur = nullptr;             // the buffer of the lane's latest frame (lane_render)
+        hipEvent_t cur_consumed = nullptr; // the event its blend records
         hipEvent_t caller = nullptr;  // the caller's stream at the frame's vpx_render (lane_tail_ok frames)
         bool used = false;
         bool dedicated = false;  // on a CU-mask stream (its own hardware queue), counted in g_lane_queues
@@ -1039,25 +1047,36 @@ int lane_render(vpx_ctx* c, const SceneView& sv, const FrameArgs& f, uint32_t ti
     vpx_ctx::Lane& L = c->lanes[c->lane_next];
     c->lane_next = (c->lane_next + 1u) % (uint32_t)c->lanes.size();
     float4* dst = out;
+    // Two sample buffers per lane, alternating: the lane's next frame waits only for the blend
+    // of the frame before its previous one, not for the previous one's (which waits for every
+    // earlier blend on the caller's stream).  The path state needs no wait: the lane's frames
+    // run in its stream's order, and the blends read only the samples.
+    const uint32_t b = L.flip;
+    L.flip = VPX_LANE_DOUBLE ? L.flip ^ 1u : 0u;
     if (!dst) {
         const size_t need = (size_t)tiles * kTilePix;
         if (L.packed_len < need) {
             VPX_HIP(c, sync_all(c));
             if (L.packed) (void)hipFree(L.packed);
-            L.packed = nullptr;
+            if (L.packed2) (void)hipFree(L.packed2);
+            L.packed = L.packed2 = nullptr;
             L.packed_len = 0;
             VPX_HIP(c, hipMalloc(&L.packed, sizeof(float4) * need));
+            if (VPX_LANE_DOUBLE) VPX_HIP(c, hipMalloc(&L.packed2, sizeof(float4) * need));
             L.packed_len = need;
         }
-        dst = L.packed;
+        dst = b ? L.packed2 : L.packed;
     }
-    // the lane's samples / path state are reused: the composite of its previous frame is done
-    if (L.used) VPX_HIP(c, hipStreamWaitEvent(L.s, L.consumed, 0));
+    bool& used = b ? L.used2 : L.used;
+    L.cur = dst;
+    L.cur_consumed = b ? L.consumed2 : L.consumed;
+    // this buffer's previous frame has been blended
+    if (used) VPX_HIP(c, hipStreamWaitEvent(L.s, L.cur_consumed, 0));
     int rc = launch_render<kFinishPackedSample>(c, L.s, L.ws, sv, f, tiles, nullptr, nullptr, dst);
     if (rc) return rc;
     VPX_HIP(c, hipEventRecord(L.rendered, L.s));
     VPX_HIP(c, hipStreamWaitEvent(c->stream, L.rendered, 0));
-    L.used = true;
+    used = true;
     lane = &L;
     return VPX_OK;
 }
@@ -1074,8 +1093,10 @@ void free_lanes(vpx_ctx* c) {
         free_fork(L.ws);
         if (L.ws.d) (void)hipFree(L.ws.d);
         if (L.packed) (void)hipFree(L.packed);
+        if (L.packed2) (void)hipFree(L.packed2);
         if (L.rendered) (void)hipEventDestroy(L.rendered);
         if (L.consumed) (void)hipEventDestroy(L.consumed);
+        if (L.consumed2) (void)hipEventDestroy(L.consumed2);
         if (L.caller) (void)hipEventDestroy(L.caller);
         if (L.s) (void)hipStreamDestroy(L.s);
     }
@@ -1234,6 +1255,7 @@ int vpx_set_pipeline(vpx_ctx* c, uint32_t depth) {
         if (se != hipSuccess ||
             hipEventCreateWithFlags(&L.rendered, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&L.consumed, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&L.consumed2, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&L.caller, hipEventDisableTiming) != hipSuccess) {
             free_lanes(c);
             return fail(c, VPX_E_DEVICE, "pipeline lane stream / events");
@@ -1771,10 +1793,10 @@ int vpx_render(vpx_ctx* c, const vpx_frame_params* p, float* accum, uint32_t* rg
         // caller's stream after the previous frame's (the same blend of the same sample)
         vpx_ctx::Lane* L = nullptr;
         if ((rc = lane_render(c, sv, f, f.num_tiles, nullptr, L))) return rc;
-        hipLaunchKernelGGL(composite_tiles, dim3(f.num_tiles), dim3(kThreads), 0, c->stream, f, L->packed,
+        hipLaunchKernelGGL(composite_tiles, dim3(f.num_tiles), dim3(kThreads), 0, c->stream, f, L->cur,
                            reinterpret_cast<float4*>(accum), rgb8);
         VPX_HIP(c, hipGetLastError());
-        VPX_HIP(c, hipEventRecord(L->consumed, c->stream));
+        VPX_HIP(c, hipEventRecord(L->cur_consumed, c->stream));
         return VPX_OK;
     }
     unsigned long long before[kCtrWords] = {};
@@ -1870,10 +1892,10 @@ static int render_tiles_impl(int MODE, vpx_ctx* c, const vpx_frame_params* p, ui
         vpx_ctx::Lane* L = nullptr;
         if ((rc = lane_render(c, sv, f, f.tiles_per_rank, nullptr, L))) return rc;
         const uint32_t P = f.tiles_per_rank * (uint32_t)kTilePix;  // this rank's running average, in frame order
-        hipLaunchKernelGGL(blend_packed, dim3(f.tiles_per_rank), dim3(kThreads), 0, c->stream, f, L->packed, accum, rgb8,
+        hipLaunchKernelGGL(blend_packed, dim3(f.tiles_per_rank), dim3(kThreads), 0, c->stream, f, L->cur, accum, rgb8,
                            P);
         VPX_HIP(c, hipGetLastError());
-        VPX_HIP(c, hipEventRecord(L->consumed, c->stream));
+        VPX_HIP(c, hipEventRecord(L->cur_consumed, c->stream));
         return VPX_OK;
     }
     unsigned long long before[kCtrWords] = {};
