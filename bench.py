@@ -65,6 +65,11 @@ EXTRA_CONFIGS = ("C2", "C3", "C4", "Z1")
 # as the first config (2.70 either way as an extra after C1).  Round-4 build (tools/gpu_r4m.sh,
 # 2 / 3 / 4 lanes): C1 0.553-0.557 / 0.555-0.556 / 0.586-0.587, C4 45.0-45.1 / 43.2-43.5 / 44.5-44.8.
 PIPELINE = {"C1": 3, "C2": 2, "C3": 3, "C4": 3, "Z1": 3}
+# A rank's share of a multi-GPU frame is a small launch: with each lane's two sample buffers
+# (round 5) four lanes keep more of it in flight for the big frames (rank 0's share at R = 8,
+# tools/rank_share.py, 3 / 4 lanes: C3 0.586 / 0.564 ms, C4 9.93 / 8.63 ms per 16-spp step;
+# C1 0.091 / 0.100 ms stays at 3; one GPU: C3 3.55 / 3.59 ms).
+PIPELINE_MULTI = {"C3": 4, "C4": 4}
 STAGE_KERNELS = {"primary": "k_primary", "shade": "k_shade", "shadow": "k_shadow_tile", "resolve": "k_resolve",
                  "bounce": "k_nearest_tile", "finish": "k_finish", "frame": "k_frame0", "instances": "k_instances"}
 
@@ -207,7 +212,7 @@ def run_config(pkg, env, cfg, steps, warmup, weak=False, sha=None, pipeline=None
     if arith:
         ctx.set_arithmetic(arith)
     if pipeline is None:
-        pipeline = PIPELINE.get(cfg, 0)
+        pipeline = PIPELINE_MULTI.get(cfg, PIPELINE.get(cfg, 0)) if env.n >= 4 else PIPELINE.get(cfg, 0)
     ctx.set_pipeline(pipeline)
     torch.cuda.synchronize()
     acc = rgb = sharded = None

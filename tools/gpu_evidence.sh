@@ -21,9 +21,10 @@ if [ "${PART:-1}" = 1 ]; then
     steps=10; [ $c = C4 ] && steps=3
     step prof_$c 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/$O/prof_$c" -o run -- python bench.py --config $c --steps $steps --warmup 2 --no-cpu --no-extra
   done
-  for c in C1 C3; do
-    step share_$c 300 env CFG=$c PIPE=3 python tools/rank_share.py
-  done
+  step share_C1 300 env CFG=C1 PIPE=3 python tools/rank_share.py
+  step share_C3 300 env CFG=C3 PIPE=3 python tools/rank_share.py
+  step share_C3p4 300 env CFG=C3 PIPE=4 python tools/rank_share.py
+  step share_C4p4 600 env CFG=C4 PIPE=4 K=5 python tools/rank_share.py
 else
   declare -A WH=([C1]="1920 1080" [C2]="1920 1080" [C3]="3840 2160" [C4]="3840 2160" [Z1]="1920 1080")
   for c in ${PMC_CFGS:-C1 C2 C3 C4 Z1}; do
