@@ -729,8 +729,8 @@ int validate_frame(vpx_ctx* c, const vpx_frame_params* p) {
 int ensure_wave(vpx_ctx* c, vpx_ctx::WaveStore& ws, uint32_t P, uint32_t L, uint32_t S) {
     const size_t f4 = sizeof(float4);
     const size_t bytes = (size_t)P * (f4 * (5 + 2 * (size_t)L + 3 * (size_t)S + 1) + 3 * sizeof(uint32_t)) +
-                         sizeof(uint32_t) * (size_t)P * 3 + (size_t)P / 4 + sizeof(uint32_t) * kPoolWords +
-                         (size_t)P * S + 22 * 256;
+                         sizeof(uint32_t) * (size_t)P * 3 + (size_t)P / 8 + sizeof(uint32_t) * kPoolWords +
+                         (size_t)P * S + 21 * 256;
     if (bytes > ws.bytes) {
         if (ws.d) {
             VPX_HIP(c, sync_all(c));
@@ -767,7 +767,6 @@ int ensure_wave(vpx_ctx* c, vpx_ctx::WaveStore& ws, uint32_t P, uint32_t L, uint
     w.live0 = (uint32_t*)take(4 * (size_t)P);
     w.live1 = (uint32_t*)take(4 * (size_t)P);
     w.amask = (uint64_t*)take((size_t)P / 8);  // P is a multiple of 256
-    w.cmask = (uint64_t*)take((size_t)P / 8);
     w.pool = (uint32_t*)take(sizeof(uint32_t) * kPoolWords);
     w.occb = (uint8_t*)take((size_t)P * S);
     return VPX_OK;
@@ -898,21 +897,20 @@ int launch_render(vpx_ctx* c, hipStream_t s, vpx_ctx::WaveStore& ws, const Scene
     // there: they keep the one-launch kernel — Z1 2.61-2.62 vs 2.63 ms split, round 4)
     const bool split = !one && fuse_head && VPX_SPLIT_PRIMARY && !(sv.num_spheres | sv.num_triangles);
     if (split)
-        hipLaunchKernelGGL((x86 ? k_primary<true, true, true, true> : k_primary<true, true, true, false>), grid, block, 0, s,
-                           sv, f, w, c->d_ctr);
+        hipLaunchKernelGGL((x86 ? k_primary<true, false, true> : k_primary<true, false, false>), grid, block, 0, s, sv, f, w,
+                           c->d_ctr);
     else if (fuse_head)
-        hipLaunchKernelGGL((one ? (x86 ? k_primary<true, true, false, true> : k_primary<true, true, false, false>)
-                                : (x86 ? k_primary<false, true, false, true> : k_primary<false, true, false, false>)),
+        hipLaunchKernelGGL((one ? (x86 ? k_primary<true, true, true> : k_primary<true, true, false>)
+                                : (x86 ? k_primary<false, true, true> : k_primary<false, true, false>)),
                            grid, block, 0, s, sv, f, w,
                            c->d_ctr);
     else
-        hipLaunchKernelGGL((one ? (x86 ? k_primary<true, false, false, true> : k_primary<true, false, false, false>)
-                                : (x86 ? k_primary<false, false, false, true> : k_primary<false, false, false, false>)),
+        hipLaunchKernelGGL((one ? (x86 ? k_primary<true, false, true> : k_primary<true, false, false>)
+                                : (x86 ? k_primary<false, false, true> : k_primary<false, false, false>)),
                            grid, block, 0, s, sv, f,
                            w, c->d_ctr);
     prof_mark(c, s, -1);
     if (split) {
-        hipLaunchKernelGGL(k_compact_cand, dim3((P / 64u + 255u) / 256u), block, 0, s, w);
         prof_mark(c, s, VPX_STAGE_INSTANCES);
         hipLaunchKernelGGL(k_instances, grid, block, 0, s, sv, f, w, c->d_ctr);
         prof_mark(c, s, -1);

@@ -99,8 +99,6 @@ struct WaveBufs {
     uint32_t* live1;  //     live{l & 1}[0 .. pool[kPoolLive + l]) (k_compact after level l - 1's shade)
     uint64_t* amask;  // [P/64] bit i of word i >> 6: the path at list position i of the level being
                       // shaded (level 0: path i) traces a next ray (the shades write it, k_compact reads it)
-    uint64_t* cmask;  // [P/64] multi-volume split head: bit p = path p's ray can still meet an instance
-                      // (k_instances' candidates, listed in live0 by k_compact_to)
     uint32_t* pool;   // [kPoolWords] the level counters (kPool*), zeroed at the start of every frame that
                       // uses them (launch_render)
     uint8_t* occb;    // [S][P] the shadow pool's result per slot: 1 = occluded (valid slots only)
@@ -851,18 +849,6 @@ __device__ __forceinline__ void nearest_end_v(const vpx_volume& vol, const uint8
 // The head's LDS: the compacted walker list, and with SHADE the tile's rays (O, D, H) and hit
 // records.  Declared by the kernel, so that k_frame0 can hand the regions on to its tail once
 // the head is done with them.
-// Whether path p's world-walked ray can still meet a later volume or a shape in
-// Renderer::FindNearest's loop: the TLAS root box within the segment [0, world t]
-// (conservative, tlas_box), or always with shapes, instances outside the tree or no TLAS.
-__device__ __forceinline__ bool instance_candidate(const SceneView& sv, const PathRay& pr, uint32_t p) {
-    const float4 d = pr.D[pr.at(p)];
-    if (!(__float_as_uint(d.w) & kActive)) return false;
-    if (!(sv.tlas_on && !sv.tlas_always && !(sv.num_spheres | sv.num_triangles) && sv.tlas_nodes)) return true;
-    const float4 o = pr.O[pr.at(p)];
-    const f3 inv = mk(__fdiv_rn(1.0f, d.x), __fdiv_rn(1.0f, d.y), __fdiv_rn(1.0f, d.z));
-    return tlas_box(sv.tlas[0], mk(o.x, o.y, o.z), inv, pr.H[pr.at(p)].x);
-}
-
 template <bool SHADE>
 struct HeadLds {
     uint32_t sh[4];
@@ -871,11 +857,7 @@ struct HeadLds {
     uint32_t hm[SHADE ? 256 : 1];
 };
 
-// SPLIT (multi-volume scenes, with SHADE): the head walks the world (volume 0) only; a path
-// whose ray can still meet an instance (instance_candidate) goes to k_instances — its ray and
-// hit record to HBM, its bit in cmask — and every other path is final and shaded here, from
-// the LDS records.
-template <bool ONE, bool SHADE, bool SPLIT = false>
+template <bool ONE, bool SHADE>
 __device__ __forceinline__ void primary_tile(const SceneView& sv, const FrameArgs& f, const WaveBufs& w,
                                              HeadLds<SHADE>& L, unsigned long long* __restrict__ ctr) {
     uint32_t* sh = L.sh;
@@ -950,73 +932,17 @@ __device__ __forceinline__ void primary_tile(const SceneView& sv, const FrameArg
     if (SHADE) {  // level 0's material switch for this thread's own path (k_primary_shade)
         __syncthreads();  // the tile's hit records, written by the compacted walkers
         Counters ks{0u, 0u, 0u};
-        bool cand = false;
-        if (SPLIT) {
-            cand = p < w.P && instance_candidate(sv, pr, p);
-            const uint64_t b = __ballot(cand);
-            if ((threadIdx.x & 63u) == 0 && p < w.P) w.cmask[p >> 6] = b;
-            if (cand) {  // k_instances continues FindNearest and shades it
-                w.O[p] = pr.O[pr.at(p)];
-                w.D[p] = pr.D[pr.at(p)];
-                w.H[p] = pr.H[pr.at(p)];
-                w.HM[p] = pr.HM[pr.at(p)];
-            }
-        }
-        const bool cont = shade_path<true>(sv, f, w, pr, cand ? ~0u : p, 0, ks);
+        const bool cont = shade_path<true>(sv, f, w, pr, p, 0, ks);
         if (f.max_bounces > 0) put_amask(w, p, cont);
         flush_counters(ks, 0u, ctr, VPX_STAGE_SHADE);
     }
 }
 
-template <bool ONE, bool SHADE = false, bool SPLIT = false, bool X86 = false>
+template <bool ONE, bool SHADE = false, bool X86 = false>
 __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_NEAREST : VPX_WPE_MULTI_NEAREST) void k_primary(SceneView sv, FrameArgs f, WaveBufs w,
                                                  unsigned long long* __restrict__ ctr) {
     __shared__ HeadLds<SHADE> L;
-    primary_tile<ONE, SHADE, SPLIT>(arith_view<X86>(sv), f, w, L, ctr);
-}
-
-// Multi-volume primary rays in two launches: the world (volume 0, first in the reference's
-// loop) walked by the lean single-volume head (k_primary<true, true, true>: 6 waves/SIMD), which
-// shades at once the paths that can no longer meet a later volume (instance_candidate: the
-// TLAS root box within the segment [0, world t]) from its LDS records and lists the others
-// (cmask -> k_compact_cand -> live0); then this instance pass over that list, 256 candidates a
-// workgroup: Renderer::FindNearest continued from volume 1 (find_nearest_rest: the same
-// candidates, order, bounds and counts as the one-launch loop), then their level-0 shade.
-// The one-launch kernel (k_primary<false, true>) carried the whole volume loop's state through
-// the world walk (112 VGPRs, 72 spilled SGPRs, 4 waves/SIMD), and every ray of the frame
-// through the instance loop: C4's primary stage took 1.46 ms against 0.59 ms for the world
-// alone (tools/c4_split.py).  Until round 4 this pass took every path of its tile, re-read their
-// rays and hits from HBM and shaded all of them at 4 waves/SIMD (137 B/pixel of HBM traffic).
-__global__ __launch_bounds__(256) VPX_WPE(VPX_WPE_MULTI_NEAREST) void k_instances(SceneView sv, FrameArgs f, WaveBufs w,
-                                                                                unsigned long long* __restrict__ ctr) {
-    const uint32_t n = w.pool[kPoolLive];  // the candidates the head listed (k_compact_to into live0)
-    if (blockIdx.x * 256u >= n) return;
-    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-    const uint32_t q = i < n ? w.live0[i] : ~0u;
-    const PathRay pr{w.O, w.D, w.H, w.HM, 0u};
-    Counters k{0u, 0u, 0u};
-    if (q != ~0u) {
-        const float4 o = w.O[q], d = w.D[q], h = w.H[q];
-        const uint32_t hm = w.HM[q];
-        Ray r;
-        r.O = mk(o.x, o.y, o.z);
-        r.D = mk(d.x, d.y, d.z);
-        r.t = h.x;
-        r.N = mk(h.y, h.z, h.w);
-        r.mat = hm & 0xffu;
-        r.inside = (hm & 0x80000000u) != 0u;
-        int32_t vox = (int32_t)((hm >> 8) & 0xffffu) - 2;
-        if (find_nearest_rest(sv, r, k, &vox)) {
-            w.H[q] = make_float4(r.t, r.N.x, r.N.y, r.N.z);
-            w.HM[q] = r.mat | ((uint32_t)(vox + 2) << 8) | (r.inside ? 0x80000000u : 0u);
-        }
-    }
-    flush_counters(k, 0u, ctr, VPX_STAGE_INSTANCES);
-    Counters ks{0u, 0u, 0u};
-    const bool cont = shade_path<true>(sv, f, w, pr, q, 0, ks);
-    // level 1's bit of a candidate (the head's ballot left it clear)
-    if (f.max_bounces > 0 && cont) atomicOr((unsigned long long*)&w.amask[q >> 6], 1ull << (q & 63u));
-    flush_counters(ks, 0u, ctr, VPX_STAGE_SHADE);
+    primary_tile<ONE, SHADE>(arith_view<X86>(sv), f, w, L, ctr);
 }
 
 // Level l + 1's live list from level l's shade bits: 256 mask words (16 k list positions) per
@@ -1052,28 +978,69 @@ __global__ __launch_bounds__(256) void k_compact(WaveBufs w, int level) {
     }
 }
 
-// k_instances' candidate list: the head's cmask bits (path-indexed) into live0, its length at
-// pool[kPoolLive] (level 0's slot, unused: level 0 is every path).  As k_compact.
-__global__ __launch_bounds__(256) void k_compact_cand(WaveBufs w) {
+// Multi-volume primary rays in two launches: the world (volume 0, first in the reference's
+// loop) walked by the lean single-volume head (k_primary<true, false>: 6 waves/SIMD, no
+// spills) writing the hit records to HBM, then this instance pass: per tile, the paths whose
+// ray can still meet a later volume or a shape — the TLAS root box within the ray's segment
+// [0, world t], or every active path when there are shapes, instances outside the tree or no
+// TLAS — compacted into the first waves, Renderer::FindNearest continued from volume 1
+// (find_nearest_rest: the same candidates, order, bounds and counts as the one-launch loop),
+// then level 0's shade for every path of the tile.  The one-launch kernel
+// (k_primary<false, true>) carried the whole volume loop's state through the world walk (112
+// VGPRs, 72 spilled SGPRs, 4 waves/SIMD), and every ray of the frame through the instance
+// loop: C4's primary stage took 1.46 ms against 0.59 ms for the world alone (tools/c4_split.py).
+// Round 5, rejected: the head shading the paths that cannot meet an instance from its LDS
+// records and this pass walking and shading only a dense list of the others — C4 43.27-43.35
+// vs 42.90-43.09 ms per step (three interleaved runs): most C4 rays are candidates, and the
+// pass's HBM traffic is mostly the shade's three area-light slots per pixel (144 B), which the
+// shadow pool reads back, not the rays it re-reads.
+__global__ __launch_bounds__(256) VPX_WPE(VPX_WPE_MULTI_NEAREST) void k_instances(SceneView sv, FrameArgs f, WaveBufs w,
+                                                                                unsigned long long* __restrict__ ctr) {
     __shared__ uint32_t sh[4];
-    __shared__ uint32_t base_s;
-    const uint32_t words = w.P >> 6;
-    if (blockIdx.x * 256u >= words) return;
-    const uint32_t wi = blockIdx.x * 256u + threadIdx.x;
-    const uint64_t m = wi < words ? w.cmask[wi] : 0ull;
-    uint32_t total;
-    const uint32_t off = block_scan((uint32_t)__popcll(m), total, sh);
-    if (threadIdx.x == 0) base_s = atomicAdd(&w.pool[kPoolLive], total);
-    __syncthreads();
-    const uint32_t base = base_s;
-    const uint32_t lane = threadIdx.x & 63u, w0 = blockIdx.x * 256u + (threadIdx.x & ~63u);
-    for (uint32_t j = 0; j < 64u; ++j) {
-        const uint64_t mj = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)m, (int)j) |
-                            (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(m >> 32), (int)j) << 32;
-        if (!mj) continue;
-        const uint32_t oj = (uint32_t)__builtin_amdgcn_readlane((int)off, (int)j);
-        if ((mj >> lane) & 1ull) w.live0[base + oj + lane_rank(mj)] = (w0 + j) * 64u + lane;
+    __shared__ uint32_t lst[256];
+    const uint32_t tb = tile_block() * 256u;
+    const uint32_t p = tb + threadIdx.x;
+    const PathRay pr{w.O, w.D, w.H, w.HM, 0u};
+    Counters k{0u, 0u, 0u};
+    bool go = false;
+    if (p < w.P && (__float_as_uint(w.D[p].w) & kActive)) {
+        go = true;
+        if (sv.tlas_on && !sv.tlas_always && !(sv.num_spheres | sv.num_triangles) && sv.tlas_nodes) {
+            const float4 o = w.O[p], d = w.D[p];
+            const f3 inv = mk(__fdiv_rn(1.0f, d.x), __fdiv_rn(1.0f, d.y), __fdiv_rn(1.0f, d.z));
+            go = tlas_box(sv.tlas[0], mk(o.x, o.y, o.z), inv, w.H[p].x);  // conservative (tlas_box)
+        }
+#ifdef VPX_DEBUG_NO_INST_WALK
+        go = false;  // timing probe only (wrong images): the pass without its instance walks
+#endif
     }
+    uint32_t total;
+    const uint32_t at = block_scan(go ? 1u : 0u, total, sh);
+    if (go) lst[at] = p;
+    __syncthreads();
+    if (threadIdx.x < total) {
+        const uint32_t q = lst[threadIdx.x];
+        const float4 o = w.O[q], d = w.D[q], h = w.H[q];
+        const uint32_t hm = w.HM[q];
+        Ray r;
+        r.O = mk(o.x, o.y, o.z);
+        r.D = mk(d.x, d.y, d.z);
+        r.t = h.x;
+        r.N = mk(h.y, h.z, h.w);
+        r.mat = hm & 0xffu;
+        r.inside = (hm & 0x80000000u) != 0u;
+        int32_t vox = (int32_t)((hm >> 8) & 0xffffu) - 2;
+        if (find_nearest_rest(sv, r, k, &vox)) {
+            w.H[q] = make_float4(r.t, r.N.x, r.N.y, r.N.z);
+            w.HM[q] = r.mat | ((uint32_t)(vox + 2) << 8) | (r.inside ? 0x80000000u : 0u);
+        }
+    }
+    flush_counters(k, 0u, ctr, VPX_STAGE_INSTANCES);
+    __syncthreads();  // the tile's hit records, as the compacted lanes left them
+    Counters ks{0u, 0u, 0u};
+    const bool cont = shade_path<true>(sv, f, w, pr, p, 0, ks);
+    if (f.max_bounces > 0) put_amask(w, p, cont);
+    flush_counters(ks, 0u, ctr, VPX_STAGE_SHADE);
 }
 
 // Renderer::FindNearest for the active paths of a tile (bounce levels).  Rejected (DESIGN.md
