@@ -64,7 +64,10 @@ EXTRA_CONFIGS = ("C2", "C3", "C4", "Z1")
 # run (vpx_kernels.hip launch_render): C2 2.50-2.52 at 2 lanes vs 2.65-2.67 at 3 without forks
 # as the first config (2.70 either way as an extra after C1).  Round-4 build (tools/gpu_r4m.sh,
 # 2 / 3 / 4 lanes): C1 0.553-0.557 / 0.555-0.556 / 0.586-0.587, C4 45.0-45.1 / 43.2-43.5 / 44.5-44.8.
-PIPELINE = {"C1": 3, "C2": 2, "C3": 3, "C4": 3, "Z1": 3}
+# Round 5, with each lane's two sample buffers and the live lists (three interleaved runs): C2
+# 2.350-2.358 (2 lanes, forks) / 2.272-2.338 (3) / 2.412-2.441 (4), and 2.64-2.70 with forks
+# at 3 lanes; C4 42.80-42.99 (3) / 43.70-43.92 (4); Z1 1.755-1.769 (2) / 1.532-1.540 (3).
+PIPELINE = {"C1": 3, "C2": 3, "C3": 3, "C4": 3, "Z1": 3}
 # A rank's share of a multi-GPU frame is a small launch: with each lane's two sample buffers
 # (round 5) four lanes keep more of it in flight for the big frames (rank 0's share at R = 8,
 # tools/rank_share.py, 3 / 4 lanes: C3 0.586 / 0.564 ms, C4 9.93 / 8.63 ms per 16-spp step;

@@ -1179,9 +1179,11 @@ __device__ __forceinline__ void mark_occluded(const WaveBufs& w, uint64_t slot, 
 // 0.5824-0.5839 vs 0.5833-0.5859 ms and runs of 4 cells 0.5843-0.5873 (round 3, three
 // interleaved runs each: noise / slower).
 // p: this thread's path (the tile's, or a live-list entry; >= w.P: none).
+// l16 (k_frame0: one slot per path, the tile's own paths): the list as 16-bit offsets into the
+// tile in the caller's LDS instead of 32-bit entries in the dynamic LDS.
 template <bool ONE, uint32_t RUN = kRunShadow>
 __device__ __forceinline__ void shadow_tile(const SceneView& sv, const WaveBufs& w, unsigned long long* __restrict__ ctr,
-                                            uint32_t* occ, uint32_t p) {
+                                            uint32_t* occ, uint32_t p, uint16_t* l16 = nullptr) {
     __shared__ uint32_t sh[4];
     if (occ)
         for (uint32_t i = threadIdx.x; i < w.S * 8u; i += 256u) occ[i] = 0u;  // published by the barriers below
@@ -1207,13 +1209,18 @@ __device__ __forceinline__ void shadow_tile(const SceneView& sv, const WaveBufs&
     }
     __syncthreads();
     total = __builtin_amdgcn_readfirstlane(sh[0]);  // wave-uniform: a scalar register
+    const uint32_t tb = tile_block() * 256u;
     {
         uint32_t at = m ? hist[key] + pos : 0u;
-        for (uint32_t b = m; b; b &= b - 1u) lst_dyn[at++] = ((uint32_t)__ffs(b) - 1u) << 27 | p;
+        if (l16) {
+            if (m) l16[at] = (uint16_t)(p - tb);  // slot 0
+        } else {
+            for (uint32_t b = m; b; b &= b - 1u) lst_dyn[at++] = ((uint32_t)__ffs(b) - 1u) << 27 | p;
+        }
     }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < total; i += 256u) {
-        const uint32_t e = lst_dyn[i];
+        const uint32_t e = l16 ? tb + l16[i] : lst_dyn[i];
         const uint64_t slot = (uint64_t)(e >> 27) * w.P + (e & 0x07ffffffu);
         if (ONE) {
             // Renderer::IsOccluded in the single volume with only the walk state live
@@ -1696,9 +1703,13 @@ __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_SHADOW : VPX_WPE_MULTI_S
 constexpr uint32_t kFuseFrameTiles = VPX_FUSE_FRAME_TILES;
 // k_frame0 occupancy: with the path state in LDS (round 3) 6 waves/SIMD spill 22 VGPRs
 // (round 2: 272) and measured 1.5 % faster than 5 (no spills) with frames in flight
-// (profiles/r03_frame_occupancy_ab.txt); 7 would need 7 x 23 KiB of LDS per CU (> 160 KiB).
+// (profiles/r03_frame_occupancy_ab.txt).  Round 5: the occluded bitmap sized for its one slot
+// per path and the shadow list as 16-bit tile offsets in static LDS (23168 instead of
+// 24128 bytes per workgroup) let 7 workgroups share a CU's 160 KiB; at 7 (72 VGPRs, 14
+// spilled) C1 measured 0.5440-0.5509 vs 0.5478-0.5580 ms at 6 (seven interleaved runs, five
+// won).
 #ifndef VPX_WPE_FRAME
-#define VPX_WPE_FRAME 6
+#define VPX_WPE_FRAME 7
 #endif
 // The depth-0 frame's path state never leaves the workgroup: a path is shaded, its light
 // resolved and its pixel finished by the same thread, and its shadow slots are walked by the
@@ -1720,7 +1731,8 @@ __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_FRAME : VPX_WPE_MULTI_NE
     __shared__ HeadLds<true> L;
     __shared__ float4 s_val[256];  // LA (a) or leaf of the path's one level
     __shared__ float4 s_sm[256];   // SM: the pending light
-    __shared__ uint32_t occ[kOccWords];
+    __shared__ uint32_t occ[8];      // one slot per path (S == 1, checked at launch)
+    __shared__ uint16_t l16[256];    // the shadow walks' list (shadow_tile)
     const uint32_t tb = tile_block() * 256u;
     const uint32_t p = tb + threadIdx.x;
     WaveBufs wl = w;
@@ -1735,11 +1747,11 @@ __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_FRAME : VPX_WPE_MULTI_NE
     primary_tile<ONE, true>(sv, f, wl, L, ctr);
     __syncthreads();
 #ifdef VPX_FRAME_P_TILE
-    shadow_tile<ONE, kRunFrameShadow>(sv, wl, ctr, occ, tile_block() * 256u + threadIdx.x);
+    shadow_tile<ONE, kRunFrameShadow>(sv, wl, ctr, occ, tile_block() * 256u + threadIdx.x, l16);
 #else
     uint32_t ps = p;  // re-derived, not kept live across the head (as pt below)
     asm volatile("" : "+v"(ps));
-    shadow_tile<ONE, kRunFrameShadow>(sv, wl, ctr, occ, ps);
+    shadow_tile<ONE, kRunFrameShadow>(sv, wl, ctr, occ, ps, l16);
 #endif
     __syncthreads();
     // the tail's own copy of p: the shade's per-lane LDS addresses are re-derived here
