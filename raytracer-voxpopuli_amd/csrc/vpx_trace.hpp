@@ -459,6 +459,13 @@ constexpr uint32_t kRunShadow = VPX_RUN_SHADOW;
 // passes 0.5424-0.5459; runs of 4 in three passes 0.5462-0.5497); k_frame0's shadow walks in two
 // passes on top, C1 0.5413-0.5431 (its own word: the other shadow walkers with two passes, C2
 // 2.466-2.480 vs 2.427-2.452).
+// k_frame0's FindNearest (7 waves/SIMD, round 5): runs of 3 cells in four passes, C1
+// 0.5433-0.5444 vs 0.5456-0.5482 ms in three, then 0.5427-0.5457 vs 0.5447-0.5484 (two boxes,
+// three interleaved runs each); five passes 0.5464-0.5474, runs of 2 in four 0.5428-0.5472.
+#ifndef VPX_RUN_FRAME_NEAREST
+#define VPX_RUN_FRAME_NEAREST (3u | 4u << 8 | 1u << 17 | 1u << 18)
+#endif
+constexpr uint32_t kRunFrameNearest = VPX_RUN_FRAME_NEAREST;
 #ifndef VPX_RUN_FRAME_SHADOW
 #define VPX_RUN_FRAME_SHADOW (3u | 2u << 8 | 1u << 17 | 0u << 18)
 #endif

@@ -857,7 +857,7 @@ struct HeadLds {
     uint32_t hm[SHADE ? 256 : 1];
 };
 
-template <bool ONE, bool SHADE>
+template <bool ONE, bool SHADE, uint32_t RUN = kRunNearest>
 __device__ __forceinline__ void primary_tile(const SceneView& sv, const FrameArgs& f, const WaveBufs& w,
                                              HeadLds<SHADE>& L, unsigned long long* __restrict__ ctr) {
     uint32_t* sh = L.sh;
@@ -918,7 +918,7 @@ __device__ __forceinline__ void primary_tile(const SceneView& sv, const FrameArg
     if (threadIdx.x < total) {
         const uint32_t q = lst[threadIdx.x];
         if (ONE) {
-            nearest_record_1v(sv, pr, q, k);
+            nearest_record_1v<kSkipwNearest, kMincNearest, RUN>(sv, pr, q, k);
         } else {
             const float4 o = pr.O[pr.at(q)], d = pr.D[pr.at(q)];
             Ray r;
@@ -1744,7 +1744,7 @@ __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_FRAME : VPX_WPE_MULTI_NE
     wl.SO = L.ray - tb;
     wl.SD = L.ray + 256 - tb;
     wl.SL = L.ray + 512 - tb;
-    primary_tile<ONE, true>(sv, f, wl, L, ctr);
+    primary_tile<ONE, true, kRunFrameNearest>(sv, f, wl, L, ctr);
     __syncthreads();
 #ifdef VPX_FRAME_P_TILE
     shadow_tile<ONE, kRunFrameShadow>(sv, wl, ctr, occ, tile_block() * 256u + threadIdx.x, l16);
