@@ -41,10 +41,13 @@ for R in (1, 2, 4, 8):
     t0 = time.perf_counter()
     for _ in range(K):
         step()
+    issue = (time.perf_counter() - t0) * 1e3 / K  # host time to enqueue a step (no sync inside)
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) * 1e3 / K
-    out.append((R, ms))
+    out.append((R, ms, issue))
     del acc, rgb
 base = out[0][1]
-print(cfg, f"pipe={os.environ.get('PIPE', '0')}", " ".join(f"R={R}: {ms:.4f} ms (x{base / ms:.2f})" for R, ms in out))
+print(cfg, f"pipe={os.environ.get('PIPE', '0')}", " ".join(f"R={R}: {ms:.4f} ms (x{base / ms:.2f})" for R, ms, _ in out))
+if os.environ.get("ISSUE"):
+    print("  host issue ms per step:", " ".join(f"R={R}: {i:.4f}" for R, _, i in out))
 ctx.close()
