@@ -1705,7 +1705,7 @@ constexpr uint32_t kFuseFrameTiles = VPX_FUSE_FRAME_TILES;
 // (round 2: 272) and measured 1.5 % faster than 5 (no spills) with frames in flight
 // (profiles/r03_frame_occupancy_ab.txt).  Round 5: the occluded bitmap sized for its one slot
 // per path and the shadow list as 16-bit tile offsets in static LDS (23168 instead of
-// 24128 bytes per workgroup) let 7 workgroups share a CU's 160 KiB; at 7 (72 VGPRs, 14
+// 24128 bytes per workgroup) let 7 workgroups share a CU's 160 KiB; at 7 (72 VGPRs, 14-19
 // spilled) C1 measured 0.5440-0.5509 vs 0.5478-0.5580 ms at 6 (seven interleaved runs, five
 // won).
 #ifndef VPX_WPE_FRAME
