@@ -1405,6 +1405,9 @@ __global__ __launch_bounds__(kPoolWg) VPX_WPE(VPX_WPE_SPOOL) void k_shadow_pool(
 __device__ __forceinline__ bool occluded_instances(const SceneView& sv, const float4* vb, const Ray& r, Counters& k) {
     const uint32_t nv = sv.num_volumes;
     uint64_t cand = 0ull;
+#ifdef VPX_DEBUG_PROBE_INST_SHADOW
+    if (VPX_DEBUG_PROBE_INST_SHADOW < 2)
+#endif
     for (uint32_t i = 1; i < nv; ++i)
         cand |= (misses_volume(vb[i], r.O, r.D) ? 0ull : 1ull) << (i - 1u);
     bool occ = false;
@@ -1413,6 +1416,10 @@ __device__ __forceinline__ bool occluded_instances(const SceneView& sv, const fl
     // volume no lane of the wave can reach costs one ballot
     for (uint32_t i = 1; i < nv; ++i) {
         const bool want = !occ && ((cand >> (i - 1u)) & 1ull);
+#ifdef VPX_DEBUG_PROBE_INST_SHADOW
+        // timing probe only (wrong images): 1 = no instance walks, 2 = no sphere tests either
+        if (VPX_DEBUG_PROBE_INST_SHADOW >= 1) continue;
+#endif
         if (!__ballot(want)) continue;
         if (!want) continue;
         const vpx_volume vol = ldu(sv.volumes, i);  // i is wave-uniform
