@@ -978,6 +978,21 @@ __global__ __launch_bounds__(256) void k_compact(WaveBufs w, int level) {
     }
 }
 
+// The instance walks' words (FindNearest in the instance grids, k_instances): the heads' words
+// measured best (C4 42.39-42.44 ms; skip minimum 1 / 3: 42.76-42.87 / 42.37-42.51, two passes
+// 42.46-42.56, skip weight 2 42.31-42.37 — two interleaved runs, noise).
+#ifndef VPX_RUN_INST_NEAREST
+#define VPX_RUN_INST_NEAREST VPX_RUN_NEAREST
+#endif
+#ifndef VPX_MINC_INST_NEAREST
+#define VPX_MINC_INST_NEAREST VPX_MINC_NEAREST
+#endif
+#ifndef VPX_SKIPW_INST_NEAREST
+#define VPX_SKIPW_INST_NEAREST 1u
+#endif
+constexpr uint32_t kRunInstNearest = VPX_RUN_INST_NEAREST, kMincInstNearest = VPX_MINC_INST_NEAREST,
+                   kSkipwInstNearest = VPX_SKIPW_INST_NEAREST;
+
 // Multi-volume primary rays in two launches: the world (volume 0, first in the reference's
 // loop) walked by the lean single-volume head (k_primary<true, false>: 6 waves/SIMD, no
 // spills) writing the hit records to HBM, then this instance pass: per tile, the paths whose
@@ -1030,7 +1045,7 @@ __global__ __launch_bounds__(256) VPX_WPE(VPX_WPE_MULTI_NEAREST) void k_instance
         r.mat = hm & 0xffu;
         r.inside = (hm & 0x80000000u) != 0u;
         int32_t vox = (int32_t)((hm >> 8) & 0xffffu) - 2;
-        if (find_nearest_rest(sv, r, k, &vox)) {
+        if (find_nearest_rest<kSkipwInstNearest, kMincInstNearest, kRunInstNearest>(sv, r, k, &vox)) {
             w.H[q] = make_float4(r.t, r.N.x, r.N.y, r.N.z);
             w.HM[q] = r.mat | ((uint32_t)(vox + 2) << 8) | (r.inside ? 0x80000000u : 0u);
         }
@@ -1402,6 +1417,20 @@ __global__ __launch_bounds__(kPoolWg) VPX_WPE(VPX_WPE_SPOOL) void k_shadow_pool(
 #ifndef VPX_INST_CULL
 #define VPX_INST_CULL 1
 #endif
+#ifndef VPX_RUN_INST_SHADOW
+#define VPX_RUN_INST_SHADOW VPX_RUN_SHADOW
+#endif
+#ifndef VPX_SKIPW_INST_SHADOW
+#define VPX_SKIPW_INST_SHADOW 4u
+#endif
+// Skip minimum 2 (cubes of one brick stepped through) for the instance grids' shadow walks:
+// C4 42.43-42.51 vs 42.71-42.96 ms (five interleaved runs, all won; 3: 42.82-42.90, 4:
+// 43.05-43.26; two passes per iteration 43.1-43.3, the two-compare step 42.7-42.8).
+#ifndef VPX_MINC_INST_SHADOW
+#define VPX_MINC_INST_SHADOW 2u
+#endif
+constexpr uint32_t kRunInstShadow = VPX_RUN_INST_SHADOW, kSkipwInstShadow = VPX_SKIPW_INST_SHADOW,
+                   kMincInstShadow = VPX_MINC_INST_SHADOW;
 __device__ __forceinline__ bool occluded_instances(const SceneView& sv, const float4* vb, const Ray& r, Counters& k) {
     const uint32_t nv = sv.num_volumes;
     uint64_t cand = 0ull;
@@ -1431,7 +1460,7 @@ __device__ __forceinline__ bool occluded_instances(const SceneView& sv, const fl
         Dda s;
         if (!dda_setup(vol, g.n, o, s)) continue;
         skip::Walk wk = to_walk(s);
-        occ = walk_wave<16, kSkipwShadow, kMincShadow, kRunShadow>(grid_view(g), wk, r.t, k.cells);
+        occ = walk_wave<16, kSkipwInstShadow, kMincInstShadow, kRunInstShadow>(grid_view(g), wk, r.t, k.cells);
     }
     if (occ) return true;
     for (uint32_t i = 0; i < sv.num_spheres; ++i)
