@@ -7,7 +7,11 @@ vpx_render call (primary rays, Trace(ray, max_bounces) flattened, the light samp
 their shadow rays, running-average accumulate, tonemap, RGB8; the wavefront kernels of
 DESIGN.md §4).  The headline line is C1 (BASELINE.json configs[1]): 1920x1080, 1024^3 world
 (monu3.vox tiled), 1 spp, depth 0.  Inputs (world, tables, accumulator)
-are resident in HBM before timing.
+are resident in HBM before timing.  Arithmetic (every config of the line, `arithmetic`): the
+reference's own — FindNearest's FastReciprocal and the rsqrtps primary normalise from this
+host's captured rcpss / rsqrtss tables (VPX_ARITH_X86_HOST), the mode whose
+output matches the reference within north_star's 1e-4 (0 pixels beyond on every full-size
+shard, tests/test_x86_arith.py); `other_arithmetic` times C1 in the exact mode beside it.
 
 N > 1 (one rank process per GPU: under torchrun, or started by this script itself as a
 torch.distributed.run child when run as plain `python bench.py --gpus N`): STRONG scaling — the configured frame (C1: 1920x1080
@@ -50,6 +54,9 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 import __graft_entry__ as entry  # noqa: E402
 
+# the reference's arithmetic (VPX_ARITH_X86_HOST) needs the host's rcpss / rsqrtss tables
+X86_HOST = os.uname().machine in ("x86_64", "i686")
+ARITH_NAMES = {0: "VPX_ARITH_EXACT", 1: "VPX_ARITH_X86_HOST"}
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 METRIC = "Mray/s (primary+shadow) at 1920×1080, 1024³ world; 1/2/4/8-GPU"
 # Z1: the reference's own scene shape (SetUpFirstZone: 21 volumes, 10 triangles, point + 5 spot +
@@ -418,9 +425,12 @@ def time_frames(o, desc, threads, warm=3, frames=20):
             "rays_per_frame": {"primary": st.primary_rays, "shadow": st.shadow_rays}}
 
 
-def cpu_baseline(pkg, desc, budget_s=12.0):
-    """The oracle (perf build) on the host: C1 row sample (value) + C0 / C0' frames."""
+def cpu_baseline(pkg, desc, budget_s=12.0, arith=0):
+    """The oracle (perf build) on the host: C1 row sample (value) + C0 / C0' frames, in the
+    headline's arithmetic (x86: the oracle's FastReciprocal / rsqrtps with this host's own
+    instructions, as the reference computes them)."""
     orc = entry.load_oracle()
+    orc.set_x86_approx(pkg.abi, arith, perf=True)
     threads = cpu_threads()
     t0 = time.time()
     o = orc.Oracle(pkg.abi, desc, perf=True)
@@ -447,7 +457,8 @@ def cpu_baseline(pkg, desc, budget_s=12.0):
                      f"(min {min(runs):.3f}, max {max(runs):.3f} Mray/s); world generated on host in {gen_s:.1f} s",
            "cpu_model": cpu_model(), "machine_logical_cpus": os.cpu_count(),
            "threads_note": "cores = threads used = the box's CPU share (OMP_NUM_THREADS); std::thread pixel pool",
-           "build": "oracle/liboracle_perf.so: gcc -O3 -march=x86-64-v3 -ffp-contract=off, FTZ/DAZ"}
+           "build": "oracle/liboracle_perf.so: gcc -O3 -march=x86-64-v3 -ffp-contract=off, FTZ/DAZ",
+           "arithmetic": ARITH_NAMES[arith]}
     for key, cfg in (("c0", "C0"), ("c0_prime", "C0m")):  # 640x360, 1 spp, depth 0
         d = pkg.scene.CONFIGS[cfg]()
         oc = orc.Oracle(pkg.abi, d, perf=True)
@@ -486,9 +497,10 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip extra_configs / weak_scaling")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
-    ap.add_argument("--arith", choices=("exact", "x86"), default="exact",
-                    help="vpx_set_arithmetic of the headline config (x86: the reference's rcpps+NR / rsqrtps, "
-                         "this host's tables); the N=1 line also reports C1 in the x86 mode as reference_arithmetic")
+    ap.add_argument("--arith", choices=("exact", "x86"), default="x86" if X86_HOST else "exact",
+                    help="vpx_set_arithmetic of every config (x86, the default on x86 hosts: the reference's "
+                         "FastReciprocal rcpps+NR and rsqrtps normalise, this host's tables, DESIGN.md §3 item 1); "
+                         "the N=1 line also reports C1 in the other mode as other_arithmetic")
     ap.add_argument("--pipeline", type=int, default=None,
                     help="frames in flight per GPU (vpx_set_pipeline lanes; 0 = serial frames); default: "
                          "per config, PIPELINE")
@@ -511,16 +523,19 @@ def main():
     arith = 1 if args.arith == "x86" else 0
     head = run_config(pkg, env, args.config, args.steps, args.warmup, sha=sha, pipeline=args.pipeline,
                       serial_frames=args.steps, arith=arith)
-    ref_arith = None
-    if env.n == 1 and not args.no_extra and not arith and os.uname().machine == "x86_64":
-        # the same workload in the reference-arithmetic mode (VPX_ARITH_X86_HOST: FindNearest's
-        # FastReciprocal and the primary rsqrtps as this host computes them, bit-identical to the
-        # oracle's x86 mode, tests/test_x86_arith.py)
-        r = run_config(pkg, env, args.config, args.steps, args.warmup, sha=sha, pipeline=args.pipeline, arith=1)
+    other_arith = None
+    if env.n == 1 and not args.no_extra and X86_HOST:
+        # the same workload in the other arithmetic mode: with the reference's arithmetic as the
+        # headline (VPX_ARITH_X86_HOST: FindNearest's FastReciprocal and the primary rsqrtps as this
+        # host computes them, bit-identical to the oracle's x86 mode, tests/test_x86_arith.py), the
+        # exact mode's C1 (exact 1/x, 1/sqrtf) beside it, and what the tables cost
+        o = 1 - arith
+        r = run_config(pkg, env, args.config, args.steps, args.warmup, sha=sha, pipeline=args.pipeline, arith=o)
         if r is not None:
-            ref_arith = {"mode": "VPX_ARITH_X86_HOST", "ms_per_step": r["ms_per_step"], "value": r["value"],
-                         "exact_ms_per_step": head["ms_per_step"],
-                         "cost": round(r["ms_per_step"] / head["ms_per_step"] - 1.0, 4)}
+            other_arith = {"mode": ARITH_NAMES[o], "ms_per_step": r["ms_per_step"], "value": r["value"],
+                           "headline_mode": ARITH_NAMES[arith], "headline_ms_per_step": head["ms_per_step"],
+                           "x86_cost": round((head["ms_per_step"] / r["ms_per_step"] if arith else
+                                              r["ms_per_step"] / head["ms_per_step"]) - 1.0, 4)}
     extra, weak = {}, None
     if not args.no_extra:
         # the extras time as many steps as the headline: with frames in flight the timed region
@@ -534,7 +549,8 @@ def main():
                 if r is not None:
                     extra[cfg] = r
         if env.n > 1:
-            weak = run_config(pkg, env, args.config, xs, min(args.warmup, 2), weak=True, sha=sha, pipeline=args.pipeline)
+            weak = run_config(pkg, env, args.config, xs, min(args.warmup, 2), weak=True, sha=sha, pipeline=args.pipeline,
+                              arith=arith)
     if env.rank == 0:
         out = {"metric": METRIC, "value": head["value"], "unit": "Mray/s", "n_gpus": env.n, "steps": args.steps,
                "warmup": args.warmup, "ms_per_step": head["ms_per_step"], "higher_is_better": True,
@@ -546,10 +562,14 @@ def main():
                           "parallelism": env.parallelism(), "frames_in_flight": head["pipeline"], "lib_sha256": sha},
                "rays_per_step": head["rays_per_step"], "mpix_per_s": head["mpix_per_s"],
                "total_mray_s": head["total_mray_s"], "roofline": head["roofline"], "cpu_baseline": None}
-        if ref_arith is not None:
-            out["reference_arithmetic"] = ref_arith
-        if arith:
-            out["config"]["arithmetic"] = "VPX_ARITH_X86_HOST"
+        out["arithmetic"] = out["config"]["arithmetic"] = ARITH_NAMES[arith]
+        out["arithmetic_def"] = ("VPX_ARITH_X86_HOST: FindNearest's per-volume rD by FastReciprocal (rcpps + one Newton "
+                                 "step, renderer.cpp:929-934) and the primary directions by rsqrtps "
+                                 "(tmpl8math.h:2356-2360), from this host's captured tables, in every config of the "
+                                 "line: the reference's own arithmetic, 0 pixels beyond 1e-4 on the full-size shards "
+                                 "(tests/test_x86_arith.py)" if arith else "VPX_ARITH_EXACT: exact 1/x and 1/sqrtf")
+        if other_arith is not None:
+            out["other_arithmetic"] = other_arith
         for k in ("serial_ms_per_frame", "serial_ms_per_step", "serial_def", "ranks"):
             if k in head:
                 out[k] = head[k]
@@ -558,7 +578,7 @@ def main():
         if weak is not None:
             out["weak_scaling"] = weak
         if env.n == 1 and not args.no_cpu:
-            out["cpu_baseline"] = cpu_baseline(pkg, pkg.scene.CONFIGS[args.config](), args.cpu_budget)
+            out["cpu_baseline"] = cpu_baseline(pkg, pkg.scene.CONFIGS[args.config](), args.cpu_budget, arith)
         print(json.dumps(out), flush=True)
     if env.dist:
         env.dist.destroy_process_group()

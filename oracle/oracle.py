@@ -81,6 +81,15 @@ def _lib(abi, perf=False):
     return lib
 
 
+def set_x86_approx(abi, on, perf=False):
+    """The reference's x86 arithmetic in the restatement (oracle_set_x86_approx): FindNearest's
+    FastReciprocal and the primary rsqrtps normalise computed with this host's rcpss / rsqrtss
+    (renderer.cpp:929-934, tmpl8math.h:2356-2360); process-wide for that build of the library."""
+    lib = _lib(abi, perf)
+    lib.oracle_set_x86_approx.argtypes = [C.c_int]
+    return lib.oracle_set_x86_approx(1 if on else 0)
+
+
 class BasicBVH:
     """src/BVH/BasicBVH.{h,cpp} restated (oracle_bvh_*): build once, intersect rays."""
 

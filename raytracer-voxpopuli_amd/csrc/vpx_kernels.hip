@@ -1013,6 +1013,9 @@ int launch_render(vpx_ctx* c, hipStream_t s, vpx_ctx::WaveStore& ws, const Scene
     // (fused tail: k_shadow_finish already finished the frame; max_bounces = -1 runs no
     // level, so the finish folds the zero leaf here)
     const bool finished = fuse_tail && f.max_bounces >= 0 && !tailed;
+    // a frame in flight that blends on its lane (tail_wait) blends here when k_tail ran: the
+    // blend must follow the caller's earlier writes and the previous frame's blend
+    if (!finished && tail_wait) VPX_HIP(c, hipStreamWaitEvent(s, *tail_wait, 0));
     if (!finished) prof_mark(c, s, VPX_STAGE_FINISH);
     if (!rp) {
         if (!finished) hipLaunchKernelGGL((k_finish<MODE>), grid, block, 0, s, f, w, accum, rgb8, packed);

@@ -4,6 +4,7 @@
 // every evaluation here does too.
 #include <atomic>
 #include <cstring>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -113,6 +114,24 @@ bool spot_check(const Model& md, uint32_t bad[2]) {
             }
     return mis[0] == 0 && mis[1] == 0;
 }
+
+// The host's tables do not change while the process runs: capture and spot-check once, and
+// serve every vpx_set_arithmetic (size query, data copy, each member of a device set) and
+// every verify from that copy.
+struct Cached {
+    Model md;
+    bool ok = false;
+};
+const Cached& cached_model() {
+    static Cached c;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        capture(c.md);
+        uint32_t bad[2] = {0, 0};
+        c.ok = spot_check(c.md, bad);
+    });
+    return c;
+}
 #endif
 
 }  // namespace
@@ -122,10 +141,9 @@ extern "C" {
 int vpx_x86_arith_tables(uint32_t* out, uint64_t cap, uint32_t info[4]) {
 #ifdef VPX_HOST_X86
     if (!info) return VPX_E_INVALID;
-    Model md;
-    capture(md);
-    uint32_t bad[2] = {0, 0};
-    if (!spot_check(md, bad)) return VPX_E_STATE;
+    const Cached& cm = cached_model();
+    if (!cm.ok) return VPX_E_STATE;
+    const Model& md = cm.md;
     info[0] = md.rcp_shift;
     info[1] = md.rsq_shift;
     info[2] = md.rsq_off;
@@ -144,8 +162,7 @@ int vpx_x86_arith_tables(uint32_t* out, uint64_t cap, uint32_t info[4]) {
 int vpx_x86_arith_verify(uint32_t lo, uint32_t hi, uint32_t threads, uint64_t mismatches[2], uint32_t first_bad[2]) {
 #ifdef VPX_HOST_X86
     if (!mismatches || !first_bad || hi < lo) return VPX_E_INVALID;
-    Model md;
-    capture(md);
+    const Model& md = cached_model().md;
     const uint32_t nt = threads ? (threads > 256 ? 256 : threads) : 1u;
     const uint64_t n = (uint64_t)hi - lo + 1;
     std::vector<uint64_t> mis(2 * nt, 0);

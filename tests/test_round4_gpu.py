@@ -114,17 +114,21 @@ def test_zone_scene_bit_exact(pkg, orc, depth):
     assert t_g.bounce_rays > 0
 
 
-@pytest.mark.parametrize("scene", ["areas-d0", "instances-areas-d0", "instances-areas-d2"])
+@pytest.mark.parametrize("scene", ["areas-d0", "instances-areas-d0", "instances-areas-d2", "roomGlass-d14-areas"])
 @pytest.mark.parametrize("lanes", [2, 4])
 def test_lane_tail_frames_in_flight(pkg, orc, scene, lanes):
     """Frames in flight whose tail is its own launch (the shadow pool's k_resolve_finish:
     area lights with several samples) blend on their lane straight into the accumulator,
     ordered by the caller's stream (no packed sample, no composite): 4 AA frames equal the
     serial frames and the oracle (single volume at depth 0, and the instanced world, where the
-    depth-2 frames go through the per-level kernels with the shadow pool's tail)."""
+    depth-2 frames go through the per-level kernels with the shadow pool's tail; and a depth-14
+    area-light frame, whose deep levels end in k_tail + k_finish: that blend waits for the
+    caller's stream too)."""
     sc = pkg.scene
     if scene == "areas-d0":
         desc = sc.city_scene("monu3", 128, 80, 64, 0, areas=sc.C3_AREAS)
+    elif scene in CASES:  # depth 14: the deep levels run in k_tail, then k_finish blends on the lane
+        desc = CASES[scene](sc)
     else:
         desc = sc.instanced_scene(n=128, inst_n=32, width=80, height=64, spp=1)
         desc.max_bounces = 2 if scene.endswith("d2") else 0

@@ -10,10 +10,12 @@ CPU (runs here): the table model equals the host's rcpss and rsqrtss for all 2^3
 GPU (runs on the MI355X box, whose host is the CPU the bench's cpu_baseline runs on): the same
 all-inputs check on that host, then frames rendered in the mode equal the oracle with
 oracle_set_x86_approx(1) bit for bit — accumulator floats, RGB8 bytes and ray / DDA-cell
-counts — for C0, C0', roomGlass-128 at depth 4, a DOF + AA frame, the zone scene and the
-instanced world (multi-volume FindNearest), and rank 0's 1/16 shard of the full-size C1 and C2
-frames (the BASELINE configs where the exact build misses north_star's 1e-4 on 0.14 % / 0.28 %
-of the pixels, profiles/r04_x86_approx_rates.json): 0 pixels beyond 1e-4 in the mode.
+counts — for C0, C0', roomGlass-128 at depth 4, a DOF + AA frame, the zone scene at depths 2
+and 14 and a depth-14 area-light room (the deep levels in k_tail), the instanced world
+(multi-volume FindNearest), and rank 0's shard of every full-size BASELINE config (C1 / C2 / Z1
+at 1/16, C3 / C4 at 1/64, C4 over its 16 accumulated frames; the exact build misses north_star's
+1e-4 on 0.14 % / 0.28 % of C1 / C2's pixels, profiles/r04_x86_approx_rates.json): 0 pixels
+beyond 1e-4 in the mode.
 """
 import ctypes as C
 import gc
@@ -128,11 +130,16 @@ def _frame_cases(sc, abi):
         "monu3-128 aa+dof d1": lambda: dof(sc.model_scene("monu3", 128, 160, 96, 1)),
         "zone 96x64 d2": lambda: zone(sc.zone_scene(96, 64, 2)),
         "instances 80x64 d1": inst,
+        # depth 14: the deep levels run in k_tail, which takes the tables through its runtime
+        # branch (the multi-volume zone scene and a single-volume area-light room)
+        "zone 96x64 d14": lambda: zone(sc.zone_scene(96, 64, 14)),
+        "roomGlass-128 64x40 d14 areas": lambda: zone(sc.city_scene("roomGlass", 128, 64, 40, 14, areas=sc.C3_AREAS[:2])),
     }
 
 
 FRAME_CASES = ["C0 teapot128 640x360 d0", "C0' monu3-128 640x360 d0", "roomGlass-128 640x360 d4",
-               "monu3-128 aa+dof d1", "zone 96x64 d2", "instances 80x64 d1"]
+               "monu3-128 aa+dof d1", "zone 96x64 d2", "instances 80x64 d1", "zone 96x64 d14",
+               "roomGlass-128 64x40 d14 areas"]
 
 
 def _counts(st):
@@ -174,29 +181,41 @@ def test_frames_in_reference_arithmetic(pkg, orc, name):
     assert c_g == (st_o.primary_rays, st_o.shadow_rays, st_o.bounce_rays, st_o.dda_cells), name
 
 
+# Ranks the full frame is cut into: rank 0's share is ~130 k pixels (C1 / C2 / Z1 at 1/16,
+# C3 / C4 at 1/64), every R-th 16x16 tile of the full-size frame (tests/test_full_size.py).
+SHARD_RANKS = {"C1": 16, "C2": 16, "C3": 64, "C4": 64, "Z1": 16}
+
+
 @pytest.mark.gpu
 @pytest.mark.skipif(not X86, reason="x86 intrinsics")
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("cfg", ["C1", "C2"])
+@pytest.mark.parametrize("cfg", ["C1", "C2", "C3", "C4", "Z1"])
 def test_full_size_shard_in_reference_arithmetic(pkg, orc, cfg):
-    """Rank 0's 1/16 shard of the full-size frame (about 130 k pixels of the 1920x1080 frame
-    over the 1024^3 world): raw samples and counts equal the oracle's x86 mode bit for bit, and
-    the exact mode's samples differ from them (the mode is what moves those pixels)."""
+    """Rank 0's shard of the full-size frame (about 130 k pixels: 1/16 of the 1920x1080 C1 / C2 /
+    Z1 frames, 1/64 of the 3840x2160 C3 / C4 frames over the 2048^3 world; C4 over all 16
+    accumulated frames, each with its own seeds): every frame's raw samples and its ray / DDA-cell
+    counts equal the oracle's x86 mode bit for bit, so 0 pixels differ beyond north_star's 1e-4.
+    The exact mode's first-frame samples are compared with the same oracle samples and the
+    number beyond 1e-4 recorded (the pixels the mode moves)."""
     torch = _gpu()
     abi = pkg.abi
     desc = pkg.scene.CONFIGS[cfg]()
-    W, H, R = desc.width, desc.height, 16
-    p = desc.frame_params(0)
+    W, H, R = desc.width, desc.height, SHARD_RANKS[cfg]
+    frames = max(1, int(desc.spp))
     ctx = pkg.context.Context(0)
     ctx.load_scene(desc)
     L = ctx.packed_len(W, H, R)
     packed = torch.zeros(L * 4, dtype=torch.float32, device="cuda")
-    res = {}
-    for mode in (abi.VPX_ARITH_EXACT, abi.VPX_ARITH_X86_HOST):
-        ctx.set_arithmetic(mode)
-        st = ctx.render_tiles(p, 0, R, packed.data_ptr(), stats=True)
+    ctx.set_arithmetic(abi.VPX_ARITH_EXACT)
+    ctx.render_tiles(desc.frame_params(0), 0, R, packed.data_ptr(), stats=True)
+    torch.cuda.synchronize()
+    g_ex = packed.view(-1, 4).cpu().numpy().copy()
+    ctx.set_arithmetic(abi.VPX_ARITH_X86_HOST)
+    gx = []
+    for f in range(frames):
+        st = ctx.render_tiles(desc.frame_params(f), 0, R, packed.data_ptr(), stats=True)
         torch.cuda.synchronize()
-        res[mode] = (packed.view(-1, 4).cpu().numpy().copy(), _counts(st))
+        gx.append((packed.view(-1, 4).cpu().numpy().copy(), _counts(st)))
     ctx.close()
     del packed
     torch.cuda.empty_cache()
@@ -205,25 +224,35 @@ def test_full_size_shard_in_reference_arithmetic(pkg, orc, cfg):
     lib = orc._lib(abi)
     lib.oracle_set_x86_approx.argtypes = [C.c_int]
     o = orc.Oracle(abi, desc)
+    so = []
     try:
         lib.oracle_set_x86_approx(1)
-        s_o, st_o = o.render_pixels(p, ids[ok].astype(np.uint32), _threads())
+        for f in range(frames):
+            so.append(o.render_pixels(desc.frame_params(f), ids[ok].astype(np.uint32), _threads()))
     finally:
         lib.oracle_set_x86_approx(0)
     del o
     gc.collect()
-    g_x86, c_x86 = res[abi.VPX_ARITH_X86_HOST]
-    g_ex = res[abi.VPX_ARITH_EXACT][0]
-    sx, se = g_x86[: len(ids)][ok], g_ex[: len(ids)][ok]
-    beyond = int((np.abs(sx[:, :3] - s_o[:, :3]) > 1e-4).any(1).sum())
-    moved = int((np.abs(se[:, :3] - s_o[:, :3]) > 1e-4).any(1).sum())
-    out = {"cfg": cfg, "pixels": int(ok.sum()), "x86_mode_beyond_1e-4": beyond, "exact_mode_beyond_1e-4": moved,
-           "cpu_model": _cpu_model()}
+    beyond, mism = 0, []
+    for f in range(frames):
+        sx, s_o = gx[f][0][: len(ids)][ok], so[f][0]
+        beyond += int((np.abs(sx[:, :3] - s_o[:, :3]) > 1e-4).any(1).sum())
+        if not np.array_equal(sx.view(np.uint32), s_o.view(np.uint32)):
+            mism.append(f)
+    st_o0 = so[0][1]
+    se = g_ex[: len(ids)][ok]
+    moved = int((np.abs(se[:, :3] - so[0][0][:, :3]) > 1e-4).any(1).sum())
+    out = {"cfg": cfg, "pixels": int(ok.sum()), "frames": frames, "x86_mode_beyond_1e-4": beyond,
+           "x86_mode_frames_not_bit_identical": mism, "exact_mode_beyond_1e-4_frame0": moved,
+           "counts_frame0": list(gx[0][1]), "cpu_model": _cpu_model()}
     print(json.dumps(out))
     od = os.path.join(REPO, "gpurun_out")
     if os.path.isdir(od):
         with open(os.path.join(od, f"x86_arith_shard_{cfg}.json"), "w") as f:
             json.dump(out, f, indent=1)
-    assert np.array_equal(sx.view(np.uint32), s_o.view(np.uint32)), out
-    assert c_x86 == (st_o.primary_rays, st_o.shadow_rays, st_o.bounce_rays, st_o.dda_cells), (c_x86, st_o.as_dict())
-    assert not np.array_equal(se.view(np.uint32), sx.view(np.uint32))
+    assert not mism and beyond == 0, out
+    for f in range(frames):
+        st_o = so[f][1]
+        assert gx[f][1] == (st_o.primary_rays, st_o.shadow_rays, st_o.bounce_rays, st_o.dda_cells), \
+            (cfg, f, gx[f][1], st_o.as_dict())
+    assert st_o0.primary_rays == int(ok.sum())
