@@ -213,6 +213,15 @@ def load_library(path=None):
     p = path or os.environ.get("VPX_LIB") or LIB_PATH
     if not os.path.exists(p):
         raise VpxError(f"{p} is missing: run __graft_entry__.build() (hipcc --offload-arch=gfx950)")
+    # One HIP runtime per process: torch's wheel bundles its own libamdhip64 (soname
+    # libamdhip64.so.7, but needed by torch as libamdhip64.so).  Loaded first, the library would
+    # bind /opt/rocm's copy and torch would then load a second runtime, after which the
+    # library's first hipGetDeviceCount fails (measured on the box: vpx_create -> VPX_E_DEVICE).
+    # With torch loaded first the library's DT_NEEDED resolves to torch's runtime by soname.
+    try:
+        import torch  # noqa: F401
+    except ImportError:  # plain C-ABI use without torch: /opt/rocm's runtime only
+        pass
     lib = C.CDLL(p)
     old_ok = os.environ.get("VPX_LIB_OLD") == "1"  # A/B runs against an earlier build (tools/gpu_ab.sh)
     for name, (res, args) in SIGNATURES.items():
