@@ -845,6 +845,8 @@ int launch_render(vpx_ctx* c, hipStream_t s, vpx_ctx::WaveStore& ws, const Scene
     // single volume, no analytic shapes: the DDA kernels' lean instances
     const bool one = sv.num_volumes == 1 && !(sv.num_spheres | sv.num_triangles);
     const bool x86 = sv.x86.tab != nullptr;  // the reference-arithmetic instances of the hot kernels
+    // the multi-volume walkers' rcp table in LDS (x86_stage_lds): its dynamic LDS bytes
+    const size_t xlds = x86 ? sizeof(uint32_t) * sv.x86.rsq_off : 0;
     // the last level's shadow -> resolve -> finish as one launch (k_shadow_finish), except
     // on the static-camera path, whose tail is the reprojection
     const bool fuse_tail = !rp;
@@ -912,7 +914,7 @@ int launch_render(vpx_ctx* c, hipStream_t s, vpx_ctx::WaveStore& ws, const Scene
     prof_mark(c, s, -1);
     if (split) {
         prof_mark(c, s, VPX_STAGE_INSTANCES);
-        hipLaunchKernelGGL(k_instances, grid, block, 0, s, sv, f, w, c->d_ctr);
+        hipLaunchKernelGGL(k_instances, grid, block, xlds, s, sv, f, w, c->d_ctr);
         prof_mark(c, s, -1);
     }
     // FindNearest for the traced rays of the next level: the bounce pool (single volume, no
@@ -927,7 +929,7 @@ int launch_render(vpx_ctx* c, hipStream_t s, vpx_ctx::WaveStore& ws, const Scene
                                dim3(kPoolWg), 0, bs, sv, w, level,
                                c->d_ctr);
         } else {  // multi-volume / shape scenes: persistent waves over the live list, 64 rays a grab
-            hipLaunchKernelGGL(k_nearest_tile, grid, block, 0, bs, sv, w, level, c->d_ctr);
+            hipLaunchKernelGGL(k_nearest_tile, grid, block, xlds, bs, sv, w, level, c->d_ctr);
         }
         prof_mark(c, bs, -1);
     };
@@ -1004,7 +1006,7 @@ int launch_render(vpx_ctx* c, hipStream_t s, vpx_ctx::WaveStore& ws, const Scene
             WaveBufs wt = w;
             wt.occb = nullptr;  // k_tail marks occluded slots in their SD words, as the tile kernels do
             prof_mark(c, s, VPX_STAGE_BOUNCE);
-            hipLaunchKernelGGL(k_tail, grid, block, 0, s, sv, f, wt, level + 1, c->d_ctr);
+            hipLaunchKernelGGL(k_tail, grid, block, xlds, s, sv, f, wt, level + 1, c->d_ctr);
             prof_mark(c, s, -1);
             tailed = true;
             break;
@@ -1520,7 +1522,12 @@ static float4 volume_bounds(const vpx_volume& v) {
                        a[0][1] * (a[1][0] * a[2][2] - a[1][2] * a[2][0]) +
                        a[0][2] * (a[1][0] * a[2][1] - a[1][1] * a[2][0]);
     const float4 none = make_float4(0.f, 0.f, 0.f, INFINITY);
-    if (!(std::fabs(det) > 1e-30) || m[12] != 0.f || m[13] != 0.f || m[14] != 0.f || m[15] != 1.f) return none;
+    // Every transform of the path is affine in rows 0-2 (xform_pos_ssem / xform_pos read m[0..11],
+    // as TransformPosition(_SSEM) does, tmpl8math.cpp:345-402), so the bottom row plays no part:
+    // SetTransform's inverse leaves m[15] = 1 +- 1 ulp on a third of C4's rotated instances, and
+    // requiring it to be exactly (0, 0, 0, 1) had put them in the TLAS's always-set, unculled
+    // (every C4 primary ray set up ~20 instance walks that Setup3DDDA then refused).
+    if (!(std::fabs(det) > 1e-30)) return none;
     double r[3][3];  // inverse of the 3x3 part
     r[0][0] = (a[1][1] * a[2][2] - a[1][2] * a[2][1]) / det;
     r[0][1] = (a[0][2] * a[2][1] - a[0][1] * a[2][2]) / det;
@@ -1744,6 +1751,8 @@ int vpx_set_arithmetic(vpx_ctx* c, uint32_t mode) {
     uint32_t info[4];
     if (vpx_x86_arith_tables(nullptr, 0, info) != VPX_OK)
         return fail(c, VPX_E_STATE, "the host's rcpss / rsqrtss do not follow the table model (or the host is not x86)");
+    if (23u - info[0] > kX86LdsBits)  // the multi-volume walkers stage the rcp table in LDS
+        return fail(c, VPX_E_STATE, "the host's rcpss key is wider than the LDS-staged table allows");
     std::vector<uint32_t> tab(info[3]);
     if (vpx_x86_arith_tables(tab.data(), tab.size(), info) != VPX_OK) return fail(c, VPX_E_STATE, "table capture failed");
     VPX_HIP(c, hipMalloc(&c->d_x86, sizeof(uint32_t) * tab.size()));

@@ -309,14 +309,42 @@ struct ORay {
 // (xa.tab set, wave-uniform): FastReciprocal = rcpps + one Newton step, (r + r) - D * (r * r)
 // (renderer.cpp:929-934, :969), rcpps from the host's captured table (vpx_x86.hpp) — a zero
 // component gives inf * 0 = NaN there, as on the host.
-__device__ __forceinline__ float fast_reciprocal1(float x, const X86Arith& xa) {
-    const float r = __uint_as_float(x86_rcp_bits(__float_as_uint(x), xa.tab, xa.rcp_shift));
+__device__ __forceinline__ float fast_reciprocal1(float x, uint32_t t) {  // t: x's table entry
+    const float r = __uint_as_float(x86_rcp_from(__float_as_uint(x), t));
     const float muls = x * (r * r);
     return (r + r) - muls;
 }
-__device__ __forceinline__ f3 nearest_rd(f3 d, const X86Arith& xa) {
+// The multi-volume walkers look the rcp table up once per component of every volume visit
+// (C4: up to 64 instance visits per wave), and from global memory each lookup is an L2 round
+// trip ahead of Setup3DDDA (C4 47.3 vs 42.4 ms per step).  These kernels stage the rcp part of
+// the table (2^(23 - rcp_shift) words: 16 KiB for the 12-bit key of the AMD EPYC host, 8 KiB for
+// the 11-bit Intel key; vpx_set_arithmetic refuses keys wider than kX86LdsBits) into their
+// dynamic LDS once per workgroup and read it there.  Call before any early return (barrier).
+constexpr uint32_t kX86LdsBits = 13;
+__device__ __forceinline__ X86Arith x86_stage_lds(const X86Arith& xa, uint32_t* lds) {
+    X86Arith o = xa;
 #ifndef VPX_NO_X86
-    if (xa.tab) return mk(fast_reciprocal1(d.x, xa), fast_reciprocal1(d.y, xa), fast_reciprocal1(d.z, xa));
+    if (xa.tab) {
+        for (uint32_t i = threadIdx.x; i < xa.rsq_off; i += blockDim.x) lds[i] = xa.tab[i];
+        __syncthreads();
+        o.tab = lds;
+    }
+#endif
+    return o;
+}
+__device__ __forceinline__ f3 nearest_rd(f3 d, const X86Arith& xa) {
+#if !defined(VPX_NO_X86) && !defined(VPX_DEBUG_X86_NO_RCP)  // (the debug hook: a timing probe, wrong results)
+    if (xa.tab) {  // the three entries' loads issued together, then the branch-free results
+        const uint32_t tx = xa.tab[x86_rcp_key(__float_as_uint(d.x), xa.rcp_shift)];
+        const uint32_t ty = xa.tab[x86_rcp_key(__float_as_uint(d.y), xa.rcp_shift)];
+        const uint32_t tz = xa.tab[x86_rcp_key(__float_as_uint(d.z), xa.rcp_shift)];
+#ifdef VPX_DEBUG_X86_WORK_EXACT  // timing probe: the table work done, the exact values used
+        const f3 fr = mk(fast_reciprocal1(d.x, tx), fast_reciprocal1(d.y, ty), fast_reciprocal1(d.z, tz));
+        return mk(__fdiv_rn(1.0f, d.x) + 0.0f * fr.x, __fdiv_rn(1.0f, d.y) + 0.0f * fr.y,
+                  __fdiv_rn(1.0f, d.z) + 0.0f * fr.z);
+#endif
+        return mk(fast_reciprocal1(d.x, tx), fast_reciprocal1(d.y, ty), fast_reciprocal1(d.z, tz));
+    }
 #endif
     return mk(__fdiv_rn(1.0f, d.x), __fdiv_rn(1.0f, d.y), __fdiv_rn(1.0f, d.z));
 }
@@ -476,8 +504,9 @@ constexpr uint32_t kRunFrameShadow = VPX_RUN_FRAME_SHADOW;
 // words (A/B overrides: VPX_*_POOL).  With the pool's registers the shadow walks take the
 // two-compare step without spilling: C3 3.684-3.719 vs 3.724-3.756 ms (three interleaved runs,
 // round 3; skip weight 2 / 8 or skip minimum 2 on top: 3.70-3.73 / 3.70-3.72 / 3.77-3.78).
-// The bounce pool keeps the tile walker's words: seg2, skip weight 1 / 4, runs of 3 cells in
-// two passes measured C2 2.63-2.66 / 2.60-2.64 / 2.66-2.75 / 2.65-2.71 vs 2.59-2.65 ms.
+// The bounce pool takes the bounce words (kRunBounce, kSkipwBounce, kMincBounce): seg2, skip
+// weight 1 / 4, runs of 3 cells in two passes measured C2 2.63-2.66 / 2.60-2.64 / 2.66-2.75 /
+// 2.65-2.71 vs 2.59-2.65 ms, and re-checked at three lanes in round 5 (within noise).
 #ifndef VPX_RUN_SHADOW_POOL
 #define VPX_RUN_SHADOW_POOL (3u | 1u << 8 | 1u << 17 | 1u << 18)
 #endif
@@ -487,19 +516,8 @@ constexpr uint32_t kRunFrameShadow = VPX_RUN_FRAME_SHADOW;
 #ifndef VPX_MINC_SHADOW_POOL
 #define VPX_MINC_SHADOW_POOL 1u
 #endif
-#ifndef VPX_RUN_BOUNCE_POOL
-#define VPX_RUN_BOUNCE_POOL (4u | 1u << 8 | 0u << 17 | 1u << 18)
-#endif
-#ifndef VPX_SKIPW_BOUNCE_POOL
-#define VPX_SKIPW_BOUNCE_POOL 2u
-#endif
-#ifndef VPX_MINC_BOUNCE_POOL
-#define VPX_MINC_BOUNCE_POOL 2u
-#endif
 constexpr uint32_t kRunShadowPool = VPX_RUN_SHADOW_POOL, kSkipwShadowPool = VPX_SKIPW_SHADOW_POOL,
                    kMincShadowPool = VPX_MINC_SHADOW_POOL;
-constexpr uint32_t kRunBouncePool = VPX_RUN_BOUNCE_POOL, kSkipwBouncePool = VPX_SKIPW_BOUNCE_POOL,
-                   kMincBouncePool = VPX_MINC_BOUNCE_POOL;
 #ifdef VPX_ASM_MARKS  // analysis builds only: label the walk phases in the ISA listing
 #define VPX_MARK(s) asm volatile("; MARK " s)
 #else
@@ -929,7 +947,17 @@ __device__ __forceinline__ bool find_nearest_rest(const SceneView& sv, Ray& r, C
     const int32_t vox0 = vox;
     uint32_t hx = 0, hy = 0, hz = 0;
     auto visit = [&](uint32_t i) {  // i is wave-uniform (for_volumes / the linear loop)
+#ifdef VPX_PHASE_PROF  // instance visits: waves, lanes, lanes past the sphere cull, lanes past Setup3DDDA
+        const uint64_t vb0 = __ballot(true);
+        const bool lead = (threadIdx.x & 63u) == (uint32_t)__ffsll((unsigned long long)vb0) - 1u;
+        if (lead) atomicAdd(&g_phase[10], 1ull), atomicAdd(&g_phase[11], (unsigned long long)__popcll(vb0));
+        const bool mv = misses_volume(ldu(sv.vbounds, i), r.O, r.D);
+        const uint64_t vb1 = __ballot(!mv);
+        if (lead) atomicAdd(&g_phase[12], (unsigned long long)__popcll(vb1));
+        if (mv) return true;
+#else
         if (misses_volume(ldu(sv.vbounds, i), r.O, r.D)) return true;
+#endif
         const vpx_volume vol = ldu(sv.volumes, i);
         const DevGrid g = ldu(sv.grids, vol.grid_id);
         skip::Walk w;
@@ -939,7 +967,15 @@ __device__ __forceinline__ bool find_nearest_rest(const SceneView& sv, Ray& r, C
             o.D = xform_vec_ssem(r.D, vol.inv_matrix);
             o.rD = nearest_rd(o.D, sv.x86);
             Dda s;
+#ifdef VPX_PHASE_PROF
+            const bool ok = dda_setup(vol, g.n, o, s);
+            const uint64_t vb2 = __ballot(ok);
+            if ((threadIdx.x & 63u) == (uint32_t)__ffsll((unsigned long long)__ballot(true)) - 1u)
+                atomicAdd(&g_phase[13], (unsigned long long)__popcll(vb2)), atomicAdd(&g_phase[14], vb2 ? 1ull : 0ull);
+            if (!ok) return true;
+#else
             if (!dda_setup(vol, g.n, o, s)) return true;
+#endif
             w = to_walk(s);
         }
         if (walk_wave<0, SKIPW, MINC, RUN>(grid_view(g), w, r.t, k.cells)) {

@@ -186,6 +186,9 @@ __device__ __forceinline__ uint32_t live_path(const WaveBufs& w, int level, uint
 // 0x7F)) (tmpl8math.h:2356-2360, renderer.cpp:1735-1765), the dot product summed
 // (x*x + y*y) + z*z as dpps does, rsqrtps from the host's captured table (vpx_x86.hpp).
 __device__ __forceinline__ Ray primary_make_ray(f3 o, f3 dir, const X86Arith& xa, bool x86) {
+#ifdef VPX_DEBUG_X86_NO_RSQ  // timing probe only (wrong results)
+    x86 = false;
+#endif
     if (!x86) return make_ray(o, dir);
     Ray r = make_ray(o, dir);
     const float dp = (dir.x * dir.x + dir.y * dir.y) + dir.z * dir.z;
@@ -978,20 +981,9 @@ __global__ __launch_bounds__(256) void k_compact(WaveBufs w, int level) {
     }
 }
 
-// The instance walks' words (FindNearest in the instance grids, k_instances): the heads' words
-// measured best (C4 42.39-42.44 ms; skip minimum 1 / 3: 42.76-42.87 / 42.37-42.51, two passes
-// 42.46-42.56, skip weight 2 42.31-42.37 — two interleaved runs, noise).
-#ifndef VPX_RUN_INST_NEAREST
-#define VPX_RUN_INST_NEAREST VPX_RUN_NEAREST
-#endif
-#ifndef VPX_MINC_INST_NEAREST
-#define VPX_MINC_INST_NEAREST VPX_MINC_NEAREST
-#endif
-#ifndef VPX_SKIPW_INST_NEAREST
-#define VPX_SKIPW_INST_NEAREST 1u
-#endif
-constexpr uint32_t kRunInstNearest = VPX_RUN_INST_NEAREST, kMincInstNearest = VPX_MINC_INST_NEAREST,
-                   kSkipwInstNearest = VPX_SKIPW_INST_NEAREST;
+// The instance walks (FindNearest in the instance grids, k_instances) take the heads' words:
+// skip minimum 1 / 3, two passes and skip weight 2 measured within noise of them (C4 42.31-42.87
+// vs 42.39-42.44 ms, two interleaved runs each, round 5).
 
 // Multi-volume primary rays in two launches: the world (volume 0, first in the reference's
 // loop) walked by the lean single-volume head (k_primary<true, false>: 6 waves/SIMD, no
@@ -1009,10 +1001,13 @@ constexpr uint32_t kRunInstNearest = VPX_RUN_INST_NEAREST, kMincInstNearest = VP
 // vs 42.90-43.09 ms per step (three interleaved runs): most C4 rays are candidates, and the
 // pass's HBM traffic is mostly the shade's three area-light slots per pixel (144 B), which the
 // shadow pool reads back, not the rays it re-reads.
-__global__ __launch_bounds__(256) VPX_WPE(VPX_WPE_MULTI_NEAREST) void k_instances(SceneView sv, FrameArgs f, WaveBufs w,
+__global__ __launch_bounds__(256) VPX_WPE(VPX_WPE_MULTI_NEAREST) void k_instances(SceneView sv_, FrameArgs f, WaveBufs w,
                                                                                 unsigned long long* __restrict__ ctr) {
     __shared__ uint32_t sh[4];
     __shared__ uint32_t lst[256];
+    extern __shared__ uint32_t x86_lds[];  // the rcp table in reference arithmetic (x86_stage_lds)
+    SceneView sv = sv_;
+    sv.x86 = x86_stage_lds(sv_.x86, x86_lds);
     const uint32_t tb = tile_block() * 256u;
     const uint32_t p = tb + threadIdx.x;
     const PathRay pr{w.O, w.D, w.H, w.HM, 0u};
@@ -1045,7 +1040,7 @@ __global__ __launch_bounds__(256) VPX_WPE(VPX_WPE_MULTI_NEAREST) void k_instance
         r.mat = hm & 0xffu;
         r.inside = (hm & 0x80000000u) != 0u;
         int32_t vox = (int32_t)((hm >> 8) & 0xffffu) - 2;
-        if (find_nearest_rest<kSkipwInstNearest, kMincInstNearest, kRunInstNearest>(sv, r, k, &vox)) {
+        if (find_nearest_rest(sv, r, k, &vox)) {
             w.H[q] = make_float4(r.t, r.N.x, r.N.y, r.N.z);
             w.HM[q] = r.mat | ((uint32_t)(vox + 2) << 8) | (r.inside ? 0x80000000u : 0u);
         }
@@ -1071,8 +1066,11 @@ __global__ __launch_bounds__(256) VPX_WPE(VPX_WPE_MULTI_NEAREST) void k_instance
 // every wave is full — a tile's compaction left a deep level's few rays spread
 // one or two per wave over the frame's 8100 tiles (Z1: 14 levels, 2 M paths at level 1, 4 k at
 // level 14, each launch scanning all 2 M).  `level` is the shade level whose rays it walks.
-__global__ __launch_bounds__(256) VPX_WPE(VPX_WPE_MULTI_NEAREST) void k_nearest_tile(SceneView sv, WaveBufs w, int level,
+__global__ __launch_bounds__(256) VPX_WPE(VPX_WPE_MULTI_NEAREST) void k_nearest_tile(SceneView sv_, WaveBufs w, int level,
                                                                                     unsigned long long* __restrict__ ctr) {
+    extern __shared__ uint32_t x86_lds[];
+    SceneView sv = sv_;
+    sv.x86 = x86_stage_lds(sv_.x86, x86_lds);
     Counters k{0u, 0u, 0u};
     const uint32_t n = live_count(w, level + 1);
     const uint32_t lane = threadIdx.x & 63u;
@@ -1167,7 +1165,7 @@ __global__ __launch_bounds__(kPoolWg) VPX_WPE(VPX_WPE_BOUNCE) void k_nearest_poo
             avail -= take;
         }
         if (!__ballot(q != ~0u)) break;  // the list is done and every lane is done
-        walk_wave<0, kSkipwBouncePool, kMincBouncePool, kRunBouncePool, true>(gv, wk, kBig, k.cells, &mode,
+        walk_wave<0, kSkipwBounce, kMincBounce, kRunBounce, true>(gv, wk, kBig, k.cells, &mode,
                                                                    more ? kPoolLeave : 65u);
     }
     flush_counters(k, 0u, ctr, VPX_STAGE_BOUNCE);
@@ -1417,20 +1415,10 @@ __global__ __launch_bounds__(kPoolWg) VPX_WPE(VPX_WPE_SPOOL) void k_shadow_pool(
 #ifndef VPX_INST_CULL
 #define VPX_INST_CULL 1
 #endif
-#ifndef VPX_RUN_INST_SHADOW
-#define VPX_RUN_INST_SHADOW VPX_RUN_SHADOW
-#endif
-#ifndef VPX_SKIPW_INST_SHADOW
-#define VPX_SKIPW_INST_SHADOW 4u
-#endif
-// Skip minimum 2 (cubes of one brick stepped through) for the instance grids' shadow walks:
-// C4 42.43-42.51 vs 42.71-42.96 ms (five interleaved runs, all won; 3: 42.82-42.90, 4:
-// 43.05-43.26; two passes per iteration 43.1-43.3, the two-compare step 42.7-42.8).
-#ifndef VPX_MINC_INST_SHADOW
-#define VPX_MINC_INST_SHADOW 2u
-#endif
-constexpr uint32_t kRunInstShadow = VPX_RUN_INST_SHADOW, kSkipwInstShadow = VPX_SKIPW_INST_SHADOW,
-                   kMincInstShadow = VPX_MINC_INST_SHADOW;
+// The instance grids' shadow walks take the shadow words with skip minimum 2 (cubes of one
+// brick stepped through): C4 42.43-42.51 vs 42.71-42.96 ms (five interleaved runs, all won; 3:
+// 42.82-42.90, 4: 43.05-43.26; two passes per iteration 43.1-43.3, the two-compare step 42.7-42.8).
+constexpr uint32_t kMincInstShadow = 2u;
 __device__ __forceinline__ bool occluded_instances(const SceneView& sv, const float4* vb, const Ray& r, Counters& k) {
     const uint32_t nv = sv.num_volumes;
     uint64_t cand = 0ull;
@@ -1460,7 +1448,7 @@ __device__ __forceinline__ bool occluded_instances(const SceneView& sv, const fl
         Dda s;
         if (!dda_setup(vol, g.n, o, s)) continue;
         skip::Walk wk = to_walk(s);
-        occ = walk_wave<16, kSkipwInstShadow, kMincInstShadow, kRunInstShadow>(grid_view(g), wk, r.t, k.cells);
+        occ = walk_wave<16, kSkipwShadow, kMincInstShadow, kRunShadow>(grid_view(g), wk, r.t, k.cells);
     }
     if (occ) return true;
     for (uint32_t i = 0; i < sv.num_spheres; ++i)
@@ -1660,12 +1648,15 @@ __global__ __launch_bounds__(256) void k_resolve_finish(SceneView sv, FrameArgs 
 // paths (Z1 at 1920x1080: 192 k at level 5, 3.7 k at level 14), so the kernel's registers (the
 // whole chain inlined) and low occupancy cost little, while each of those levels cost ~0.2 ms
 // of launches and latency chains in the per-level kernels.
-__global__ __launch_bounds__(256) VPX_WPE(2) void k_tail(SceneView sv, FrameArgs f, WaveBufs w, int level,
+__global__ __launch_bounds__(256) VPX_WPE(2) void k_tail(SceneView sv_, FrameArgs f, WaveBufs w, int level,
                                                       unsigned long long* __restrict__ ctr) {
     Counters kn{0u, 0u, 0u}, ks{0u, 0u, 0u}, kh{0u, 0u, 0u};
     const uint32_t n = live_count(w, level);
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-    if (blockIdx.x * 256u >= n) return;
+    if (blockIdx.x * 256u >= n) return;  // (workgroup-uniform: before the staging barrier)
+    extern __shared__ uint32_t x86_lds[];
+    SceneView sv = sv_;
+    sv.x86 = x86_stage_lds(sv_.x86, x86_lds);
     const uint32_t p = i < n ? live_path(w, level, i) : ~0u;
     const PathRay pr{w.O, w.D, w.H, w.HM, 0u};
     for (int l = level; p != ~0u; ++l) {

@@ -38,28 +38,41 @@ struct X86Arith {
 // rcpss(x) as bits: the table holds rcp(1.m) for the key's mantissas; the exponent moves the
 // result by 2^-(e - 127).  Zero / denormal -> signed infinity, infinity -> signed zero, NaN ->
 // the quieted NaN, results below the normal range -> signed zero (flush).
-VPX_HDX uint32_t x86_rcp_bits(uint32_t u, const uint32_t* tab, uint32_t shift) {
+// Split in two so that a caller can issue the table loads of several inputs before using any
+// (the key is a valid index for every input, specials included): x86_rcp_key gives the index,
+// x86_rcp_from the result from the input and its entry t, branch-free.
+VPX_HDX uint32_t x86_rcp_key(uint32_t u, uint32_t shift) { return (u & 0x7fffffu) >> shift; }
+VPX_HDX uint32_t x86_rcp_from(uint32_t u, uint32_t t) {
     const uint32_t s = u & 0x80000000u, e = (u >> 23) & 0xffu, m = u & 0x7fffffu;
-    if (e == 0u) return s | 0x7f800000u;
-    if (e == 255u) return m ? (u | 0x400000u) : s;
-    const uint32_t t = tab[m >> shift];
     const int32_t ne = (int32_t)((t >> 23) & 0xffu) + 127 - (int32_t)e;
-    return ne <= 0 ? s : (s | ((uint32_t)ne << 23) | (t & 0x7fffffu));
+    uint32_t r = ne <= 0 ? s : (s | ((uint32_t)ne << 23) | (t & 0x7fffffu));
+    r = e == 0u ? (s | 0x7f800000u) : r;
+    r = e == 255u ? (m ? (u | 0x400000u) : s) : r;
+    return r;
+}
+VPX_HDX uint32_t x86_rcp_bits(uint32_t u, const uint32_t* tab, uint32_t shift) {
+    return x86_rcp_from(u, tab[x86_rcp_key(u, shift)]);
 }
 
 // rsqrtss(x) as bits: the table holds rsqrt of [1, 4) (parity 1 = [2, 4)); an even exponent
 // step 2q moves the result by 2^-q.  +-0 / denormals -> signed infinity, negative -> the
-// default NaN, +inf -> +0, NaN -> the quieted NaN.
-VPX_HDX uint32_t x86_rsq_bits(uint32_t u, const uint32_t* tab, uint32_t shift) {
+// default NaN, +inf -> +0, NaN -> the quieted NaN.  (Key and result split as for rcp.)
+VPX_HDX uint32_t x86_rsq_key(uint32_t u, uint32_t shift) {
+    const uint32_t par = ((u >> 23) & 1u) ^ 1u;  // (e - 127) odd: the [2, 4) half
+    return ((par << 23) | (u & 0x7fffffu)) >> shift;
+}
+VPX_HDX uint32_t x86_rsq_from(uint32_t u, uint32_t t) {
     const uint32_t e = (u >> 23) & 0xffu, m = u & 0x7fffffu;
-    if (e == 0u) return (u & 0x80000000u) | 0x7f800000u;
-    if (e == 255u && m) return u | 0x400000u;
-    if (u & 0x80000000u) return 0xffc00000u;
-    if (e == 255u) return 0u;
-    const uint32_t par = (e & 1u) ^ 1u;  // (e - 127) odd: the [2, 4) half
-    const uint32_t t = tab[((par << 23) | m) >> shift];
+    const uint32_t par = (e & 1u) ^ 1u;
     const int32_t q = ((int32_t)e - 127 - (int32_t)par) / 2;  // exact: the difference is even
-    return ((uint32_t)((int32_t)((t >> 23) & 0xffu) - q) << 23) | (t & 0x7fffffu);
+    uint32_t r = ((uint32_t)((int32_t)((t >> 23) & 0xffu) - q) << 23) | (t & 0x7fffffu);
+    r = (u & 0x80000000u) ? 0xffc00000u : r;
+    r = e == 255u ? (m ? (u | 0x400000u) : ((u & 0x80000000u) ? 0xffc00000u : 0u)) : r;
+    r = e == 0u ? ((u & 0x80000000u) | 0x7f800000u) : r;
+    return r;
+}
+VPX_HDX uint32_t x86_rsq_bits(uint32_t u, const uint32_t* tab, uint32_t shift) {
+    return x86_rsq_from(u, tab[x86_rsq_key(u, shift)]);
 }
 
 }  // namespace vpx

@@ -32,3 +32,7 @@ for name, off in (("nearest", 0), ("shadow", 16)):
           f"cyc/iter={cs / max(ns, 1):.0f} | skip: cycles={ck:.3e} iters={nk} lanes/iter={lk / max(nk, 1):.1f} "
           f"cyc/iter={ck / max(nk, 1):.0f} | per walk: step it={ns / walks:.1f} skip it={nk / walks:.1f} | "
           f"refused lanes/iter={fb / max(nk, 1):.2f} | finished lanes/step iter={cf / max(ns, 1):.1f}")
+v = list(ph)
+if v[10]:
+    print(f"[instances] wave visits={v[10]} lane visits={v[11]} ({v[11] / v[10]:.1f}/wave visit) past sphere cull={v[12]} "
+          f"past Setup3DDDA={v[13]} wave visits with a walk={v[14]}")
