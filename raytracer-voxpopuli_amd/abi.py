@@ -183,6 +183,7 @@ SIGNATURES = {
     "vpx_camera_look_at": (C.c_int, [C.POINTER(C.c_float), C.POINTER(C.c_float), C.c_uint32, C.c_uint32,
                                      C.POINTER(Camera)]),
     "vpx_volume_set_transform": (C.c_int, [C.POINTER(C.c_float)] * 3 + [C.POINTER(Volume)]),
+    "vpx_volume_bounds": (C.c_int, [C.POINTER(Volume), C.POINTER(C.c_float)]),
     "vpx_default_materials": (C.c_int, [C.POINTER(Material)]),
     "vpx_pixel_seed": (C.c_uint32, [C.c_uint32] * 6),
     "vpx_bvh_set": (C.c_int, [C.c_void_p, C.POINTER(BvhTri), C.c_uint32]),

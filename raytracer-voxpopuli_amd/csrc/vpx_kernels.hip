@@ -1665,6 +1665,13 @@ int vpx_set_volumes(vpx_ctx* c, const vpx_volume* v, uint32_t count) {
     return build_tlas(c, bounds);
 }
 
+int vpx_volume_bounds(const vpx_volume* v, float out[4]) {
+    if (!v || !out) return VPX_E_INVALID;
+    const float4 b = volume_bounds(*v);
+    out[0] = b.x, out[1] = b.y, out[2] = b.z, out[3] = b.w;
+    return VPX_OK;
+}
+
 int vpx_set_materials(vpx_ctx* c, const vpx_material* m, uint32_t count) {
     VPX_GROUP_ALL(c, vpx_set_materials(m_, m, count));
     if (!c || !m) return fail(c, VPX_E_INVALID, "null argument");
