@@ -497,12 +497,14 @@ uint32_t vpx_bvh_depth(const vpx_bvh_node* nodes, uint32_t nodes_used);
    xorshift32 state *seed (advanced; the three draws of a float3 taken left to right —
    C++ leaves that order unspecified). */
 int vpx_bvh_random_tris(uint32_t* seed, vpx_bvh_tri out[64]);
-/* The world bounding sphere the device culls a volume's walks with (no reference counterpart:
-   the reference tests every volume in Renderer::FindNearest / IsOccluded, renderer.cpp:209-243,
-   946-1018): out = (centre x, y, z, radius^2) of the cube b0..b1 mapped by the inverse of the
-   affine part of inv_matrix (rows 0-2, as TransformPosition reads it), inflated by 0.1 % of the
-   radius + 1e-3 of the scale; radius^2 = +inf when the 3x3 part is singular (never culled). */
-int vpx_volume_bounds(const vpx_volume* v, float out[4]);
+/* The world box the device culls a volume's walks with (no reference counterpart: the
+   reference sets up every volume in Renderer::FindNearest / IsOccluded, renderer.cpp:209-243,
+   946-1018): out = (lo x, y, z, hi x, y, z), the box of the cube b0..b1's corners mapped by the
+   inverse of the affine part of inv_matrix (rows 0-2, as TransformPosition reads it), padded by
+   0.1 % of the half-diagonal + 1e-3 of the scale and rounded outward; +-inf when the 3x3 part
+   is singular (never culled).  A ray's segment [0, t] that misses the box reads no cell of the
+   volume in the reference's loop. */
+int vpx_volume_bounds(const vpx_volume* v, float out[6]);
 
 #ifdef __cplusplus
 }

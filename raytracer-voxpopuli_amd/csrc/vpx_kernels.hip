@@ -453,7 +453,7 @@ struct vpx_ctx {
     uint32_t d_grids_cap = 0;
     std::vector<vpx_volume> volumes;
     vpx_volume* d_volumes = nullptr;
-    float4* d_vbounds = nullptr;  // per volume: world bounding sphere (centre, radius^2), see volume_bounds
+    float4* d_vbounds = nullptr;  // per volume: its cube's inflated world box (lo, hi), see volume_bounds
     void* d_tlas = nullptr;       // instance TLAS: nodes, then the leaf volume list (build_tlas)
     uint32_t tlas_nodes = 0;
     bool tlas_on = false;
@@ -1510,23 +1510,24 @@ int vpx_grid_checksum(vpx_ctx* c, uint32_t id, uint64_t* out) {
     return VPX_OK;
 }
 
-// World-space bounding sphere of a volume's cube, for the volume cull in find_nearest /
-// is_occluded: the cube [b0, b1] mapped by the inverse of inv_matrix (the matrix the walk
-// actually uses, inverted in double), inflated far beyond float rounding (0.1 % of the
-// radius + 1e-3 of the scale) so a ray that misses it also misses the cube in the
-// reference's float arithmetic.  A singular or non-affine inv_matrix disables the cull.
-static float4 volume_bounds(const vpx_volume& v) {
+// The world box a volume's walks are culled with (misses_volume, the TLAS): the cube b0..b1
+// through the inverse of inv_matrix's affine part (rows 0-2: every transform of the path —
+// xform_pos_ssem / xform_pos, TransformPosition(_SSEM), tmpl8math.cpp:345-402 — reads only
+// those; SetTransform's inverse leaves m[15] = 1 +- 1 ulp on a third of C4's instances), its 8
+// corners in double, padded by 0.1 % of the half-diagonal + 1e-3 of the scale and rounded
+// outward to float, so that the reference's float cube test (Setup3DDDA) can only succeed, and
+// its walk only read a cell, for rays whose segment meets the box.  A singular 3x3 part gives
+// an infinite box (never culled).  [0] = lo, [1] = hi (w = 0).
+struct VolBox {
+    float4 lo, hi;
+};
+static VolBox volume_bounds(const vpx_volume& v) {
     const float* m = v.inv_matrix;
     const double a[3][3] = {{m[0], m[1], m[2]}, {m[4], m[5], m[6]}, {m[8], m[9], m[10]}};
     const double det = a[0][0] * (a[1][1] * a[2][2] - a[1][2] * a[2][1]) -
                        a[0][1] * (a[1][0] * a[2][2] - a[1][2] * a[2][0]) +
                        a[0][2] * (a[1][0] * a[2][1] - a[1][1] * a[2][0]);
-    const float4 none = make_float4(0.f, 0.f, 0.f, INFINITY);
-    // Every transform of the path is affine in rows 0-2 (xform_pos_ssem / xform_pos read m[0..11],
-    // as TransformPosition(_SSEM) does, tmpl8math.cpp:345-402), so the bottom row plays no part:
-    // SetTransform's inverse leaves m[15] = 1 +- 1 ulp on a third of C4's rotated instances, and
-    // requiring it to be exactly (0, 0, 0, 1) had put them in the TLAS's always-set, unculled
-    // (every C4 primary ray set up ~20 instance walks that Setup3DDDA then refused).
+    const VolBox none{make_float4(-INFINITY, -INFINITY, -INFINITY, 0.f), make_float4(INFINITY, INFINITY, INFINITY, 0.f)};
     if (!(std::fabs(det) > 1e-30)) return none;
     double r[3][3];  // inverse of the 3x3 part
     r[0][0] = (a[1][1] * a[2][2] - a[1][2] * a[2][1]) / det;
@@ -1539,33 +1540,44 @@ static float4 volume_bounds(const vpx_volume& v) {
     r[2][1] = (a[0][1] * a[2][0] - a[0][0] * a[2][1]) / det;
     r[2][2] = (a[0][0] * a[1][1] - a[0][1] * a[1][0]) / det;
     const double t[3] = {m[3], m[7], m[11]};
-    double pts[8][3], cen[3] = {0, 0, 0};
+    double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
     for (int k = 0; k < 8; ++k) {
         const double q[3] = {(k & 1) ? v.b1[0] : v.b0[0], (k & 2) ? v.b1[1] : v.b0[1], (k & 4) ? v.b1[2] : v.b0[2]};
         for (int i = 0; i < 3; ++i) {
-            pts[k][i] = r[i][0] * (q[0] - t[0]) + r[i][1] * (q[1] - t[1]) + r[i][2] * (q[2] - t[2]);
-            cen[i] += pts[k][i] / 8.0;
+            const double p = r[i][0] * (q[0] - t[0]) + r[i][1] * (q[1] - t[1]) + r[i][2] * (q[2] - t[2]);
+            lo[i] = std::min(lo[i], p), hi[i] = std::max(hi[i], p);
         }
     }
-    double rad = 0.0;
-    for (int k = 0; k < 8; ++k)
-        rad = std::max(rad, std::sqrt((pts[k][0] - cen[0]) * (pts[k][0] - cen[0]) + (pts[k][1] - cen[1]) * (pts[k][1] - cen[1]) +
-                                      (pts[k][2] - cen[2]) * (pts[k][2] - cen[2])));
-    const double scale = 1.0 + std::fabs(cen[0]) + std::fabs(cen[1]) + std::fabs(cen[2]) + rad;
-    const double rr = rad * 1.001 + 1e-3 * scale;
-    if (!std::isfinite(rr)) return none;
-    return make_float4((float)cen[0], (float)cen[1], (float)cen[2], (float)(rr * rr));
+    double half = 0.0, cen = 0.0;
+    for (int i = 0; i < 3; ++i) {
+        half += (hi[i] - lo[i]) * (hi[i] - lo[i]) / 4.0;
+        cen += std::fabs((lo[i] + hi[i]) / 2.0);
+    }
+    half = std::sqrt(half);
+    const double pad = half * 1e-3 + 1e-3 * (1.0 + cen + half);
+    VolBox b;
+    float* out[2] = {&b.lo.x, &b.hi.x};
+    for (int i = 0; i < 3; ++i) {
+        if (!std::isfinite(lo[i] - pad) || !std::isfinite(hi[i] + pad)) return none;
+        out[0][i] = std::nextafter((float)(lo[i] - pad), -INFINITY);
+        out[1][i] = std::nextafter((float)(hi[i] + pad), INFINITY);
+    }
+    b.lo.w = b.hi.w = 0.f;
+    return b;
 }
 
 // Instance TLAS (the C4 lattice of 64 instances over the world volume): a BVH over the
-// inflated world bounding spheres (volume_bounds) of volumes 1..n-1, built once per
+// inflated world boxes (volume_bounds) of volumes 1..n-1, built once per
 // vpx_set_volumes (volume 0, first in the reference's loop, is walked before the tree is
 // asked, so the instances' candidates are bounded by its hit).
-// Boxes are the spheres' AABBs widened by a further 1e-4 of the scale and rounded outward
-// to float, so every volume misses_volume keeps is a candidate.  Median split on the
+// Boxes are the volumes' boxes widened by a further 1e-4 of the scale and rounded outward to
+// float, so every volume misses_volume keeps is a candidate.  Median split on the
 // longest centroid axis (ties by index), leaves of <= 4 volumes (their bit mask), nodes in
 // depth-first order with skip links (TlasNode).  Volumes without finite bounds go to the
 // always-set.
+#ifndef VPX_TLAS_LEAF
+#define VPX_TLAS_LEAF 4  // volumes per TLAS leaf
+#endif
 struct TlasBuild {
     std::vector<TlasNode> nodes;
     struct Item {
@@ -1588,7 +1600,7 @@ struct TlasBuild {
             nd.lo[k] = std::nextafter((float)lo[k], -INFINITY);
             nd.hi[k] = std::nextafter((float)hi[k], INFINITY);
         }
-        if (count <= 4) {
+        if (count <= (uint32_t)VPX_TLAS_LEAF) {
             nd.leaf = 1;
             for (uint32_t i = first; i < first + count; ++i) nd.mask |= 1ull << (items[i].id - 1u);
             nodes[me] = nd;
@@ -1607,7 +1619,7 @@ struct TlasBuild {
     }
 };
 
-int build_tlas(vpx_ctx* c, const std::vector<float4>& bounds) {
+int build_tlas(vpx_ctx* c, const std::vector<VolBox>& bounds) {
     c->tlas_on = false;
     c->tlas_nodes = 0;
     c->tlas_always = 0;
@@ -1615,15 +1627,18 @@ int build_tlas(vpx_ctx* c, const std::vector<float4>& bounds) {
     if (count < 2 || count > kTlasMaxVolumes) return VPX_OK;  // one volume / too many: the linear loop
     TlasBuild b;
     for (uint32_t i = 1; i < count; ++i) {  // volume 0 is walked first, outside the tree
-        const float4 s = bounds[i];
-        if (!std::isfinite(s.w)) {
+        const VolBox& vb = bounds[i];
+        const double lo[3] = {vb.lo.x, vb.lo.y, vb.lo.z}, hi[3] = {vb.hi.x, vb.hi.y, vb.hi.z};
+        if (!std::isfinite(lo[0] + lo[1] + lo[2] + hi[0] + hi[1] + hi[2])) {
             c->tlas_always |= 1ull << (i - 1u);
             continue;
         }
-        const double r = std::sqrt((double)s.w), cc[3] = {s.x, s.y, s.z};
-        const double pad = r * 1e-4 + 1e-4 * (1.0 + std::fabs(cc[0]) + std::fabs(cc[1]) + std::fabs(cc[2]) + r);
+        double half = 0.0, cen = 0.0;
+        for (int k = 0; k < 3; ++k) half += (hi[k] - lo[k]) * (hi[k] - lo[k]) / 4.0, cen += std::fabs((lo[k] + hi[k]) / 2.0);
+        half = std::sqrt(half);
+        const double pad = half * 1e-4 + 1e-4 * (1.0 + cen + half);
         TlasBuild::Item it{};
-        for (int k = 0; k < 3; ++k) it.lo[k] = cc[k] - r - pad, it.hi[k] = cc[k] + r + pad, it.c[k] = cc[k];
+        for (int k = 0; k < 3; ++k) it.lo[k] = lo[k] - pad, it.hi[k] = hi[k] + pad, it.c[k] = (lo[k] + hi[k]) / 2.0;
         it.id = i;
         b.items.push_back(it);
     }
@@ -1648,7 +1663,7 @@ int vpx_set_volumes(vpx_ctx* c, const vpx_volume* v, uint32_t count) {
         c->d_volumes = nullptr;
         c->d_vbounds = nullptr;
         VPX_HIP(c, hipMalloc(&c->d_volumes, sizeof(vpx_volume) * count));
-        VPX_HIP(c, hipMalloc(&c->d_vbounds, sizeof(float4) * count));
+        VPX_HIP(c, hipMalloc(&c->d_vbounds, sizeof(VolBox) * count));
         c->d_volumes_cap = count;
     }
     // Invariant: d_volumes, d_vbounds and the TLAS (d_tlas) describe the same volumes.  The
@@ -1656,19 +1671,19 @@ int vpx_set_volumes(vpx_ctx* c, const vpx_volume* v, uint32_t count) {
     // candidates, k_shadow_inst's slot cull), so a volume update that skipped build_tlas would
     // silently drop instance hits and shadows: every writer of d_volumes goes through here.
     c->volumes.assign(v, v + count);
-    std::vector<float4> bounds(count);
+    std::vector<VolBox> bounds(count);
     for (uint32_t i = 0; i < count; ++i) bounds[i] = volume_bounds(v[i]);
     if (count) {
         VPX_HIP(c, hipMemcpy(c->d_volumes, v, sizeof(vpx_volume) * count, hipMemcpyHostToDevice));
-        VPX_HIP(c, hipMemcpy(c->d_vbounds, bounds.data(), sizeof(float4) * count, hipMemcpyHostToDevice));
+        VPX_HIP(c, hipMemcpy(c->d_vbounds, bounds.data(), sizeof(VolBox) * count, hipMemcpyHostToDevice));
     }
     return build_tlas(c, bounds);
 }
 
-int vpx_volume_bounds(const vpx_volume* v, float out[4]) {
+int vpx_volume_bounds(const vpx_volume* v, float out[6]) {
     if (!v || !out) return VPX_E_INVALID;
-    const float4 b = volume_bounds(*v);
-    out[0] = b.x, out[1] = b.y, out[2] = b.z, out[3] = b.w;
+    const VolBox b = volume_bounds(*v);
+    out[0] = b.lo.x, out[1] = b.lo.y, out[2] = b.lo.z, out[3] = b.hi.x, out[4] = b.hi.y, out[5] = b.hi.z;
     return VPX_OK;
 }
 

@@ -57,7 +57,7 @@ constexpr uint32_t kTlasMaxVolumes = 65;
 #ifndef VPX_TLAS_SLOAD
 #define VPX_TLAS_SLOAD 1  // the instance pass reads the TLAS and its candidates' records with scalar loads
 #endif
-constexpr uint32_t kTlasMaxNodes = 64;
+constexpr uint32_t kTlasMaxNodes = 128;  // 2 x 64 - 1 with one volume per leaf
 struct TlasNode {
     float lo[3];
     uint32_t skip;
@@ -69,7 +69,7 @@ struct TlasNode {
 struct SceneView {
     const DevGrid* grids;
     const vpx_volume* volumes;
-    const float4* vbounds;  // per volume: world bounding sphere (xyz centre, w radius^2), inflated
+    const float4* vbounds;  // per volume: its cube's inflated world AABB, [2i] lo xyz, [2i + 1] hi xyz
     const TlasNode* tlas;   // instance TLAS (global memory; the multi-volume kernels stage it in LDS)
     uint32_t tlas_on, tlas_nodes;
     uint64_t tlas_always;   // instances outside the tree (no finite bounds): always candidates
@@ -798,27 +798,16 @@ struct Counters {
     uint32_t nearest;
 };
 
-// Volume cull: true when the ray's line misses the volume's inflated world bounding sphere,
-// or the sphere lies wholly behind an origin outside it — then the object-space cube test
-// of Setup3DDDA (Cube::Contains / Cube::Intersect, scene.cpp:166-210) fails too, so the
-// reference reads no cell of that volume and skipping it changes nothing.  The margin
-// (vpx_kernels.hip volume_bounds) dwarfs the float rounding of both tests.
-__device__ __forceinline__ bool misses_volume(const float4 b, f3 o, f3 d) {
-    const f3 oc = mk(b.x, b.y, b.z) - o;
-    const float oc2 = dot(oc, oc), bb = dot(oc, d), dd = dot(d, d);
-    const bool outside = oc2 > b.w;
-    return outside && (bb < 0.0f || bb * bb < (oc2 - b.w) * dd);
-}
-
-// Conservative slab test of a TLAS box against the segment o + t d, 0 <= t <= bound: a NaN
-// slab (0 * inf on an axis the ray runs along a box face) never rejects.  A volume whose
-// box starts beyond `bound` is not a candidate: its cube entry lies beyond it too (the box
-// holds the cube with a margin far above float rounding), so the reference's walk of that
-// volume ends before its first cell (`while (s.t < ray.t)`, scene.cpp:761, 1015).
-__device__ __forceinline__ bool tlas_box(const TlasNode& nd, f3 o, f3 inv, float bound) {
+// Conservative slab test of a box against the segment o + t d, 0 <= t <= bound (inv = 1 / d
+// per component, exact): false only when the segment misses the box.  A box that starts
+// beyond `bound` is missed: a cube inside it (with a margin far above float rounding) is
+// entered beyond the bound too, so the reference's walk of that volume ends before its first
+// cell (`while (s.t < ray.t)`, scene.cpp:761, 1015).
+__device__ __forceinline__ bool seg_box(float lx, float ly, float lz, float hx, float hy, float hz, f3 o, f3 inv,
+                                        float bound) {
     float t0 = 0.0f, t1 = bound;
-    const float ta[3] = {(nd.lo[0] - o.x) * inv.x, (nd.lo[1] - o.y) * inv.y, (nd.lo[2] - o.z) * inv.z};
-    const float tb[3] = {(nd.hi[0] - o.x) * inv.x, (nd.hi[1] - o.y) * inv.y, (nd.hi[2] - o.z) * inv.z};
+    const float ta[3] = {(lx - o.x) * inv.x, (ly - o.y) * inv.y, (lz - o.z) * inv.z};
+    const float tb[3] = {(hx - o.x) * inv.x, (hy - o.y) * inv.y, (hz - o.z) * inv.z};
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
         t0 = fmaxf(t0, fminf(ta[k], tb[k]));
@@ -826,13 +815,36 @@ __device__ __forceinline__ bool tlas_box(const TlasNode& nd, f3 o, f3 inv, float
     }
     return !(t1 < t0);
 }
+__device__ __forceinline__ f3 world_inv(f3 d) { return mk(__fdiv_rn(1.0f, d.x), __fdiv_rn(1.0f, d.y), __fdiv_rn(1.0f, d.z)); }
+
+// Volume cull: true when the ray's segment [0, bound] misses the inflated world AABB of the
+// volume's cube (vpx_kernels.hip volume_bounds: the 8 corners through the affine map the
+// walks use, padded and rounded outward) — then Setup3DDDA (Cube::Contains / Cube::Intersect,
+// scene.cpp:166-210) fails, or enters the cube beyond ray.t, and the reference reads no cell of
+// that volume, so skipping it changes nothing.  bound = the ray's t as it stands, which the
+// reference's loop bounds each volume's walk with.  (Until round 6 a bounding sphere and the
+// ray's line: the zone scene's long thin volumes passed ~7 spheres per ray, but ~2 cubes.)
+__device__ __forceinline__ bool misses_volume(const float4* vb, uint32_t i, f3 o, f3 inv, float bound) {
+    const float4 lo = vb[2u * i], hi = vb[2u * i + 1u];
+    return !seg_box(lo.x, lo.y, lo.z, hi.x, hi.y, hi.z, o, inv, bound);
+}
+__device__ __forceinline__ bool misses_volume_u(const float4* vb, uint32_t i, f3 o, f3 inv, float bound) {
+    const float4 lo = ldu(vb, 2u * i), hi = ldu(vb, 2u * i + 1u);  // i wave-uniform: scalar loads
+    return !seg_box(lo.x, lo.y, lo.z, hi.x, hi.y, hi.z, o, inv, bound);
+}
+
+// A TLAS node's box (seg_box): a NaN slab (0 * inf on an axis the ray runs along a box face)
+// yields NaN bounds that fminf / fmaxf drop.
+__device__ __forceinline__ bool tlas_box(const TlasNode& nd, f3 o, f3 inv, float bound) {
+    return seg_box(nd.lo[0], nd.lo[1], nd.lo[2], nd.hi[0], nd.hi[1], nd.hi[2], o, inv, bound);
+}
 
 // The volume loop of Renderer::FindNearest / IsOccluded over the TLAS.  Volume 0 (the world,
 // first in the reference's order) is walked by every lane first; then the wave traverses the
 // tree once, wave-uniform (a node is entered when any lane's segment reaches its box: the
 // ray packet of an 8x8 pixel block), each lane collecting the leaves IT reaches before its
 // bound as it stands after volume 0.  Every volume whose walk the reference would start and
-// read a cell of is among them (boxes hold the inflated bounding spheres of misses_volume,
+// read a cell of is among them (boxes hold the inflated cube boxes of misses_volume,
 // and a box starting beyond the bound holds a cube whose walk ends before its first cell,
 // `while (s.t < ray.t)`, scene.cpp:761, 1015).  The wave then walks the union of the lanes'
 // candidates in increasing index order, each lane only its own — the linear loop restricted
@@ -841,7 +853,7 @@ __device__ __forceinline__ bool tlas_box(const TlasNode& nd, f3 o, f3 inv, float
 // SKIP0: volume 0 was walked already (the instance pass, k_instances, after the world pass):
 // start from the tree with the bound as it stands.
 template <bool SKIP0 = false, class Body>
-__device__ __forceinline__ void for_volumes(const SceneView& sv, f3 o, f3 d, const float& bound, Body body) {
+__device__ __forceinline__ void for_volumes(const SceneView& sv, f3 o, f3 inv, const float& bound, Body body) {
     bool live = true, first = true;
     uint64_t mine = 0, any = 0;  // this lane's / the wave's candidates, bit k = volume k + 1
     for (;;) {
@@ -856,7 +868,6 @@ __device__ __forceinline__ void for_volumes(const SceneView& sv, f3 o, f3 d, con
             first = false;
             mine = sv.tlas_always;
             any = sv.tlas_always;
-            const f3 inv = mk(__fdiv_rn(1.0f, d.x), __fdiv_rn(1.0f, d.y), __fdiv_rn(1.0f, d.z));
             for (uint32_t n = 0; n < sv.tlas_nodes;) {
                 const TlasNode nd = ldu(sv.tlas, n);
                 const bool h = live && tlas_box(nd, o, inv, bound);
@@ -878,13 +889,29 @@ __device__ __forceinline__ void for_volumes(const SceneView& sv, f3 o, f3 d, con
 // The winner's normal and material are formed once after the loop (the reference forms
 // them at every improving hit; the last one is the winner's, from the same object-space
 // ray and t), so only t and the hit cell are carried through the walks.
+#ifdef VPX_PHASE_PROF  // FindNearest volume visits: waves, lanes, lanes past the sphere cull / Setup3DDDA
+__device__ __forceinline__ void prof_visit(int what, bool pass) {
+    const uint64_t act = __ballot(true), ok = __ballot(pass);
+    if ((threadIdx.x & 63u) != (uint32_t)__ffsll((unsigned long long)act) - 1u) return;
+    if (what == 0) atomicAdd(&g_phase[10], 1ull), atomicAdd(&g_phase[11], (unsigned long long)__popcll(act));
+    if (what == 1) atomicAdd(&g_phase[12], (unsigned long long)__popcll(ok));
+    if (what == 2) atomicAdd(&g_phase[13], (unsigned long long)__popcll(ok)), atomicAdd(&g_phase[14], ok ? 1ull : 0ull);
+}
+#define VPX_PROF_VISIT(what, pass) prof_visit(what, pass)
+#else
+#define VPX_PROF_VISIT(what, pass)
+#endif
 template <uint32_t SKIPW = kSkipwNearest, uint32_t MINC = kMincNearest, uint32_t RUN = kRunNearest>
 __device__ __forceinline__ int32_t find_nearest(const SceneView& sv, Ray& r, Counters& k) {
     int32_t vox = -2;
     ++k.nearest;
     uint32_t hx = 0, hy = 0, hz = 0;  // hit cell in volume `vox`
+    const f3 inv = world_inv(r.D);     // the volume culls' slabs (misses_volume)
     auto visit = [&](uint32_t i) {
-        if (misses_volume(sv.vbounds[i], r.O, r.D)) return true;  // Setup3DDDA would fail
+        VPX_PROF_VISIT(0, true);
+        const bool mv = misses_volume(sv.vbounds, i, r.O, inv, r.t);
+        VPX_PROF_VISIT(1, !mv);
+        if (mv) return true;  // Setup3DDDA would fail
         const vpx_volume& vol = sv.volumes[i];
         const DevGrid g = sv.grids[vol.grid_id];
         skip::Walk w;
@@ -894,7 +921,9 @@ __device__ __forceinline__ int32_t find_nearest(const SceneView& sv, Ray& r, Cou
             o.D = xform_vec_ssem(r.D, vol.inv_matrix);
             o.rD = nearest_rd(o.D, sv.x86);
             Dda s;
-            if (!dda_setup(vol, g.n, o, s)) return true;
+            const bool ok = dda_setup(vol, g.n, o, s);
+            VPX_PROF_VISIT(2, ok);
+            if (!ok) return true;
             w = to_walk(s);
         }
         if (walk_wave<0, SKIPW, MINC, RUN>(grid_view(g), w, r.t, k.cells)) {
@@ -907,7 +936,7 @@ __device__ __forceinline__ int32_t find_nearest(const SceneView& sv, Ray& r, Cou
     // with the TLAS, volume 0 (the world, first in the reference's order) is walked before
     // the tree is asked, so the instances' candidates are bounded by its hit
     if (sv.tlas_on)
-        for_volumes(sv, r.O, r.D, r.t, visit);
+        for_volumes(sv, r.O, inv, r.t, visit);
     else
         for (uint32_t i = 0; i < sv.num_volumes; ++i) visit(i);
     if (vox >= 0) {
@@ -946,18 +975,12 @@ __device__ __forceinline__ bool find_nearest_rest(const SceneView& sv, Ray& r, C
     int32_t vox = *vox_io;
     const int32_t vox0 = vox;
     uint32_t hx = 0, hy = 0, hz = 0;
+    const f3 inv = world_inv(r.D);
     auto visit = [&](uint32_t i) {  // i is wave-uniform (for_volumes / the linear loop)
-#ifdef VPX_PHASE_PROF  // instance visits: waves, lanes, lanes past the sphere cull, lanes past Setup3DDDA
-        const uint64_t vb0 = __ballot(true);
-        const bool lead = (threadIdx.x & 63u) == (uint32_t)__ffsll((unsigned long long)vb0) - 1u;
-        if (lead) atomicAdd(&g_phase[10], 1ull), atomicAdd(&g_phase[11], (unsigned long long)__popcll(vb0));
-        const bool mv = misses_volume(ldu(sv.vbounds, i), r.O, r.D);
-        const uint64_t vb1 = __ballot(!mv);
-        if (lead) atomicAdd(&g_phase[12], (unsigned long long)__popcll(vb1));
+        VPX_PROF_VISIT(0, true);
+        const bool mv = misses_volume_u(sv.vbounds, i, r.O, inv, r.t);
+        VPX_PROF_VISIT(1, !mv);
         if (mv) return true;
-#else
-        if (misses_volume(ldu(sv.vbounds, i), r.O, r.D)) return true;
-#endif
         const vpx_volume vol = ldu(sv.volumes, i);
         const DevGrid g = ldu(sv.grids, vol.grid_id);
         skip::Walk w;
@@ -967,15 +990,9 @@ __device__ __forceinline__ bool find_nearest_rest(const SceneView& sv, Ray& r, C
             o.D = xform_vec_ssem(r.D, vol.inv_matrix);
             o.rD = nearest_rd(o.D, sv.x86);
             Dda s;
-#ifdef VPX_PHASE_PROF
             const bool ok = dda_setup(vol, g.n, o, s);
-            const uint64_t vb2 = __ballot(ok);
-            if ((threadIdx.x & 63u) == (uint32_t)__ffsll((unsigned long long)__ballot(true)) - 1u)
-                atomicAdd(&g_phase[13], (unsigned long long)__popcll(vb2)), atomicAdd(&g_phase[14], vb2 ? 1ull : 0ull);
+            VPX_PROF_VISIT(2, ok);
             if (!ok) return true;
-#else
-            if (!dda_setup(vol, g.n, o, s)) return true;
-#endif
             w = to_walk(s);
         }
         if (walk_wave<0, SKIPW, MINC, RUN>(grid_view(g), w, r.t, k.cells)) {
@@ -986,7 +1003,7 @@ __device__ __forceinline__ bool find_nearest_rest(const SceneView& sv, Ray& r, C
         return true;
     };
     if (sv.tlas_on)
-        for_volumes<true>(sv, r.O, r.D, r.t, visit);
+        for_volumes<true>(sv, r.O, inv, r.t, visit);
     else
         for (uint32_t i = 1; i < sv.num_volumes; ++i) visit(i);
     bool changed = vox != vox0;
@@ -1025,8 +1042,9 @@ __device__ __forceinline__ bool find_nearest_rest(const SceneView& sv, Ray& r, C
 // 50.4-50.6 at 4 (round 3, three interleaved runs).
 __device__ __forceinline__ bool is_occluded(const SceneView& sv, const Ray& r, Counters& k, uint32_t first = 0) {
     bool occ = false;
+    const f3 inv = world_inv(r.D);
     auto visit = [&](uint32_t i) {
-        if (misses_volume(sv.vbounds[i], r.O, r.D)) return true;  // Setup3DDDA would fail
+        if (misses_volume(sv.vbounds, i, r.O, inv, r.t)) return true;  // no cell read
         const vpx_volume& vol = sv.volumes[i];
         ORay o;
         o.O = xform_pos(r.O, vol.inv_matrix);

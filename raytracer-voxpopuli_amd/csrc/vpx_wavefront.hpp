@@ -1401,8 +1401,8 @@ __global__ __launch_bounds__(kPoolWg) VPX_WPE(VPX_WPE_SPOOL) void k_shadow_pool(
 // the world left unoccluded (k_shadow_pool walked volume 0, the first in the reference's loop,
 // renderer.cpp:209-243): volumes 1.. in order, then the shapes; an occluder sets the slot's
 // occb byte.  The slots' IsOccluded calls were counted by the pool.
-// The instances' bounding spheres (up to 64: volumes 1..64, bit k = volume k + 1) are tested
-// first, all of them, from a copy in LDS — a branch-free loop of independent tests — and the
+// The instances' boxes (up to 64: volumes 1..64, bit k = volume k + 1) are tested against the
+// slot's segment first, all of them, from a copy in LDS — a branch-free loop of independent tests — and the
 // walks then visit the candidates in increasing index order (wave-uniform: one grid per walk),
 // each lane stopping at its first occluder: the reference's loop (renderer.cpp:209-243)
 // restricted to the volumes whose Setup3DDDA can succeed (misses_volume), so the same
@@ -1425,8 +1425,9 @@ __device__ __forceinline__ bool occluded_instances(const SceneView& sv, const fl
 #ifdef VPX_DEBUG_PROBE_INST_SHADOW
     if (VPX_DEBUG_PROBE_INST_SHADOW < 2)
 #endif
+    const f3 inv = world_inv(r.D);
     for (uint32_t i = 1; i < nv; ++i)
-        cand |= (misses_volume(vb[i], r.O, r.D) ? 0ull : 1ull) << (i - 1u);
+        cand |= (misses_volume(vb, i, r.O, inv, r.t) ? 0ull : 1ull) << (i - 1u);
     bool occ = false;
 
     // the volumes in increasing index order, wave-uniform (a walk needs one grid per wave); a
@@ -1524,8 +1525,8 @@ __device__ __forceinline__ void shadow_inst_chunk(const SceneView& sv, const Wav
 template <bool L0>
 __global__ __launch_bounds__(256) VPX_WPE(VPX_WPE_MULTI_SHADOW) void k_shadow_inst(SceneView sv, WaveBufs w, int level,
                                                                                   unsigned long long* __restrict__ ctr) {
-    __shared__ float4 vb[kTlasMaxVolumes];
-    if (VPX_INST_MASK && threadIdx.x < sv.num_volumes && threadIdx.x < kTlasMaxVolumes)
+    __shared__ float4 vb[2 * kTlasMaxVolumes];
+    if (VPX_INST_MASK && threadIdx.x < 2u * sv.num_volumes && threadIdx.x < 2u * kTlasMaxVolumes)
         vb[threadIdx.x] = sv.vbounds[threadIdx.x];  // published by the barriers in the chunk
     if (L0) {
         shadow_inst_chunk(sv, w, ctr, vb, tile_block() * 256u + threadIdx.x);

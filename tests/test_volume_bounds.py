@@ -1,13 +1,15 @@
-"""The bounding spheres the device culls volume walks with (vpx_volume_bounds, host-side, no GPU).
+"""The world boxes the device culls volume walks with (vpx_volume_bounds, host-side, no GPU).
 
-FindNearest's instance pass and IsOccluded's instance loop skip a volume whose inflated world
-bounding sphere the ray's line misses (misses_volume): the reference's Setup3DDDA fails for
-such a ray, so no cell is read (renderer.cpp:209-243, 946-1018; scene.cpp:719-749).  The
-sphere bounds the cube b0..b1 under the inverse of the affine part of inv_matrix, the only part
+FindNearest and IsOccluded skip a volume whose inflated world box the ray's segment [0, t]
+misses (misses_volume): the reference's Setup3DDDA then fails or enters the cube beyond ray.t,
+so no cell is read (renderer.cpp:209-243, 946-1018; scene.cpp:719-749, 761, 1015).  The box
+holds the cube b0..b1 under the inverse of the affine part of inv_matrix, the only part
 TransformPosition(_SSEM) reads (tmpl8math.cpp:345-402).  Round 6: SetTransform's inverse leaves
-inv_matrix[15] = 1 +- 1 ulp on 20 of C4's 64 rotated instances; the bounds used to demand an
-exact (0, 0, 0, 1) bottom row and gave those instances an infinite radius, so every ray walked
-their setup (C4 42.4 -> 33.5 ms per step once fixed).
+inv_matrix[15] = 1 +- 1 ulp on 20 of C4's 64 rotated instances; the bounds (then spheres) used
+to demand an exact (0, 0, 0, 1) bottom row and left those instances unbounded, so every ray set
+up their walks (C4 42.4 -> 33.5 ms per step once fixed).  The spheres became boxes tested
+against the segment, not the line: the zone scene's long thin volumes passed ~7 spheres per
+ray for ~2 cubes entered.
 """
 import ctypes as C
 
@@ -16,7 +18,7 @@ import pytest
 
 
 def bounds(pkg, vol):
-    out = (C.c_float * 4)()
+    out = (C.c_float * 6)()
     assert pkg.abi.load_library().vpx_volume_bounds(C.byref(vol), out) == pkg.abi.VPX_OK
     return np.array(list(out), np.float64)
 
@@ -41,10 +43,12 @@ def test_every_volume_gets_a_finite_enclosing_sphere(pkg, scene):
     for i, vol in enumerate(desc.volumes):
         b = bounds(pkg, vol)
         assert np.isfinite(b).all(), (i, b, rows[i])
-        d = np.linalg.norm(cube_corners_world(vol) - b[:3], axis=1)
-        assert (d * d < b[3]).all(), (i, d.max() ** 2, b[3])  # inflated: strictly inside
-        r = np.sqrt(b[3])
-        assert r < 1.01 * d.max() + 1e-3 * (1 + np.abs(b[:3]).sum() + r) + 1e-6  # and not loose
+        c = cube_corners_world(vol)
+        lo, hi = b[:3], b[3:]
+        assert (c > lo).all() and (c < hi).all(), (i, c.min(0), c.max(0), lo, hi)  # padded: strictly inside
+        half = np.linalg.norm(c.max(0) - c.min(0)) / 2
+        slack = 1.5e-3 * half + 1.5e-3 * (1 + np.abs((lo + hi) / 2).sum() + half) + 1e-6
+        assert (c.min(0) - lo < slack).all() and (hi - c.max(0) < slack).all(), i  # and not loose
 
 
 def test_singular_volume_is_never_culled(pkg):
@@ -52,5 +56,5 @@ def test_singular_volume_is_never_culled(pkg):
     for k in range(16):
         vol.inv_matrix[k] = 0.0
     b = bounds(pkg, vol)
-    assert b[3] == np.inf
-    assert pkg.abi.load_library().vpx_volume_bounds(None, (C.c_float * 4)()) == pkg.abi.VPX_E_INVALID
+    assert (b[:3] == -np.inf).all() and (b[3:] == np.inf).all()
+    assert pkg.abi.load_library().vpx_volume_bounds(None, (C.c_float * 6)()) == pkg.abi.VPX_E_INVALID
