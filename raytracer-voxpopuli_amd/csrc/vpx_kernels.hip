@@ -31,6 +31,9 @@ namespace {
 constexpr int kTile = 16;  // 16x16 pixels per tile / 256-thread workgroup
 #ifndef VPX_SPLIT_PRIMARY
 #define VPX_SPLIT_PRIMARY 1  // multi-volume primary rays: lean world walk + instance pass (k_instances)
+#ifndef VPX_DEFER_INSTANCES
+#define VPX_DEFER_INSTANCES 1  // depth 0: the world head shades the paths no instance can change (DEFER)
+#endif
 #endif
 #ifndef VPX_LANE_TAIL
 #define VPX_LANE_TAIL 1  // frames in flight blend in their own tail launch where they have one (lane_tail_ok)
@@ -898,7 +901,13 @@ int launch_render(vpx_ctx* c, hipStream_t s, vpx_ctx::WaveStore& ws, const Scene
     // (scenes with analytic shapes test them on every ray, so no ray skips the second pass
     // there: they keep the one-launch kernel — Z1 2.61-2.62 vs 2.63 ms split, round 4)
     const bool split = !one && fuse_head && VPX_SPLIT_PRIMARY && !(sv.num_spheres | sv.num_triangles);
-    if (split)
+    // at depth 0 the world head shades the paths that cannot meet an instance itself and the
+    // instance pass takes only the others (k_primary / k_instances DEFER)
+    const bool defer = split && f.max_bounces == 0 && VPX_DEFER_INSTANCES;
+    if (defer)
+        hipLaunchKernelGGL((x86 ? k_primary<true, true, true, true> : k_primary<true, true, false, true>), grid, block, 0, s,
+                           sv, f, w, c->d_ctr);
+    else if (split)
         hipLaunchKernelGGL((x86 ? k_primary<true, false, true> : k_primary<true, false, false>), grid, block, 0, s, sv, f, w,
                            c->d_ctr);
     else if (fuse_head)
@@ -914,7 +923,7 @@ int launch_render(vpx_ctx* c, hipStream_t s, vpx_ctx::WaveStore& ws, const Scene
     prof_mark(c, s, -1);
     if (split) {
         prof_mark(c, s, VPX_STAGE_INSTANCES);
-        hipLaunchKernelGGL(k_instances, grid, block, xlds, s, sv, f, w, c->d_ctr);
+        hipLaunchKernelGGL(defer ? k_instances<true> : k_instances<false>, grid, block, xlds, s, sv, f, w, c->d_ctr);
         prof_mark(c, s, -1);
     }
     // FindNearest for the traced rays of the next level: the bounce pool (single volume, no

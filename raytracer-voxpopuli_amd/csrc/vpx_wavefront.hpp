@@ -860,7 +860,21 @@ struct HeadLds {
     uint32_t hm[SHADE ? 256 : 1];
 };
 
-template <bool ONE, bool SHADE, uint32_t RUN = kRunNearest>
+// Whether FindNearest may still find something after volume 0 for a ray whose world walk
+// ended at t: the TLAS root box within its segment [0, t] (conservative, tlas_box), or always
+// when there are shapes, volumes outside the tree or no TLAS (the instance pass's candidates).
+__device__ __forceinline__ bool meets_later_volume(const SceneView& sv, f3 o, f3 d, float t) {
+    if (!(sv.tlas_on && !sv.tlas_always && !(sv.num_spheres | sv.num_triangles) && sv.tlas_nodes)) return true;
+    return tlas_box(sv.tlas[0], o, world_inv(d), t);
+}
+
+// DEFER (multi-volume scenes without shapes at Trace depth 0, the head of k_instances<true>):
+// after the world walk a path whose ray cannot meet a later volume (meets_later_volume) is
+// final — the head shades it from its LDS records like a single-volume head; the others are
+// written to HBM and flagged in amask (one ballot word per wave, unused at depth 0) for the
+// instance pass, which continues FindNearest and shades only them.  C4: ~15 % of the primary
+// rays reach the instance lattice's box.
+template <bool ONE, bool SHADE, uint32_t RUN = kRunNearest, bool DEFER = false>
 __device__ __forceinline__ void primary_tile(const SceneView& sv, const FrameArgs& f, const WaveBufs& w,
                                              HeadLds<SHADE>& L, unsigned long long* __restrict__ ctr) {
     uint32_t* sh = L.sh;
@@ -935,17 +949,32 @@ __device__ __forceinline__ void primary_tile(const SceneView& sv, const FrameArg
     if (SHADE) {  // level 0's material switch for this thread's own path (k_primary_shade)
         __syncthreads();  // the tile's hit records, written by the compacted walkers
         Counters ks{0u, 0u, 0u};
-        const bool cont = shade_path<true>(sv, f, w, pr, p, 0, ks);
-        if (f.max_bounces > 0) put_amask(w, p, cont);
+        bool defer = false;
+        if (DEFER && p < w.P) {
+            const float4 d = pr.D[pr.at(p)];
+            if (__float_as_uint(d.w) & kActive) {
+                const float4 o = pr.O[pr.at(p)], h = pr.H[pr.at(p)];
+                defer = meets_later_volume(sv, mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), h.x);
+                if (defer) {  // the instance pass reads the ray and the world's hit record
+                    w.O[p] = o;
+                    w.D[p] = d;
+                    w.H[p] = h;
+                    w.HM[p] = pr.HM[pr.at(p)];
+                }
+            }
+        }
+        if (DEFER) put_amask(w, p, defer);
+        const bool cont = defer ? false : shade_path<true>(sv, f, w, pr, p, 0, ks);
+        if (!DEFER && f.max_bounces > 0) put_amask(w, p, cont);
         flush_counters(ks, 0u, ctr, VPX_STAGE_SHADE);
     }
 }
 
-template <bool ONE, bool SHADE = false, bool X86 = false>
+template <bool ONE, bool SHADE = false, bool X86 = false, bool DEFER = false>
 __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_NEAREST : VPX_WPE_MULTI_NEAREST) void k_primary(SceneView sv, FrameArgs f, WaveBufs w,
                                                  unsigned long long* __restrict__ ctr) {
     __shared__ HeadLds<SHADE> L;
-    primary_tile<ONE, SHADE>(arith_view<X86>(sv), f, w, L, ctr);
+    primary_tile<ONE, SHADE, kRunNearest, DEFER>(arith_view<X86>(sv), f, w, L, ctr);
 }
 
 // Level l + 1's live list from level l's shade bits: 256 mask words (16 k list positions) per
@@ -1001,6 +1030,9 @@ __global__ __launch_bounds__(256) void k_compact(WaveBufs w, int level) {
 // vs 42.90-43.09 ms per step (three interleaved runs): most C4 rays are candidates, and the
 // pass's HBM traffic is mostly the shade's three area-light slots per pixel (144 B), which the
 // shadow pool reads back, not the rays it re-reads.
+// DEFER: after k_primary<true, true, X86, true> — only the paths the head flagged in amask
+// (their rays and world hit records in HBM) are continued and shaded; the head shaded the rest.
+template <bool DEFER>
 __global__ __launch_bounds__(256) VPX_WPE(VPX_WPE_MULTI_NEAREST) void k_instances(SceneView sv_, FrameArgs f, WaveBufs w,
                                                                                 unsigned long long* __restrict__ ctr) {
     __shared__ uint32_t sh[4];
@@ -1013,17 +1045,16 @@ __global__ __launch_bounds__(256) VPX_WPE(VPX_WPE_MULTI_NEAREST) void k_instance
     const PathRay pr{w.O, w.D, w.H, w.HM, 0u};
     Counters k{0u, 0u, 0u};
     bool go = false;
-    if (p < w.P && (__float_as_uint(w.D[p].w) & kActive)) {
-        go = true;
-        if (sv.tlas_on && !sv.tlas_always && !(sv.num_spheres | sv.num_triangles) && sv.tlas_nodes) {
-            const float4 o = w.O[p], d = w.D[p];
-            const f3 inv = mk(__fdiv_rn(1.0f, d.x), __fdiv_rn(1.0f, d.y), __fdiv_rn(1.0f, d.z));
-            go = tlas_box(sv.tlas[0], mk(o.x, o.y, o.z), inv, w.H[p].x);  // conservative (tlas_box)
-        }
-#ifdef VPX_DEBUG_NO_INST_WALK
-        go = false;  // timing probe only (wrong images): the pass without its instance walks
-#endif
+    if (DEFER) {
+        go = p < w.P && ((w.amask[p >> 6] >> (p & 63u)) & 1ull);
+    } else if (p < w.P && (__float_as_uint(w.D[p].w) & kActive)) {
+        const float4 o = w.O[p], d = w.D[p];
+        go = meets_later_volume(sv, mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), w.H[p].x);
     }
+    const bool mine = go;  // (DEFER: the paths this pass shades)
+#ifdef VPX_DEBUG_NO_INST_WALK
+    go = false;  // timing probe only (wrong images): the pass without its instance walks
+#endif
     uint32_t total;
     const uint32_t at = block_scan(go ? 1u : 0u, total, sh);
     if (go) lst[at] = p;
@@ -1048,8 +1079,12 @@ __global__ __launch_bounds__(256) VPX_WPE(VPX_WPE_MULTI_NEAREST) void k_instance
     flush_counters(k, 0u, ctr, VPX_STAGE_INSTANCES);
     __syncthreads();  // the tile's hit records, as the compacted lanes left them
     Counters ks{0u, 0u, 0u};
-    const bool cont = shade_path<true>(sv, f, w, pr, p, 0, ks);
-    if (f.max_bounces > 0) put_amask(w, p, cont);
+    if (DEFER) {
+        if (mine) shade_path<true>(sv, f, w, pr, p, 0, ks);
+    } else {
+        const bool cont = shade_path<true>(sv, f, w, pr, p, 0, ks);
+        if (f.max_bounces > 0) put_amask(w, p, cont);
+    }
     flush_counters(ks, 0u, ctr, VPX_STAGE_SHADE);
 }
 
