@@ -687,6 +687,13 @@ SceneView view_of(const vpx_ctx* c, const float sky[3], int32_t area_samples, bo
     sv.sky_hdr = c->sky_hdr;
     sv.sky_tex = (sky_tex && c->d_sky) ? 1u : 0u;
     sv.x86 = c->x86;
+    // one grid for every volume after the world: lane_volumes (vpx_trace.hpp)
+    sv.inst_grid = -1;
+    for (size_t i = 1; i < c->volumes.size(); ++i) {
+        const int32_t gi = (int32_t)c->volumes[i].grid_id;
+        if (i == 1) sv.inst_grid = gi;
+        else if (gi != sv.inst_grid) { sv.inst_grid = -1; break; }
+    }
     return sv;
 }
 
@@ -733,7 +740,7 @@ int ensure_wave(vpx_ctx* c, vpx_ctx::WaveStore& ws, uint32_t P, uint32_t L, uint
     const size_t f4 = sizeof(float4);
     const size_t bytes = (size_t)P * (f4 * (5 + 2 * (size_t)L + 3 * (size_t)S + 1) + 3 * sizeof(uint32_t)) +
                          sizeof(uint32_t) * (size_t)P * 3 + (size_t)P / 8 + sizeof(uint32_t) * kPoolWords +
-                         (size_t)P * S + 21 * 256;
+                         (size_t)P * S + sizeof(uint32_t) * (size_t)P * S + 22 * 256;
     if (bytes > ws.bytes) {
         if (ws.d) {
             VPX_HIP(c, sync_all(c));
@@ -772,6 +779,7 @@ int ensure_wave(vpx_ctx* c, vpx_ctx::WaveStore& ws, uint32_t P, uint32_t L, uint
     w.amask = (uint64_t*)take((size_t)P / 8);  // P is a multiple of 256
     w.pool = (uint32_t*)take(sizeof(uint32_t) * kPoolWords);
     w.occb = (uint8_t*)take((size_t)P * S);
+    (void)take(sizeof(uint32_t) * (size_t)P * S);  // slot_list (vpx_wavefront.hpp), right after occb
     return VPX_OK;
 }
 
@@ -871,11 +879,16 @@ int launch_render(vpx_ctx* c, hipStream_t s, vpx_ctx::WaveStore& ws, const Scene
         const uint32_t grabs = (P / 64u + sgrab - 1u) / sgrab;
         const uint32_t waves = std::min(grabs, c->cus * 4u * (uint32_t)VPX_WPE_SPOOL);
         const uint32_t wpb = kPoolWg / 64u;
-        hipLaunchKernelGGL(k_shadow_pool, dim3((waves + wpb - 1u) / wpb), dim3(kPoolWg), 0, s, sv, w, level, sgrab,
-                           c->d_ctr);
-        if (!one)
-            hipLaunchKernelGGL(level ? k_shadow_inst<false> : k_shadow_inst<true>, grid, block, slds, s, sv, w, level,
-                               c->d_ctr);
+        hipLaunchKernelGGL(one ? k_shadow_pool<false> : k_shadow_pool<true>, dim3((waves + wpb - 1u) / wpb), dim3(kPoolWg), 0,
+                           s, sv, w, level, sgrab, c->d_ctr);
+        if (!one) {
+            if (VPX_SHADOW_SLOTS)  // the pool's list of the slots a later volume may occlude
+                hipLaunchKernelGGL(k_shadow_slots, dim3(std::min(tiles * S, c->cus * (uint32_t)VPX_WPE_MULTI_SHADOW)), block, 0, s,
+                                   sv, w, level, c->d_ctr);
+            else
+                hipLaunchKernelGGL(level ? k_shadow_inst<false> : k_shadow_inst<true>, grid, block, slds, s, sv, w, level,
+                                   c->d_ctr);
+        }
     };
     if (one && fuse_tail && f.max_bounces == 0 && tiles <= kFuseFrameTiles && S == 1) {
         // the whole depth-0 frame in one launch (k_frame0), its path state and one shadow slot

@@ -89,6 +89,9 @@ struct SceneView {
     uint32_t sky_w, sky_h;
     float sky_hdr;
     uint32_t sky_tex;
+    // the grid every volume after the world (1 .. n-1) uses, or -1: then a wave's lanes can walk
+    // different instances in one walk (lane_volumes), the grid data being the same
+    int32_t inst_grid;
     // reference arithmetic (vpx_set_arithmetic): the host's rcpss / rsqrtss tables, or a null
     // tab for the exact 1/x and 1/sqrtf of the default mode
     X86Arith x86;
@@ -884,6 +887,42 @@ __device__ __forceinline__ void for_volumes(const SceneView& sv, f3 o, f3 inv, c
     }
 }
 
+// A lane's TLAS candidates (bit k = volume k + 1): the leaves its segment [0, bound] reaches
+// (wave-uniform traversal, as for_volumes), plus the always-set.
+__device__ __forceinline__ uint64_t tlas_candidates(const SceneView& sv, f3 o, f3 inv, float bound) {
+    uint64_t mine = sv.tlas_always;
+    for (uint32_t n = 0; n < sv.tlas_nodes;) {
+        const TlasNode nd = ldu(sv.tlas, n);
+        const bool h = tlas_box(nd, o, inv, bound);
+        if (nd.leaf) {
+            if (h) mine |= nd.mask;
+            ++n;
+        } else {
+            n = __ballot(h) ? n + 1 : nd.skip;
+        }
+    }
+    return mine;
+}
+
+// Lane volumes: when every volume after the world uses one grid (SceneView::inst_grid, C4's 64
+// instances of one model), a wave walks each lane's own next candidate in one walk — the grid
+// data is shared, only the object-space rays differ — so a wave costs the most candidates any
+// one lane visits instead of the union of its lanes' candidates (walked one volume at a time,
+// for_volumes).  Each lane visits its candidates in increasing index order with its bound as it
+// stands: the reference's loop for that ray (renderer.cpp:209-243, 946-1018), the same cells,
+// hits and counts.  next(): the lane's next volume whose walk can read a cell (Setup3DDDA
+// succeeds) and its walk state; false when it has none.
+template <class Next, class Done>
+__device__ __forceinline__ void lane_volumes(const skip::GridView& gv, Next next, Done done) {
+    for (;;) {
+        skip::Walk w;
+        uint32_t vi = 0;
+        const bool have = next(w, vi);
+        if (!__ballot(have)) break;
+        if (have) done(w, vi);
+    }
+}
+
 // Renderer::FindNearest, renderer.cpp:946-1018.  Linear loop over the volumes with the
 // SSE transforms; a later volume wins only with a strictly smaller t (ties -> lowest index).
 // The winner's normal and material are formed once after the loop (the reference forms
@@ -963,6 +1002,9 @@ __device__ __forceinline__ int32_t find_nearest(const SceneView& sv, Ray& r, Cou
     return vox;
 }
 
+#ifndef VPX_LANE_VOLUMES
+#define VPX_LANE_VOLUMES 1
+#endif
 // Renderer::FindNearest from volume 1 on (renderer.cpp:946-1018), for a ray whose walk of
 // volume 0 already left r.t / the hit record (*vox = 0 on a hit there, else -2): the
 // instance pass of multi-volume primary rays (k_instances), whose world walk ran in the lean
@@ -1002,10 +1044,40 @@ __device__ __forceinline__ bool find_nearest_rest(const SceneView& sv, Ray& r, C
         }
         return true;
     };
-    if (sv.tlas_on)
+    if (sv.tlas_on && sv.inst_grid >= 0 && VPX_LANE_VOLUMES) {
+        uint64_t rest = tlas_candidates(sv, r.O, inv, r.t);
+        const DevGrid g = ldu(sv.grids, (uint32_t)sv.inst_grid);
+        auto next = [&](skip::Walk& w, uint32_t& vi) {
+            while (rest) {
+                const uint32_t i = (uint32_t)__ffsll((unsigned long long)rest);  // bit i - 1 = volume i
+                rest &= rest - 1ull;
+                if (misses_volume(sv.vbounds, i, r.O, inv, r.t)) continue;
+                const vpx_volume& vol = sv.volumes[i];  // this lane's own volume
+                ORay o;
+                o.O = xform_pos_ssem(r.O, vol.inv_matrix);
+                o.D = xform_vec_ssem(r.D, vol.inv_matrix);
+                o.rD = nearest_rd(o.D, sv.x86);
+                Dda s;
+                if (!dda_setup(vol, g.n, o, s)) continue;
+                w = to_walk(s);
+                vi = i;
+                return true;
+            }
+            return false;
+        };
+        auto done = [&](skip::Walk& w, uint32_t vi) {
+            if (walk_wave<0, SKIPW, MINC, RUN>(grid_view(g), w, r.t, k.cells)) {
+                r.t = w.t;
+                hx = w.X, hy = w.Y, hz = w.Z;
+                vox = (int32_t)vi;
+            }
+        };
+        lane_volumes(grid_view(g), next, done);
+    } else if (sv.tlas_on) {
         for_volumes<true>(sv, r.O, inv, r.t, visit);
-    else
+    } else {
         for (uint32_t i = 1; i < sv.num_volumes; ++i) visit(i);
+    }
     bool changed = vox != vox0;
     if (changed) {
         const vpx_volume& vol = sv.volumes[vox];

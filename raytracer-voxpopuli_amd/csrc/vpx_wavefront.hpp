@@ -101,11 +101,20 @@ struct WaveBufs {
                       // shaded (level 0: path i) traces a next ray (the shades write it, k_compact reads it)
     uint32_t* pool;   // [kPoolWords] the level counters (kPool*), zeroed at the start of every frame that
                       // uses them (launch_render)
-    uint8_t* occb;    // [S][P] the shadow pool's result per slot: 1 = occluded (valid slots only)
+    uint8_t* occb;    // [S][P] the shadow pool's result per slot: 1 = occluded (valid slots only),
+                      // followed by slot_list's [S * P] words
     float4* RD;    // [W*H] reprojection: level-0 intersection point, w = material bits (image order)
     uint32_t P;    // paths (pixels) this call
     uint32_t S;    // shadow slots per path
 };
+
+// Multi-volume scenes: the slots the shadow pool left unoccluded whose segment may meet a later
+// volume (slot << 27 | path), pool[kPoolSlots + level * kLineWords] of them; stored after occb
+// (ensure_wave) rather than in a WaveBufs field of its own (the pool's registers: a bigger
+// kernel argument block cost k_shadow_pool two more spilled VGPRs).
+__device__ __forceinline__ uint32_t* slot_list(const WaveBufs& w) {
+    return reinterpret_cast<uint32_t*>(w.occb + (((size_t)w.P * w.S + 255u) & ~(size_t)255u));
+}
 
 // Level counters in WaveBufs::pool: the length of level l's live-path list, and the pools'
 // chunk grabs (kGrabStripes counters per level) of its shadow walks and its bounce walks.
@@ -123,7 +132,8 @@ struct WaveBufs {
 constexpr uint32_t kGrabLines = VPX_GRAB_LINES, kLineWords = 32;
 constexpr uint32_t kGrabBlock = (kGrabLines + 1u) * kLineWords;  // per level: the counters, then the mask
 constexpr uint32_t kPoolLive = 0, kPoolShadow = kLineWords, kPoolBounce = kPoolShadow + kMaxLevels * kGrabBlock,
-                   kPoolWords = kPoolBounce + kMaxLevels * kGrabBlock;
+                   kPoolSlots = kPoolBounce + kMaxLevels * kGrabBlock,  // per level, its own line: slist's length
+                   kPoolWords = kPoolSlots + kMaxLevels * kLineWords;
 
 // The next of `chunks` chunks for this wave (wave-uniform; lane 0 takes it), ~0u when none is
 // left.  blk: the level's grab block; line: the wave's current counter (wave-uniform).
@@ -1333,6 +1343,10 @@ constexpr uint32_t kShadowList = 1024;  // listed slots per wave (LDS: 4 KiB)
 #ifndef VPX_WPE_SPOOL
 #define VPX_WPE_SPOOL 5
 #endif
+#ifndef VPX_SHADOW_SLOTS
+#define VPX_SHADOW_SLOTS 1  // multi-volume area-light shadows: k_shadow_slots over the pool's list (else k_shadow_inst)
+#endif
+template <bool MULTI>  // multi-volume / shape scenes: the pool walks the world and lists the rest (slist)
 __global__ __launch_bounds__(kPoolWg) VPX_WPE(VPX_WPE_SPOOL) void k_shadow_pool(SceneView sv, WaveBufs w, int level,
                                                                               uint32_t grab,
                                                                               unsigned long long* __restrict__ ctr) {
@@ -1355,10 +1369,35 @@ __global__ __launch_bounds__(kPoolWg) VPX_WPE(VPX_WPE_SPOOL) void k_shadow_pool(
     uint32_t avail = 0u, cur = 0u;
     bool more = true;
     uint32_t line = pool_line0();
+    // multi-volume / shape scenes: the pool walks the world (volume 0); a slot it leaves
+    // unoccluded whose segment may meet a later volume goes to the level's slot list for
+    // k_shadow_slots (one atomic per wave and batch of finished lanes)
     for (;;) {
-        if (e != ~0u && mode >= kWalkMiss) {
-            w.occb[(uint64_t)(e >> 27) * w.P + (e & 0x07ffffffu)] = mode == kWalkHit ? 1u : 0u;
-            e = ~0u;
+        if constexpr (!(MULTI && VPX_SHADOW_SLOTS)) {  // (single volume: the result only)
+            if (e != ~0u && mode >= kWalkMiss) {
+                w.occb[(uint64_t)(e >> 27) * w.P + (e & 0x07ffffffu)] = mode == kWalkHit ? 1u : 0u;
+                e = ~0u;
+            }
+        } else {
+            const bool fin = e != ~0u && mode >= kWalkMiss;
+            bool app = false;
+            if (fin) {
+                const uint64_t slot = (uint64_t)(e >> 27) * w.P + (e & 0x07ffffffu);
+                w.occb[slot] = mode == kWalkHit ? 1u : 0u;
+                if (mode != kWalkHit) {
+                    const float4 so = w.SO[slot], sd = w.SD[slot];
+                    app = meets_later_volume(sv, mk(so.x, so.y, so.z), mk(sd.x, sd.y, sd.z), so.w);
+                }
+            }
+            const uint64_t b = __ballot(app);
+            if (b) {
+                uint32_t base = 0u;
+                if (lane == (uint32_t)__ffsll((unsigned long long)b) - 1u)
+                    base = atomicAdd(&w.pool[kPoolSlots + level * kLineWords], (uint32_t)__popcll(b));
+                base = (uint32_t)__builtin_amdgcn_readlane((int)base, __ffsll((unsigned long long)b) - 1);
+                if (app) slot_list(w)[base + lane_rank(b)] = e;
+            }
+            if (fin) e = ~0u;
         }
         while (more) {
             const uint64_t idle = __ballot(e == ~0u);
@@ -1464,6 +1503,40 @@ __device__ __forceinline__ bool occluded_instances(const SceneView& sv, const fl
     for (uint32_t i = 1; i < nv; ++i)
         cand |= (misses_volume(vb, i, r.O, inv, r.t) ? 0ull : 1ull) << (i - 1u);
     bool occ = false;
+    if (sv.inst_grid >= 0 && VPX_LANE_VOLUMES) {  // each lane its own next candidate (lane_volumes)
+        const DevGrid g = ldu(sv.grids, (uint32_t)sv.inst_grid);
+        uint64_t rest = cand;
+        auto next = [&](skip::Walk& wk, uint32_t& vi) {
+            while (rest) {
+                const uint32_t i = (uint32_t)__ffsll((unsigned long long)rest);  // bit i - 1 = volume i
+                rest &= rest - 1ull;
+                const vpx_volume& vol = sv.volumes[i];
+                ORay o;
+                o.O = xform_pos(r.O, vol.inv_matrix);
+                o.D = xform_vec(r.D, vol.inv_matrix);
+                o.rD = mk(__fdiv_rn(1.0f, o.D.x), __fdiv_rn(1.0f, o.D.y), __fdiv_rn(1.0f, o.D.z));
+                Dda s;
+                if (!dda_setup(vol, g.n, o, s)) continue;
+                wk = to_walk(s);
+                vi = i;
+                return true;
+            }
+            return false;
+        };
+        auto done = [&](skip::Walk& wk, uint32_t) {
+            if (walk_wave<16, kSkipwShadow, kMincInstShadow, kRunShadow>(grid_view(g), wk, r.t, k.cells)) {
+                occ = true;
+                rest = 0ull;  // the reference returns at the first occluder
+            }
+        };
+        lane_volumes(grid_view(g), next, done);
+        if (occ) return true;
+        for (uint32_t i = 0; i < sv.num_spheres; ++i)
+            if (sphere_is_hit(sv.spheres[i], r)) return true;
+        for (uint32_t i = 0; i < sv.num_triangles; ++i)
+            if (tri_is_hit(sv.triangles[i], r)) return true;
+        return false;
+    }
 
     // the volumes in increasing index order, wave-uniform (a walk needs one grid per wave); a
     // volume no lane of the wave can reach costs one ballot
@@ -1474,6 +1547,10 @@ __device__ __forceinline__ bool occluded_instances(const SceneView& sv, const fl
         if (VPX_DEBUG_PROBE_INST_SHADOW >= 1) continue;
 #endif
         if (!__ballot(want)) continue;
+#ifdef VPX_PHASE_PROF  // instance shadow visits: waves, lanes walking
+        if ((threadIdx.x & 63u) == (uint32_t)__ffsll((unsigned long long)__ballot(true)) - 1u)
+            atomicAdd(&g_phase[25], 1ull), atomicAdd(&g_phase[26], (unsigned long long)__popcll(__ballot(want)));
+#endif
         if (!want) continue;
         const vpx_volume vol = ldu(sv.volumes, i);  // i is wave-uniform
         ORay o;
@@ -1548,6 +1625,10 @@ __device__ __forceinline__ void shadow_inst_chunk(const SceneView& sv, const Wav
         r.O = mk(so.x, so.y, so.z);
         r.D = mk(sd.x, sd.y, sd.z);
         r.t = so.w;
+#ifdef VPX_PHASE_PROF  // slots reaching the instance loop
+        if ((threadIdx.x & 63u) == (uint32_t)__ffsll((unsigned long long)__ballot(true)) - 1u)
+            atomicAdd(&g_phase[27], (unsigned long long)__popcll(__ballot(true))), atomicAdd(&g_phase[28], 1ull);
+#endif
         const bool occ = (VPX_INST_MASK && sv.num_volumes <= kTlasMaxVolumes)
                              ? occluded_instances(sv, vb, r, k)
                              : is_occluded(sv, r, k, 1u);
@@ -1571,6 +1652,36 @@ __global__ __launch_bounds__(256) VPX_WPE(VPX_WPE_MULTI_SHADOW) void k_shadow_in
     if (blockIdx.x * 256u >= n) return;  // one chunk per workgroup (k_nearest_tile)
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
     shadow_inst_chunk(sv, w, ctr, vb, i < n ? live_path(w, level, i) : ~0u);
+}
+
+// The rest of Renderer::IsOccluded (volumes 1.., then the shapes) for the shadow pool's slot
+// list (slots the world left unoccluded whose segment may meet a later volume): the same
+// per-slot loop as k_shadow_inst, over a dense list instead of every slot of every tile — C4's
+// ~16 k candidate slots per frame had cost a scan of all 25 M slots' flags and rays.
+// Persistent workgroups striding over the list (its length is on the device).
+__global__ __launch_bounds__(256) VPX_WPE(VPX_WPE_MULTI_SHADOW) void k_shadow_slots(SceneView sv, WaveBufs w, int level,
+                                                                                   unsigned long long* __restrict__ ctr) {
+    __shared__ float4 vb[2 * kTlasMaxVolumes];
+    if (VPX_INST_MASK && threadIdx.x < 2u * sv.num_volumes && threadIdx.x < 2u * kTlasMaxVolumes)
+        vb[threadIdx.x] = sv.vbounds[threadIdx.x];
+    __syncthreads();
+    Counters k{0u, 0u, 0u};
+    const uint32_t n = __builtin_amdgcn_readfirstlane(w.pool[kPoolSlots + level * kLineWords]);
+    for (uint32_t base = blockIdx.x * 256u; base < n; base += gridDim.x * 256u) {
+        const uint32_t i = base + threadIdx.x;
+        if (i >= n) continue;
+        const uint32_t e = slot_list(w)[i];
+        const uint64_t slot = (uint64_t)(e >> 27) * w.P + (e & 0x07ffffffu);
+        const float4 so = w.SO[slot], sd = w.SD[slot];
+        Ray r;
+        r.O = mk(so.x, so.y, so.z);
+        r.D = mk(sd.x, sd.y, sd.z);
+        r.t = so.w;
+        const bool occ = (VPX_INST_MASK && sv.num_volumes <= kTlasMaxVolumes) ? occluded_instances(sv, vb, r, k)
+                                                                              : is_occluded(sv, r, k, 1u);
+        if (occ) w.occb[slot] = 1u;
+    }
+    flush_counters(k, 0u, ctr, VPX_STAGE_SHADOW);
 }
 
 // ------------------------------------------------------------------- stage 4

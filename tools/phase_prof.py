@@ -36,3 +36,6 @@ v = list(ph)
 if v[10]:
     print(f"[instances] wave visits={v[10]} lane visits={v[11]} ({v[11] / v[10]:.1f}/wave visit) past sphere cull={v[12]} "
           f"past Setup3DDDA={v[13]} wave visits with a walk={v[14]}")
+if v[28]:
+    print(f"[instance shadows] slots={v[27]} in {v[28]} waves ({v[27] / v[28]:.1f}/wave); volume visits: waves={v[25]} "
+          f"lanes walking={v[26]} ({v[26] / max(v[25], 1):.1f}/wave visit, {v[25] / v[28]:.1f} visits/wave)")
