@@ -112,7 +112,7 @@ def pmc_summary(kernel, config, W, H, sha):
         except (OSError, ValueError):
             continue
         ks = d.get("kernels", {})
-        parts = kernel.split("+")  # a stage of two launches (e.g. k_shadow_pool+k_shadow_inst)
+        parts = kernel.split("+")  # a stage of two launches (e.g. k_shadow_pool+k_shadow_slots)
         if (d.get("config") == config and d.get("width") == W and d.get("height") == H
                 and d.get("lib_sha256") == sha and all(k in ks for k in parts)):
             best, src = combine_pmc([ks[k] for k in parts]), os.path.relpath(f, REPO)
@@ -311,9 +311,9 @@ def run_config(pkg, env, cfg, steps, warmup, weak=False, sha=None, pipeline=None
         kernels = dict(STAGE_KERNELS)
         if len(desc.volumes) == 1 and not (desc.spheres or desc.triangles):  # the pools
             kernels["bounce"] = "k_nearest_pool"
-        if desc.areas and desc.area_samples > 1:  # area lights: the shadow pool (+ k_shadow_inst)
+        if desc.areas and desc.area_samples > 1:  # area lights: the shadow pool (+ k_shadow_slots)
             kernels.update(shadow="k_shadow_pool" if len(desc.volumes) == 1 and not (desc.spheres or desc.triangles)
-                           else "k_shadow_pool+k_shadow_inst", finish="k_resolve_finish")
+                           else "k_shadow_pool+k_shadow_slots", finish="k_resolve_finish")
         if fused:
             kernels["shadow"] = "k_shadow_finish" if desc.max_bounces == 0 else "k_shadow_tile+k_shadow_finish"
         # rank 0's own work (its launches, cells and pixels)

@@ -867,8 +867,9 @@ int launch_render(vpx_ctx* c, hipStream_t s, vpx_ctx::WaveStore& ws, const Scene
     // each, pool / tile kernels): C3 3.72, 3.71 / 4.96, 4.94; C2 (one point light, one slot per
     // path) 2.83, 2.84 / 2.64, 2.71 — so point / spot / directional lights keep the tile kernels.
     // Multi-volume / shape scenes: the world's walks (volume 0, first in IsOccluded's loop) in
-    // the pool, the rest of the loop in k_shadow_inst for the slots the world left unoccluded:
-    // C4 51.7 / 51.8 -> 47.6 / 47.7 ms per 16-spp step (shadow stage 2.13 -> 1.62 + 0.15 ms).
+    // the pool, the rest of the loop for the slots the world left unoccluded: k_shadow_inst per
+    // tile (round 3: C4 51.7 -> 47.6 ms per 16-spp step), then (round 6) k_shadow_slots over the
+    // pool's list of the slots whose segment may meet a later volume.
     const bool spool = !rp && S > 1;
     if (!spool) w.occb = nullptr;  // k_resolve reads the slots' SD flags
     const uint32_t sgrab = std::max(1u, std::min(4u, kShadowList / (64u * S)));
@@ -881,14 +882,9 @@ int launch_render(vpx_ctx* c, hipStream_t s, vpx_ctx::WaveStore& ws, const Scene
         const uint32_t wpb = kPoolWg / 64u;
         hipLaunchKernelGGL(one ? k_shadow_pool<false> : k_shadow_pool<true>, dim3((waves + wpb - 1u) / wpb), dim3(kPoolWg), 0,
                            s, sv, w, level, sgrab, c->d_ctr);
-        if (!one) {
-            if (VPX_SHADOW_SLOTS)  // the pool's list of the slots a later volume may occlude
-                hipLaunchKernelGGL(k_shadow_slots, dim3(std::min(tiles * S, c->cus * (uint32_t)VPX_WPE_MULTI_SHADOW)), block, 0, s,
-                                   sv, w, level, c->d_ctr);
-            else
-                hipLaunchKernelGGL(level ? k_shadow_inst<false> : k_shadow_inst<true>, grid, block, slds, s, sv, w, level,
-                                   c->d_ctr);
-        }
+        if (!one)  // the pool's list of the slots a later volume may occlude
+            hipLaunchKernelGGL(k_shadow_slots, dim3(std::min(tiles * S, c->cus * (uint32_t)VPX_WPE_SHADOW_SLOTS)), block, 0, s, sv,
+                               w, level, c->d_ctr);
     };
     if (one && fuse_tail && f.max_bounces == 0 && tiles <= kFuseFrameTiles && S == 1) {
         // the whole depth-0 frame in one launch (k_frame0), its path state and one shadow slot
@@ -1690,7 +1686,7 @@ int vpx_set_volumes(vpx_ctx* c, const vpx_volume* v, uint32_t count) {
     }
     // Invariant: d_volumes, d_vbounds and the TLAS (d_tlas) describe the same volumes.  The
     // instance kernels cull by the TLAS root box and the bounding spheres (FindNearest's
-    // candidates, k_shadow_inst's slot cull), so a volume update that skipped build_tlas would
+    // candidates, the shadow pool's slot list), so a volume update that skipped build_tlas would
     // silently drop instance hits and shadows: every writer of d_volumes goes through here.
     c->volumes.assign(v, v + count);
     std::vector<VolBox> bounds(count);

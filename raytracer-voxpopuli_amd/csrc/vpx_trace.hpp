@@ -1108,7 +1108,7 @@ __device__ __forceinline__ bool find_nearest_rest(const SceneView& sv, Ray& r, C
 // Renderer::IsOccluded, renderer.cpp:209-243 (scalar transforms, exact 1/D).  The linear
 // volume loop: through the instance TLAS it measured slower (C4 IsOccluded 2.67 vs 2.57 ms:
 // most shadow rays end in the world volume, the rest cross the instance lattice).
-// first: the volume the loop starts at (k_shadow_inst: 1, after the shadow pool walked the
+// first: the volume the loop starts at (k_shadow_slots: 1, after the shadow pool walked the
 // world, volume 0).  The instances alone through the TLAS (the world's walk left to the pool)
 // were slower too: C4 48.6-48.9 vs 47.2-47.4 ms per step at 5 waves/SIMD (8 spilled VGPRs),
 // 50.4-50.6 at 4 (round 3, three interleaved runs).

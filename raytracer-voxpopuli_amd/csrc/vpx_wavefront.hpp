@@ -739,7 +739,7 @@ __global__ __launch_bounds__(256) void k_resolve(SceneView sv, WaveBufs w, int l
 #ifndef VPX_WPE_MULTI_NEAREST
 #define VPX_WPE_MULTI_NEAREST 4
 #endif
-// The multi-volume shadow kernels (k_shadow_inst, k_shadow_tile<false>, k_shadow_finish<false>)
+// The multi-volume shadow kernels (k_shadow_tile<false>, k_shadow_finish<false>; round 4 also k_shadow_inst)
 // at 6 (80 VGPRs, 15-18 spilled): C4 42.91 / 42.60 / 42.84 vs 43.18 / 42.94 / 44.99 ms at 5,
 // Z1 within noise (round 4, tools/gpu_r4n.sh); k_nearest_tile at 5 (49 spilled VGPRs): Z1
 // 2.66 vs 2.50-2.52.
@@ -1343,9 +1343,6 @@ constexpr uint32_t kShadowList = 1024;  // listed slots per wave (LDS: 4 KiB)
 #ifndef VPX_WPE_SPOOL
 #define VPX_WPE_SPOOL 5
 #endif
-#ifndef VPX_SHADOW_SLOTS
-#define VPX_SHADOW_SLOTS 1  // multi-volume area-light shadows: k_shadow_slots over the pool's list (else k_shadow_inst)
-#endif
 template <bool MULTI>  // multi-volume / shape scenes: the pool walks the world and lists the rest (slist)
 __global__ __launch_bounds__(kPoolWg) VPX_WPE(VPX_WPE_SPOOL) void k_shadow_pool(SceneView sv, WaveBufs w, int level,
                                                                               uint32_t grab,
@@ -1373,7 +1370,7 @@ __global__ __launch_bounds__(kPoolWg) VPX_WPE(VPX_WPE_SPOOL) void k_shadow_pool(
     // unoccluded whose segment may meet a later volume goes to the level's slot list for
     // k_shadow_slots (one atomic per wave and batch of finished lanes)
     for (;;) {
-        if constexpr (!(MULTI && VPX_SHADOW_SLOTS)) {  // (single volume: the result only)
+        if constexpr (!MULTI) {  // (single volume: the result only)
             if (e != ~0u && mode >= kWalkMiss) {
                 w.occb[(uint64_t)(e >> 27) * w.P + (e & 0x07ffffffu)] = mode == kWalkHit ? 1u : 0u;
                 e = ~0u;
@@ -1571,95 +1568,18 @@ __device__ __forceinline__ bool occluded_instances(const SceneView& sv, const fl
     return false;
 }
 
-// One tile's (or 256 live-list entries') remaining slots: p = this thread's path (>= P: none).
-__device__ __forceinline__ void shadow_inst_chunk(const SceneView& sv, const WaveBufs& w, unsigned long long* __restrict__ ctr,
-                                                  const float4* vb, uint32_t p) {
-    __shared__ uint32_t sh[4];
-    extern __shared__ uint32_t lst_dyn[];  // [S * 256]
-    __shared__ uint32_t hist[kLightKeys];
-    if (threadIdx.x < kLightKeys) hist[threadIdx.x] = 0u;
-    Counters k{0u, 0u, 0u};
-    const uint32_t smv = p < w.P ? w.smask[p] : 0u;
-    const uint32_t m = smv & kSlotBits, key = smv >> 16;
-    // a slot whose segment [0, tmax] misses the instance TLAS's root box meets no instance (the
-    // root box holds every instance's inflated bounding sphere; a cube entered beyond tmax
-    // reads no cell, scene.cpp:1015): it is left unoccluded without a list entry
-    const bool cull = VPX_INST_CULL && sv.tlas_on && !sv.tlas_always && sv.tlas_nodes &&
-                      !(sv.num_spheres | sv.num_triangles);
-    uint32_t mine = 0u;
-    for (uint32_t b = m; b; b &= b - 1u) {
-        const uint32_t sl = (uint32_t)__ffs(b) - 1u;
-        const uint64_t slot = (uint64_t)sl * w.P + p;
-        if (w.occb[slot]) continue;
-        if (cull) {
-            const float4 so = w.SO[slot], sd = w.SD[slot];
-            const f3 inv = mk(__fdiv_rn(1.0f, sd.x), __fdiv_rn(1.0f, sd.y), __fdiv_rn(1.0f, sd.z));
-            if (!tlas_box(sv.tlas[0], mk(so.x, so.y, so.z), inv, so.w)) continue;
-        }
-        mine |= 1u << sl;
-    }
-    __syncthreads();  // hist zeroed (and vb staged)
-    // the tile's remaining slots grouped by light (shadow_tile's counting sort): a wave's lanes
-    // head the same way and share their candidate instances
-    const uint32_t pos = mine ? atomicAdd(&hist[key], (uint32_t)__popc(mine)) : 0u;
-    __syncthreads();
-    if (threadIdx.x < 64) {
-        const uint32_t v = threadIdx.x < kLightKeys ? hist[threadIdx.x] : 0u;
-        uint32_t t;
-        const uint32_t ex = wave_prefix(v, t);
-        if (threadIdx.x < kLightKeys) hist[threadIdx.x] = ex;
-        if (threadIdx.x == 0) sh[0] = t;
-    }
-    __syncthreads();
-    const uint32_t total = __builtin_amdgcn_readfirstlane(sh[0]);
-    {
-        uint32_t at = mine ? hist[key] + pos : 0u;
-        for (uint32_t b = mine; b; b &= b - 1u) lst_dyn[at++] = ((uint32_t)__ffs(b) - 1u) << 27 | p;
-    }
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < total; i += 256u) {
-        const uint32_t e = lst_dyn[i];
-        const uint64_t slot = (uint64_t)(e >> 27) * w.P + (e & 0x07ffffffu);
-        const float4 so = w.SO[slot], sd = w.SD[slot];
-        Ray r;
-        r.O = mk(so.x, so.y, so.z);
-        r.D = mk(sd.x, sd.y, sd.z);
-        r.t = so.w;
-#ifdef VPX_PHASE_PROF  // slots reaching the instance loop
-        if ((threadIdx.x & 63u) == (uint32_t)__ffsll((unsigned long long)__ballot(true)) - 1u)
-            atomicAdd(&g_phase[27], (unsigned long long)__popcll(__ballot(true))), atomicAdd(&g_phase[28], 1ull);
-#endif
-        const bool occ = (VPX_INST_MASK && sv.num_volumes <= kTlasMaxVolumes)
-                             ? occluded_instances(sv, vb, r, k)
-                             : is_occluded(sv, r, k, 1u);
-        if (occ) w.occb[slot] = 1u;
-    }
-    flush_counters(k, 0u, ctr, VPX_STAGE_SHADOW);
-}
-
-// L0 (level 0): one tile per workgroup; later levels: the live list, 256 entries per grab.
-template <bool L0>
-__global__ __launch_bounds__(256) VPX_WPE(VPX_WPE_MULTI_SHADOW) void k_shadow_inst(SceneView sv, WaveBufs w, int level,
-                                                                                  unsigned long long* __restrict__ ctr) {
-    __shared__ float4 vb[2 * kTlasMaxVolumes];
-    if (VPX_INST_MASK && threadIdx.x < 2u * sv.num_volumes && threadIdx.x < 2u * kTlasMaxVolumes)
-        vb[threadIdx.x] = sv.vbounds[threadIdx.x];  // published by the barriers in the chunk
-    if (L0) {
-        shadow_inst_chunk(sv, w, ctr, vb, tile_block() * 256u + threadIdx.x);
-        return;
-    }
-    const uint32_t n = live_count(w, level);
-    if (blockIdx.x * 256u >= n) return;  // one chunk per workgroup (k_nearest_tile)
-    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-    shadow_inst_chunk(sv, w, ctr, vb, i < n ? live_path(w, level, i) : ~0u);
-}
-
 // The rest of Renderer::IsOccluded (volumes 1.., then the shapes) for the shadow pool's slot
 // list (slots the world left unoccluded whose segment may meet a later volume): the same
-// per-slot loop as k_shadow_inst, over a dense list instead of every slot of every tile — C4's
-// ~16 k candidate slots per frame had cost a scan of all 25 M slots' flags and rays.
+// per-slot loop k_shadow_inst ran (round 5) over every slot of every tile, now over a dense
+// list — C4's ~16 k candidate slots per frame had cost a scan of all 25 M slots' flags and rays
+// (with lane_volumes: C4 32.5 -> 30.2 ms per step).
 // Persistent workgroups striding over the list (its length is on the device).
-__global__ __launch_bounds__(256) VPX_WPE(VPX_WPE_MULTI_SHADOW) void k_shadow_slots(SceneView sv, WaveBufs w, int level,
+// 4 waves/SIMD (106 VGPRs, no spills): C4 29.82-29.83 ms per step vs 29.66-29.81 at 5 (5 spilled
+// VGPRs) and 30.25-30.36 at 6 (42 spilled, 96 B of scratch per lane).
+#ifndef VPX_WPE_SHADOW_SLOTS
+#define VPX_WPE_SHADOW_SLOTS 4
+#endif
+__global__ __launch_bounds__(256) VPX_WPE(VPX_WPE_SHADOW_SLOTS) void k_shadow_slots(SceneView sv, WaveBufs w, int level,
                                                                                    unsigned long long* __restrict__ ctr) {
     __shared__ float4 vb[2 * kTlasMaxVolumes];
     if (VPX_INST_MASK && threadIdx.x < 2u * sv.num_volumes && threadIdx.x < 2u * kTlasMaxVolumes)

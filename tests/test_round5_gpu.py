@@ -1,8 +1,8 @@
 """Round-5 GPU parity: world updates between frames that the instance kernels' culls depend on.
 
-k_shadow_inst culls shadow slots by the instance TLAS's root box and FindNearest's instance
-pass by the TLAS and the volumes' bounding spheres, so d_volumes, d_vbounds and the TLAS must
-change together (vpx_set_volumes rebuilds all three).  Here the instances move between two
+The shadow pool lists only the slots whose segment meets the instance TLAS's root box, and
+the instance walks cull by the TLAS and the volumes' world boxes, so d_volumes, d_vbounds and
+the TLAS must change together (vpx_set_volumes rebuilds all three).  Here the instances move between two
 accumulated frames (their transforms permuted, so every index gets another place) and the
 accumulator, screen and counts must still equal the oracle's, which has no culls at all.
 """
