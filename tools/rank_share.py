@@ -22,6 +22,8 @@ ctx = pkg.context.Context(0)
 ctx.set_stream(s.cuda_stream)
 ctx.load_scene(desc)
 ctx.set_pipeline(int(os.environ.get("PIPE", "0")))
+if os.environ.get("ARITH", "x86") == "x86":  # the bench line's arithmetic (VPX_ARITH_X86_HOST)
+    ctx.set_arithmetic(pkg.abi.VPX_ARITH_X86_HOST)
 W, H = desc.width, desc.height
 spp = max(1, int(desc.spp))
 out = []
@@ -47,7 +49,7 @@ for R in (1, 2, 4, 8):
     out.append((R, ms, issue))
     del acc, rgb
 base = out[0][1]
-print(cfg, f"pipe={os.environ.get('PIPE', '0')}", " ".join(f"R={R}: {ms:.4f} ms (x{base / ms:.2f})" for R, ms, _ in out))
+print(cfg, f"pipe={os.environ.get('PIPE', '0')} arith={os.environ.get('ARITH', 'x86')}", " ".join(f"R={R}: {ms:.4f} ms (x{base / ms:.2f})" for R, ms, _ in out))
 if os.environ.get("ISSUE"):
     print("  host issue ms per step:", " ".join(f"R={R}: {i:.4f}" for R, _, i in out))
 ctx.close()
