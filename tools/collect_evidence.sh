@@ -3,7 +3,7 @@
 # GPU-suite tail, rank shares, PMC traffic and counters.  Runs here, not on the GPU box.
 set -eu
 cd "$(dirname "$0")/.."
-TAG=${TAG:-r05}
+TAG=${TAG:-r06}
 E=gpurun_out/ev
 if [ -f $E/gputests.log ]; then tail -3 $E/gputests.log > profiles/${TAG}_gputests_tail.txt; fi
 for c in C1 C2 C3 C4 Z1; do

@@ -10,7 +10,7 @@
 set -u
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out/ev
 export TMPDIR=/tmp
-TAG=${TAG:-r05}
+TAG=${TAG:-r06}
 O=gpurun_out/ev
 step() { name=$1; shift; echo "== $name"; timeout -k 10 "$@" > $O/$name.log 2>&1; rc=$?; echo "$name rc=$rc"; grep -v amdgpu.ids $O/$name.log | tail -${TAILN:-2} | cut -c1-300; if [ $rc -ne 0 ]; then exit $rc; fi; }
 sha256sum raytracer-voxpopuli_amd/libvpx_hip.so | tee $O/lib.sha256
@@ -25,6 +25,7 @@ if [ "${PART:-1}" = 1 ]; then
   step share_C3 300 env CFG=C3 PIPE=3 python tools/rank_share.py
   step share_C3p4 300 env CFG=C3 PIPE=4 python tools/rank_share.py
   step share_C4p4 600 env CFG=C4 PIPE=4 K=5 python tools/rank_share.py
+  step share_C4p3 600 env CFG=C4 PIPE=3 K=5 python tools/rank_share.py
 else
   declare -A WH=([C1]="1920 1080" [C2]="1920 1080" [C3]="3840 2160" [C4]="3840 2160" [Z1]="1920 1080")
   for c in ${PMC_CFGS:-C1 C2 C3 C4 Z1}; do
