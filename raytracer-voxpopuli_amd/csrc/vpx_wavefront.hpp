@@ -1715,7 +1715,14 @@ __global__ __launch_bounds__(256) void k_resolve_finish(SceneView sv, FrameArgs 
 // paths (Z1 at 1920x1080: 192 k at level 5, 3.7 k at level 14), so the kernel's registers (the
 // whole chain inlined) and low occupancy cost little, while each of those levels cost ~0.2 ms
 // of launches and latency chains in the per-level kernels.
-__global__ __launch_bounds__(256) VPX_WPE(2) void k_tail(SceneView sv_, FrameArgs f, WaveBufs w, int level,
+// Its occupancy (round 6, Z1 ms per step, two interleaved runs): 2 waves/SIMD (172 VGPRs, SGPR
+// spills only, to VGPR lanes) 1.488 / 1.495, 3 (168, 10 spilled VGPRs) 1.491 / 1.507, 4 (128, 80
+// spilled, 212 B of scratch) 1.521 / 1.531 — the deep levels hold too few paths for a third wave
+// per SIMD to find work, so the kernel costs its longest path's chain either way.
+#ifndef VPX_WPE_TAIL
+#define VPX_WPE_TAIL 2
+#endif
+__global__ __launch_bounds__(256) VPX_WPE(VPX_WPE_TAIL) void k_tail(SceneView sv_, FrameArgs f, WaveBufs w, int level,
                                                       unsigned long long* __restrict__ ctr) {
     Counters kn{0u, 0u, 0u}, ks{0u, 0u, 0u}, kh{0u, 0u, 0u};
     const uint32_t n = live_count(w, level);
