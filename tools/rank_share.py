@@ -27,7 +27,7 @@ if os.environ.get("ARITH", "x86") == "x86":  # the bench line's arithmetic (VPX_
 W, H = desc.width, desc.height
 spp = max(1, int(desc.spp))
 out = []
-for R in (1, 2, 4, 8):
+for R in [int(x) for x in os.environ.get("RS", "1,2,4,8").split(",")]:
     L = ctx.packed_len(W, H, R)
     acc = torch.zeros(L * 4, dtype=torch.float32, device="cuda")
     rgb = torch.zeros(L, dtype=torch.int32, device="cuda")
