@@ -870,7 +870,14 @@ int launch_render(vpx_ctx* c, hipStream_t s, vpx_ctx::WaveStore& ws, const Scene
     // the pool, the rest of the loop for the slots the world left unoccluded: k_shadow_inst per
     // tile (round 3: C4 51.7 -> 47.6 ms per 16-spp step), then (round 6) k_shadow_slots over the
     // pool's list of the slots whose segment may meet a later volume.
-    const bool spool = !rp && S > 1;
+// Round 6: single-volume frames with one slot per path (C2's point light) through the pool
+// too — C2 at 3 lanes 2.294-2.353 vs 2.352-2.400 ms per step (three interleaved runs; at 2
+// lanes with forks 2.45-2.47 vs 2.40-2.41).  (Round 3, before the live lists and the lanes'
+// double buffers, it had measured 2.83 vs 2.64-2.71.)
+#ifndef VPX_SPOOL_ONE_SLOT
+#define VPX_SPOOL_ONE_SLOT 1
+#endif
+    const bool spool = !rp && (S > 1 || (one && VPX_SPOOL_ONE_SLOT));
     if (!spool) w.occb = nullptr;  // k_resolve reads the slots' SD flags
     const uint32_t sgrab = std::max(1u, std::min(4u, kShadowList / (64u * S)));
     // persistent launches over a level's live list (its length is on the device): as many
