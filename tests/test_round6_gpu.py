@@ -1,0 +1,110 @@
+"""Round-6 GPU parity: the instance paths the round added, each against the oracle bit for bit.
+
+- Depth-0 frames of multi-volume scenes shade the paths that cannot meet an instance in the
+  world head and defer the others to k_instances (DEFER); deeper frames keep the per-tile pass.
+- The shadow pool lists the slots a later volume may occlude and k_shadow_slots walks only
+  those (with shapes in the scene every unoccluded slot is listed).
+- Instances that share one grid walk each lane's own next candidate in one walk (lane_volumes,
+  SceneView::inst_grid); instances of different grids keep the wave's union of candidates.
+Scenes: a world plus a lattice of rotated, scaled instances (C4's shape), their grids shared or
+alternating between two, with area lights (several slots per path), with and without an
+analytic sphere, at depths 0 and 2, serial and with frames in flight.
+Also: the library loaded before torch in a fresh process still finds the device.
+"""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():
+    pytest.skip("no GPU", allow_module_level=True)
+
+from cases import bits  # noqa: E402
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def lattice_scene(pkg, grids, depth, sphere=False, n_inst=27):
+    sc, abi = pkg.scene, pkg.abi
+    desc = sc.model_scene("monu3", 64, 64, 48, depth, city_lights=True)
+    size, vox, _ = sc.load_model("monu3")
+    desc.grids.append(sc.GridSpec(n=32, dense=sc.load_model_grid(size, vox, 32)))
+    if grids == 2:
+        desc.grids.append(sc.GridSpec(n=16, dense=sc.load_model_grid(size, vox, 16)))
+    rng = np.random.default_rng(7)
+    vols = [sc.volume()]
+    for k in range(n_inst):
+        i, j, l = k % 3, (k // 3) % 3, k // 9
+        pos = (0.3 * i - 0.2, 0.5 + 0.25 * j, 0.3 * l - 0.2)
+        vols.append(sc.volume(pos, tuple(rng.uniform(0.08, 0.16, 3)), tuple(rng.uniform(-2, 2, 3)),
+                              grid_id=1 + (k % grids)))
+    desc.volumes = (abi.Volume * len(vols))(*vols)
+    desc.areas = [sc.area_light((0.5, 2.2, 0.5), radius=0.5), sc.area_light((-0.8, 1.5, 0.2), radius=0.3)]
+    desc.area_samples = 3
+    if sphere:
+        desc.spheres = [abi.Sphere(abi.vec3((0.35, 0.9, 0.3)), 0.12, 8)]
+    desc.flags = abi.VPX_FLAG_AA
+    return desc
+
+
+def render(pkg, desc, frames, lanes=0):
+    ctx = pkg.context.Context(0)
+    s = torch.cuda.Stream()
+    ctx.set_stream(s.cuda_stream)
+    ctx.load_scene(desc)
+    ctx.set_pipeline(lanes)
+    W, H = desc.width, desc.height
+    acc = torch.zeros(W * H * 4, dtype=torch.float32, device="cuda")
+    rgb = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    ctx.counters(reset=True)
+    with torch.cuda.stream(s):
+        for f in range(frames):
+            ctx.render(desc.frame_params(f), acc.data_ptr(), rgb.data_ptr())
+    ctx.synchronize()
+    st = ctx.counters()
+    out = (bits(acc.cpu().numpy().reshape(-1, 4)), rgb.cpu().numpy().view(np.uint32),
+           tuple(int(getattr(st, k)) for k in ("primary_rays", "shadow_rays", "bounce_rays", "dda_cells")))
+    ctx.close()
+    return out
+
+
+def oracle(orc, pkg, desc, frames):
+    o = orc.Oracle(pkg.abi, desc)
+    acc, tot = None, np.zeros(4, np.int64)
+    for f in range(frames):
+        acc, rgb, st = o.render(desc.frame_params(f), accum=acc)
+        tot += [st.primary_rays, st.shadow_rays, st.bounce_rays, st.dda_cells]
+    return bits(acc), rgb.view(np.uint32), tuple(int(x) for x in tot)
+
+
+@pytest.mark.parametrize("grids", [1, 2])
+@pytest.mark.parametrize("depth", [0, 2])
+@pytest.mark.parametrize("sphere", [False, True])
+def test_instance_paths_bit_exact(pkg, orc, grids, depth, sphere):
+    desc = lattice_scene(pkg, grids, depth, sphere)
+    frames = 2
+    a_o, r_o, c_o = oracle(orc, pkg, desc, frames)
+    for lanes in (0, 3):
+        a_g, r_g, c_g = render(pkg, desc, frames, lanes)
+        assert np.array_equal(a_g, a_o), f"accumulator differs ({lanes} lanes)"
+        assert np.array_equal(r_g, r_o), f"RGB8 differs ({lanes} lanes)"
+        assert c_g == c_o, (lanes, c_g, c_o)
+    assert c_o[1] > 0 and c_o[3] > 0
+
+
+def test_library_loaded_before_torch():
+    """A fresh process that loads libvpx_hip.so before importing torch (the package imports
+    torch first, abi.load_library) creates a context: one HIP runtime in the process."""
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "import __graft_entry__ as e\n"
+            "pkg = e.load_package(); pkg.abi.load_library()\n"
+            "import torch\n"
+            "c = pkg.context.Context(0); c.close(); print('ctx ok')\n") % REPO
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "ctx ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
