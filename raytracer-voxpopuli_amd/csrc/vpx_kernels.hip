@@ -877,7 +877,13 @@ int launch_render(vpx_ctx* c, hipStream_t s, vpx_ctx::WaveStore& ws, const Scene
 #ifndef VPX_SPOOL_ONE_SLOT
 #define VPX_SPOOL_ONE_SLOT 1
 #endif
-    const bool spool = !rp && (S > 1 || (one && VPX_SPOOL_ONE_SLOT));
+// Only for frames in flight: the serial frames (the context's stream, with the level fork)
+// keep the tile kernels — C2 serial 3.32-3.33 ms per frame vs 3.51-3.54 with the pool (tile
+// kernels everywhere: 3.31-3.35 serial, 2.35-2.39 in flight; three interleaved runs).
+#ifndef VPX_SPOOL_ONE_SERIAL
+#define VPX_SPOOL_ONE_SERIAL 0
+#endif
+    const bool spool = !rp && (S > 1 || (one && VPX_SPOOL_ONE_SLOT && (VPX_SPOOL_ONE_SERIAL || &ws != &c->wave)));
     if (!spool) w.occb = nullptr;  // k_resolve reads the slots' SD flags
     const uint32_t sgrab = std::max(1u, std::min(4u, kShadowList / (64u * S)));
     // persistent launches over a level's live list (its length is on the device): as many
