@@ -865,7 +865,9 @@ int launch_render(vpx_ctx* c, hipStream_t s, vpx_ctx::WaveStore& ws, const Scene
     // lights (several slots per path, long walks), except on the static-camera path (its
     // reprojection test reads the tile kernel's SD flags).  Measured (ms per step, two runs
     // each, pool / tile kernels): C3 3.72, 3.71 / 4.96, 4.94; C2 (one point light, one slot per
-    // path) 2.83, 2.84 / 2.64, 2.71 — so point / spot / directional lights keep the tile kernels.
+    // path) 2.83, 2.84 / 2.64, 2.71 (round 3) — so point / spot / directional lights kept the
+    // tile kernels; since round 6 single-volume frames in flight use the pool for them too
+    // (VPX_SPOOL_ONE_SLOT below: C2 -2.4 %).
     // Multi-volume / shape scenes: the world's walks (volume 0, first in IsOccluded's loop) in
     // the pool, the rest of the loop for the slots the world left unoccluded: k_shadow_inst per
     // tile (round 3: C4 51.7 -> 47.6 ms per 16-spp step), then (round 6) k_shadow_slots over the
