@@ -947,7 +947,12 @@ int launch_render(vpx_ctx* c, hipStream_t s, vpx_ctx::WaveStore& ws, const Scene
     prof_mark(c, s, -1);
     if (split) {
         prof_mark(c, s, VPX_STAGE_INSTANCES);
-        hipLaunchKernelGGL(defer ? k_instances<true> : k_instances<false>, grid, block, xlds, s, sv, f, w, c->d_ctr);
+        if (defer) {  // the deferred paths as a dense list (k_compact), then k_instances_list
+            hipLaunchKernelGGL(k_compact, dim3((P / 64u + 255u) / 256u), block, 0, s, w, 0);
+            hipLaunchKernelGGL(k_instances_list, grid, block, xlds, s, sv, f, w, c->d_ctr);
+        } else {
+            hipLaunchKernelGGL(k_instances, grid, block, xlds, s, sv, f, w, c->d_ctr);
+        }
         prof_mark(c, s, -1);
     }
     // FindNearest for the traced rays of the next level: the bounce pool (single volume, no

@@ -878,7 +878,7 @@ __device__ __forceinline__ bool meets_later_volume(const SceneView& sv, f3 o, f3
     return tlas_box(sv.tlas[0], o, world_inv(d), t);
 }
 
-// DEFER (multi-volume scenes without shapes at Trace depth 0, the head of k_instances<true>):
+// DEFER (multi-volume scenes without shapes at Trace depth 0, the head of k_instances_list):
 // after the world walk a path whose ray cannot meet a later volume (meets_later_volume) is
 // final — the head shades it from its LDS records like a single-volume head; the others are
 // written to HBM and flagged in amask (one ballot word per wave, unused at depth 0) for the
@@ -1040,9 +1040,6 @@ __global__ __launch_bounds__(256) void k_compact(WaveBufs w, int level) {
 // vs 42.90-43.09 ms per step (three interleaved runs): most C4 rays are candidates, and the
 // pass's HBM traffic is mostly the shade's three area-light slots per pixel (144 B), which the
 // shadow pool reads back, not the rays it re-reads.
-// DEFER: after k_primary<true, true, X86, true> — only the paths the head flagged in amask
-// (their rays and world hit records in HBM) are continued and shaded; the head shaded the rest.
-template <bool DEFER>
 __global__ __launch_bounds__(256) VPX_WPE(VPX_WPE_MULTI_NEAREST) void k_instances(SceneView sv_, FrameArgs f, WaveBufs w,
                                                                                 unsigned long long* __restrict__ ctr) {
     __shared__ uint32_t sh[4];
@@ -1055,13 +1052,10 @@ __global__ __launch_bounds__(256) VPX_WPE(VPX_WPE_MULTI_NEAREST) void k_instance
     const PathRay pr{w.O, w.D, w.H, w.HM, 0u};
     Counters k{0u, 0u, 0u};
     bool go = false;
-    if (DEFER) {
-        go = p < w.P && ((w.amask[p >> 6] >> (p & 63u)) & 1ull);
-    } else if (p < w.P && (__float_as_uint(w.D[p].w) & kActive)) {
+    if (p < w.P && (__float_as_uint(w.D[p].w) & kActive)) {
         const float4 o = w.O[p], d = w.D[p];
         go = meets_later_volume(sv, mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), w.H[p].x);
     }
-    const bool mine = go;  // (DEFER: the paths this pass shades)
 #ifdef VPX_DEBUG_NO_INST_WALK
     go = false;  // timing probe only (wrong images): the pass without its instance walks
 #endif
@@ -1089,12 +1083,53 @@ __global__ __launch_bounds__(256) VPX_WPE(VPX_WPE_MULTI_NEAREST) void k_instance
     flush_counters(k, 0u, ctr, VPX_STAGE_INSTANCES);
     __syncthreads();  // the tile's hit records, as the compacted lanes left them
     Counters ks{0u, 0u, 0u};
-    if (DEFER) {
-        if (mine) shade_path<true>(sv, f, w, pr, p, 0, ks);
-    } else {
-        const bool cont = shade_path<true>(sv, f, w, pr, p, 0, ks);
-        if (f.max_bounces > 0) put_amask(w, p, cont);
+    const bool cont = shade_path<true>(sv, f, w, pr, p, 0, ks);
+    if (f.max_bounces > 0) put_amask(w, p, cont);
+    flush_counters(ks, 0u, ctr, VPX_STAGE_SHADE);
+}
+
+// The deferred instance pass (depth 0, after k_primary<.., DEFER>): the head's amask bits
+// turned into live list 1 by k_compact (at Trace depth 0 the level lists are otherwise unused),
+// one list entry per lane — FindNearest continued from volume 1, then the path's level-0 shade
+// by the same lane, no tile barrier.  The same per-path operations as k_instances.  Per tile
+// instead (the deferred ~15 % of a tile's paths in its first wave, the shade after a tile
+// barrier): C4 29.77-29.91 vs 28.59-28.65 ms per step (three interleaved runs).
+// 4 waves/SIMD (128 VGPRs, 6 spilled): 28.62-28.69 vs 28.91-29.03 ms at 3 (134, none).
+#ifndef VPX_WPE_INST_LIST
+#define VPX_WPE_INST_LIST VPX_WPE_MULTI_NEAREST
+#endif
+__global__ __launch_bounds__(256) VPX_WPE(VPX_WPE_INST_LIST) void k_instances_list(SceneView sv_, FrameArgs f, WaveBufs w,
+                                                                                     unsigned long long* __restrict__ ctr) {
+    extern __shared__ uint32_t x86_lds[];
+    const uint32_t n = live_count(w, 1);
+    if (blockIdx.x * 256u >= n) return;  // (workgroup-uniform: before the staging barrier; the
+                                         // launch is sized for every path)
+    SceneView sv = sv_;
+    sv.x86 = x86_stage_lds(sv_.x86, x86_lds);
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    const PathRay pr{w.O, w.D, w.H, w.HM, 0u};
+    Counters k{0u, 0u, 0u}, ks{0u, 0u, 0u};
+    if (i < n) {
+        const uint32_t q = live_list(w, 1)[i];
+        {
+            const float4 o = w.O[q], d = w.D[q], h = w.H[q];
+            const uint32_t hm = w.HM[q];
+            Ray r;
+            r.O = mk(o.x, o.y, o.z);
+            r.D = mk(d.x, d.y, d.z);
+            r.t = h.x;
+            r.N = mk(h.y, h.z, h.w);
+            r.mat = hm & 0xffu;
+            r.inside = (hm & 0x80000000u) != 0u;
+            int32_t vox = (int32_t)((hm >> 8) & 0xffffu) - 2;
+            if (find_nearest_rest(sv, r, k, &vox)) {
+                w.H[q] = make_float4(r.t, r.N.x, r.N.y, r.N.z);
+                w.HM[q] = r.mat | ((uint32_t)(vox + 2) << 8) | (r.inside ? 0x80000000u : 0u);
+            }
+        }
+        shade_path<true>(sv, f, w, pr, q, 0, ks);
     }
+    flush_counters(k, 0u, ctr, VPX_STAGE_INSTANCES);
     flush_counters(ks, 0u, ctr, VPX_STAGE_SHADE);
 }
 
