@@ -1,7 +1,8 @@
 """Round-6 GPU parity: the instance paths the round added, each against the oracle bit for bit.
 
 - Depth-0 frames of multi-volume scenes shade the paths that cannot meet an instance in the
-  world head and defer the others to k_instances (DEFER); deeper frames keep the per-tile pass.
+  world head and defer the others (k_compact's list, k_instances_list); deeper frames keep the
+  per-tile k_instances.
 - The shadow pool lists the slots a later volume may occlude and k_shadow_slots walks only
   those (with shapes in the scene every unoccluded slot is listed).
 - Instances that share one grid walk each lane's own next candidate in one walk (lane_volumes,
@@ -9,7 +10,8 @@
 Scenes: a world plus a lattice of rotated, scaled instances (C4's shape), their grids shared or
 alternating between two, with area lights (several slots per path), with and without an
 analytic sphere, at depths 0 and 2, serial and with frames in flight.
-Also: the library loaded before torch in a fresh process still finds the device.
+Also: the static-camera branch over the lattice, and the library loaded before torch in a
+fresh process still finds the device.
 """
 import os
 import subprocess
@@ -108,3 +110,35 @@ def test_library_loaded_before_torch():
             "c = pkg.context.Context(0); c.close(); print('ctx ok')\n") % REPO
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "ctx ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
+
+
+@pytest.mark.parametrize("depth", [0, 2])
+def test_static_camera_reprojection_instances(pkg, orc, depth):
+    """Renderer::Tick's static branch (TraceReproject, renderer.cpp:1996-2101) over the instance
+    lattice: at depth 0 the deferred instance pass shades the paths a later volume may change,
+    including the reprojection's level-0 record; 3 frames, the live camera nudged after the
+    first, RGB8 and the illumination history bit-exact."""
+    sc = pkg.scene
+    desc = lattice_scene(pkg, 1, depth)
+    desc.flags = 0
+    r = pkg.renderer.Renderer(desc, 0)
+    r.Init()
+    r.staticCamera = True
+    o = orc.Oracle(pkg.abi, desc)
+    hist_o = np.zeros((desc.width * desc.height, 4), np.float32)
+    prev = sc.prev_camera(desc._cam_pos, desc._cam_target, desc.width, desc.height)
+    for f in range(3):
+        if f > 0:
+            pos = tuple(np.float32(v) + np.float32((0.0, 0.004, 0.04)[f]) for v in desc._cam_pos)
+            desc.camera = sc.look_at(pos, desc._cam_target, desc.width, desc.height)
+            r.ctx.set_camera(desc.camera)
+            o.set_camera(desc.camera)
+        st = r.Tick(0.0, stats=True)
+        torch.cuda.synchronize()
+        rgb_g = r.screen_host().reshape(-1).copy()
+        hist_g = r.history_host().reshape(-1, 4).copy()
+        rgb_o, ost = o.render_reproject(desc.frame_params(f), prev, hist_o)
+        assert np.array_equal(bits(hist_g), bits(hist_o)), f"frame {f}: history"
+        assert np.array_equal(rgb_g, rgb_o), f"frame {f}: rgb8"
+        assert (st.shadow_rays, st.bounce_rays, st.dda_cells) == (ost.shadow_rays, ost.bounce_rays, ost.dda_cells)
+    r.ctx.close()
