@@ -74,7 +74,9 @@ EXTRA_CONFIGS = ("C2", "C3", "C4", "Z1")
 # Round 5, with each lane's two sample buffers and the live lists (three interleaved runs): C2
 # 2.350-2.358 (2 lanes, forks) / 2.272-2.338 (3) / 2.412-2.441 (4), and 2.64-2.70 with forks
 # at 3 lanes; C4 42.80-42.99 (3) / 43.70-43.92 (4); Z1 1.755-1.769 (2) / 1.532-1.540 (3).
-PIPELINE = {"C1": 3, "C2": 3, "C3": 3, "C4": 3, "Z1": 3}
+# Round 6, accumulation windows (vpx_render_window, 4 frames a chain): C4 26.84-26.87 (4 lanes)
+# / 28.50-28.57 (3), profiles/r06_window_ab.txt.
+PIPELINE = {"C1": 3, "C2": 3, "C3": 3, "C4": 4, "Z1": 3}
 # A rank's share of a multi-GPU frame is a small launch: with each lane's two sample buffers
 # (round 5) four lanes keep more of it in flight for the big frames (rank 0's share at R = 8,
 # tools/rank_share.py, 3 / 4 lanes: C3 0.586 / 0.564 ms, C4 9.93 / 8.63 ms per 16-spp step;
@@ -234,12 +236,15 @@ def run_config(pkg, env, cfg, steps, warmup, weak=False, sha=None, pipeline=None
                                              host_gather=env.shared)
 
     def step():
-        for f in range(spp):  # accumulation window: w = 1/(f+1), per-frame seeds (renderer.cpp:1791-1828)
-            if sharded is None:
-                ctx.render(desc.frame_params(frame_index=f), acc.data_ptr(), rgb.data_ptr())
+        # accumulation window: w = 1/(f+1), per-frame seeds (renderer.cpp:1791-1828); one library
+        # call per window (vpx_render_window: a rank's small share of several frames per chain)
+        if sharded is None:
+            if spp == 1:
+                ctx.render(desc.frame_params(frame_index=0), acc.data_ptr(), rgb.data_ptr())
             else:
-                sharded.render(f)
-        if sharded is not None:
+                ctx.render_window(desc.frame_params(frame_index=0), spp, acc.data_ptr(), rgb.data_ptr())
+        else:
+            sharded.render_window(0, spp)
             sharded.publish()
 
     launches = spp * (4 * (desc.max_bounces + 1) + 4)  # stage launches per step, upper bound

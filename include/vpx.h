@@ -355,6 +355,20 @@ uint64_t vpx_tiles_packed_len(uint32_t width, uint32_t height, uint32_t tile_w,
 int vpx_render_tiles_accum(vpx_ctx* ctx, const vpx_frame_params* params, uint32_t tile_w,
                            uint32_t tile_h, uint32_t rank, uint32_t n_ranks, float* accum_packed,
                            uint32_t* rgb8_packed, vpx_stats* stats);
+/* Accumulation windows: frames frame_index .. frame_index + n_frames - 1 of params (the
+   reference's spp loop of Renderer::Tick calls, renderer.cpp:1646-1891, one per frame with
+   w = 1/(n+1)), with the same results as n_frames calls of vpx_render /
+   vpx_render_tiles_accum (bit-identical accumulator and RGB8).  When a frame's share is small
+   (a rank's 1/n_ranks of the tiles), several frames render in ONE chain of launches — frame b
+   in tile blocks [b*T, (b+1)*T) with its own seeds — and a single blend folds their samples
+   into the accumulator in frame order; large frames render one chain each.  Lanes
+   (vpx_set_pipeline) carry the chains as they carry frames.  VPX_FLAG_NO_TONEMAP frames and
+   device sets (vpx_create_multi) render frame by frame. */
+int vpx_render_window(vpx_ctx* ctx, const vpx_frame_params* params, uint32_t n_frames, float* accum,
+                      uint32_t* rgb8);
+int vpx_render_tiles_accum_window(vpx_ctx* ctx, const vpx_frame_params* params, uint32_t n_frames,
+                                  uint32_t tile_w, uint32_t tile_h, uint32_t rank, uint32_t n_ranks,
+                                  float* accum_packed, uint32_t* rgb8_packed);
 /* Rank 0: scatter n_ranks gathered packed RGB8 buffers (back to back, DEVICE) into the
    screen rgb8 (uint32[W*H], DEVICE). */
 int vpx_composite_rgb8(vpx_ctx* ctx, const vpx_frame_params* params, uint32_t tile_w,

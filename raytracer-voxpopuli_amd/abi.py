@@ -160,6 +160,9 @@ SIGNATURES = {
                                          C.c_uint32, C.c_void_p, C.c_void_p, C.POINTER(Stats)]),
     "vpx_composite_rgb8": (C.c_int, [C.c_void_p, C.POINTER(FrameParams), C.c_uint32, C.c_uint32, C.c_uint32,
                                      C.c_void_p, C.c_void_p]),
+    "vpx_render_window": (C.c_int, [C.c_void_p, C.POINTER(FrameParams), C.c_uint32, C.c_void_p, C.c_void_p]),
+    "vpx_render_tiles_accum_window": (C.c_int, [C.c_void_p, C.POINTER(FrameParams), C.c_uint32, C.c_uint32,
+                                                C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p]),
     "vpx_tiles_packed_len": (C.c_uint64, [C.c_uint32] * 5),
     "vpx_composite_tiles": (C.c_int, [C.c_void_p, C.POINTER(FrameParams), C.c_uint32, C.c_uint32, C.c_uint32,
                                       C.c_void_p, C.c_void_p, C.c_void_p]),

@@ -154,6 +154,19 @@ class Context:
                                                   C.byref(st) if st is not None else None), "vpx_render_tiles_accum")
         return st
 
+    def render_window(self, params, n_frames, accum_ptr, rgb_ptr=None):
+        """Frames params.frame_index .. + n_frames - 1 accumulated in order (vpx_render_window):
+        the results of n_frames render() calls; small frames share one chain of launches."""
+        self._chk(self.lib.vpx_render_window(self.h, C.byref(params), n_frames, C.c_void_p(accum_ptr),
+                                             C.c_void_p(rgb_ptr or 0)), "vpx_render_window")
+
+    def render_tiles_accum_window(self, params, n_frames, rank, n_ranks, accum_packed_ptr, rgb_packed_ptr, tile=16):
+        """render_tiles_accum over an accumulation window (vpx_render_tiles_accum_window): the
+        rank's share of several frames in one chain of launches."""
+        self._chk(self.lib.vpx_render_tiles_accum_window(self.h, C.byref(params), n_frames, tile, tile, rank, n_ranks,
+                                                         C.c_void_p(accum_packed_ptr), C.c_void_p(rgb_packed_ptr)),
+                  "vpx_render_tiles_accum_window")
+
     def composite_rgb8(self, params, n_ranks, gathered_ptr, rgb_ptr, tile=16):
         self._chk(self.lib.vpx_composite_rgb8(self.h, C.byref(params), tile, tile, n_ranks, C.c_void_p(gathered_ptr),
                                               C.c_void_p(rgb_ptr)), "vpx_composite_rgb8")

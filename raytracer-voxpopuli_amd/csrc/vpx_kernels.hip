@@ -92,6 +92,40 @@ __global__ __launch_bounds__(kThreads) void blend_packed(FrameArgs f, const floa
     }
 }
 
+// Frame weights of one window chain (renderer.cpp:1651's 1/(n+1), computed on the host as
+// frame_of does, so every blend uses the per-frame path's exact weights).
+constexpr uint32_t kMaxWindow = 64;
+struct WindowWeights {
+    float w[kMaxWindow], iw[kMaxWindow];
+};
+
+// An accumulation window's samples (frame b of the chain at [b*T*256, (b+1)*T*256)) folded
+// into the accumulator in frame order: per pixel the same blend of the same samples as B
+// calls of k_finish / composite_tiles / blend_packed, and the tonemap of the last.  image:
+// the one-GPU image (accum/rgb8 indexed by pixel); else a rank's packed accumulator.
+__global__ __launch_bounds__(kThreads) void blend_window(FrameArgs f, const float4* __restrict__ sample, uint32_t B,
+                                                         WindowWeights ww, int image, float4* __restrict__ accum,
+                                                         uint32_t* __restrict__ rgb8) {
+    const uint32_t T = f.batch_tiles;
+    const uint32_t p = blockIdx.x * kThreads + threadIdx.x;
+    uint32_t x, y;
+    const bool valid = path_pixel(f, p, x, y);
+    if (image && !valid) return;
+    const uint64_t a_at = image ? (uint64_t)y * f.width + x : p;
+    if (!valid) {
+        accum[a_at] = make_float4(0.f, 0.f, 0.f, 0.f);
+        rgb8[a_at] = 0u;
+        return;
+    }
+    float4 a = accum[a_at];
+    for (uint32_t b = 0; b < B; ++b) {
+        const float4 s = sample[((uint64_t)b * T << 8) + p];
+        a = blend(a, mk(s.x, s.y, s.z), ww.w[b], ww.iw[b]);
+    }
+    accum[a_at] = a;
+    if (rgb8) rgb8[a_at] = tonemap_pack(a);
+}
+
 // Rank-0 scatter of the gathered packed RGB8 tiles (sharded-accumulator flow).
 __global__ __launch_bounds__(kThreads) void composite_rgb8(FrameArgs f, const uint32_t* __restrict__ gathered,
                                                            uint32_t* __restrict__ rgb8) {
@@ -528,6 +562,9 @@ struct vpx_ctx {
     // static-camera path images (float4[W*H] each): albedo, illumination, ray data, temp
     float4* rp_buf = nullptr;
     size_t rp_pixels = 0;
+    // a window chain's samples when no lanes run (vpx_render_window)
+    float4* win_buf = nullptr;
+    size_t win_len = 0;
     // device set (vpx_create_multi): one member context per device; this context only
     // forwards (VPX_GROUP_*) and runs the tile-sharded vpx_render (group_render)
     std::vector<vpx_ctx*> members;
@@ -715,6 +752,7 @@ FrameArgs frame_of(const vpx_ctx* c, const vpx_frame_params* p, uint32_t rank, u
     f.rank = rank;
     f.n_ranks = n_ranks;
     f.tiles_per_rank = (f.num_tiles + n_ranks - 1) / n_ranks;
+    f.batch_tiles = 0;
     return f;
 }
 
@@ -901,7 +939,7 @@ int launch_render(vpx_ctx* c, hipStream_t s, vpx_ctx::WaveStore& ws, const Scene
             hipLaunchKernelGGL(k_shadow_slots, dim3(std::min(tiles * S, c->cus * (uint32_t)VPX_WPE_SHADOW_SLOTS)), block, 0, s, sv,
                                w, level, c->d_ctr);
     };
-    if (one && fuse_tail && f.max_bounces == 0 && tiles <= kFuseFrameTiles && S == 1) {
+    if (one && fuse_tail && f.max_bounces == 0 && tiles <= kFuseFrameTiles && S == 1 && !f.batch_tiles) {
         // the whole depth-0 frame in one launch (k_frame0), its path state and one shadow slot
         // per path in LDS; with area lights the frame splits to use the shadow pool
         prof_mark(c, s, VPX_STAGE_FRAME);
@@ -1243,6 +1281,7 @@ int vpx_destroy(vpx_ctx* c) {
         if (p) (void)hipFree(p);
     for (hipEvent_t e : c->prof_ev) (void)hipEventDestroy(e);
     if (c->rp_buf) (void)hipFree(c->rp_buf);
+    if (c->win_buf) (void)hipFree(c->win_buf);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->ev2) (void)hipEventDestroy(c->ev2);
@@ -1987,6 +2026,96 @@ static int render_tiles_impl(int MODE, vpx_ctx* c, const vpx_frame_params* p, ui
         stats->total_ms = ms;
     }
     return VPX_OK;
+}
+
+// Tiles per window chain: frames join a chain while it holds at most this many tiles, and
+// (with lanes) a window keeps at least one chain per lane.  C4 (32400 tiles a frame, 16 spp,
+// 4 lanes): one GPU renders 4 chains of 4 frames (26.9 ms a step against 28.5 frame by
+// frame), rank 0 of 8 (4050 tiles) 4 chains of 4 frames (3.7 ms against 7.3): profiles/r06_window_ab.txt.
+#ifndef VPX_WINDOW_TILES
+#define VPX_WINDOW_TILES 131072
+#endif
+#ifndef VPX_WINDOW_LANE_CAP
+#define VPX_WINDOW_LANE_CAP 1
+#endif
+
+static int render_window_impl(vpx_ctx* c, const vpx_frame_params* p, uint32_t n, uint32_t rank, uint32_t n_ranks,
+                              bool image, float* accum, uint32_t* rgb8) {
+    if (!c) return VPX_E_INVALID;
+    int rc = validate_frame(c, p);
+    if (rc) return rc;
+    if (n == 0) return VPX_OK;
+    if (image ? !accum : (!accum || !rgb8)) return fail(c, VPX_E_INVALID, "null accumulator buffer");
+    if (n_ranks == 0 || rank >= n_ranks) return fail(c, VPX_E_INVALID, "bad rank");
+    const FrameArgs f0 = frame_of(c, p, rank, n_ranks);
+    const uint32_t T = image ? f0.num_tiles : f0.tiles_per_rank;
+    uint32_t bmax = std::min<uint32_t>(kMaxWindow, std::max<uint32_t>(1u, VPX_WINDOW_TILES / T));
+    // at least one chain per lane, so the lanes keep chains in flight as they do frames
+    if (VPX_WINDOW_LANE_CAP && c->lanes.size() > 1)
+        bmax = std::min<uint32_t>(bmax, std::max<uint32_t>(1u, (n + (uint32_t)c->lanes.size() - 1) / (uint32_t)c->lanes.size()));
+    // the shadow lists pack a path index into 27 bits (validate_frame's bound per chain)
+    while (bmax > 1 && (uint64_t)bmax * T * kTilePix > (1ull << 27)) --bmax;
+    const bool per_frame = bmax == 1 || n == 1 || (p->flags & VPX_FLAG_NO_TONEMAP) || !c->members.empty();
+    for (uint32_t i = 0; i < n;) {
+        vpx_frame_params q = *p;
+        q.frame_index = p->frame_index + i;
+        if (per_frame) {
+            rc = image ? vpx_render(c, &q, accum, rgb8, nullptr)
+                       : vpx_render_tiles_accum(c, &q, kTile, kTile, rank, n_ranks, accum, rgb8, nullptr);
+            if (rc) return rc;
+            ++i;
+            continue;
+        }
+        const uint32_t B = std::min(bmax, n - i);
+        VPX_HIP(c, hipSetDevice(c->device));
+        const SceneView sv = view_of(c, q.sky, q.area_samples, (q.flags & VPX_FLAG_SKY) != 0);
+        FrameArgs f = frame_of(c, &q, rank, n_ranks);
+        f.batch_tiles = T;
+        WindowWeights ww;
+        for (uint32_t b = 0; b < B; ++b) {  // frame_of's weight per frame
+            ww.w[b] = 1.0f / ((float)(q.frame_index + b) + 1.0f);
+            ww.iw[b] = 1.0f - ww.w[b];
+        }
+        float4* samples = nullptr;
+        vpx_ctx::Lane* L = nullptr;
+        if (!c->lanes.empty()) {
+            if ((rc = lane_render(c, sv, f, B * T, nullptr, L))) return rc;
+            samples = L->cur;
+        } else {
+            const size_t need = (size_t)B * T * kTilePix;
+            if (c->win_len < need) {
+                VPX_HIP(c, hipStreamSynchronize(c->stream));
+                if (c->win_buf) (void)hipFree(c->win_buf);
+                c->win_buf = nullptr;
+                c->win_len = 0;
+                VPX_HIP(c, hipMalloc(&c->win_buf, sizeof(float4) * need));
+                c->win_len = need;
+            }
+            samples = c->win_buf;
+            if ((rc = launch_render<kFinishPackedSample>(c, c->stream, c->wave, sv, f, B * T, nullptr, nullptr,
+                                                         samples)))
+                return rc;
+        }
+        hipLaunchKernelGGL(blend_window, dim3(T), dim3(kThreads), 0, c->stream, f, samples, B, ww, image ? 1 : 0,
+                           reinterpret_cast<float4*>(accum), rgb8);
+        VPX_HIP(c, hipGetLastError());
+        if (L) VPX_HIP(c, hipEventRecord(L->cur_consumed, c->stream));
+        i += B;
+    }
+    return VPX_OK;
+}
+
+int vpx_render_window(vpx_ctx* c, const vpx_frame_params* p, uint32_t n_frames, float* accum, uint32_t* rgb8) {
+    return render_window_impl(c, p, n_frames, 0, 1, true, accum, rgb8);
+}
+
+int vpx_render_tiles_accum_window(vpx_ctx* c, const vpx_frame_params* p, uint32_t n_frames, uint32_t tile_w,
+                                  uint32_t tile_h, uint32_t rank, uint32_t n_ranks, float* accum_packed,
+                                  uint32_t* rgb8_packed) {
+    VPX_GROUP_FIRST(c, vpx_render_tiles_accum_window(m_, p, n_frames, tile_w, tile_h, rank, n_ranks, accum_packed,
+                                                     rgb8_packed));
+    if (c && (tile_w != kTile || tile_h != kTile)) return fail(c, VPX_E_INVALID, "tiles must be 16x16");
+    return render_window_impl(c, p, n_frames, rank, n_ranks, false, accum_packed, rgb8_packed);
 }
 
 int vpx_render_tiles(vpx_ctx* c, const vpx_frame_params* p, uint32_t tile_w, uint32_t tile_h, uint32_t rank,

@@ -54,6 +54,9 @@ struct FrameArgs {
     uint32_t tiles_x, tiles_y, num_tiles;
     uint32_t rank, n_ranks;
     uint32_t tiles_per_rank;
+    // an accumulation window rendered in one chain (vpx_render_window): paths of frame
+    // frame_index + b fill tile blocks [b*batch_tiles, (b+1)*batch_tiles); 0 = one frame
+    uint32_t batch_tiles;
 };
 
 // Per-path level forms: level l's 2-bit form at bits 2l..2l+1 and a sentinel 1 just above
@@ -248,14 +251,26 @@ __device__ __forceinline__ void tile_lane_xy(uint32_t lane, uint32_t& lx, uint32
 }
 // Path index -> pixel: path p = j*256 + lane covers the j-th tile of this rank
 // (tile = rank + j*n_ranks), lane as tile_lane_xy.
-__device__ __forceinline__ bool path_pixel(const FrameArgs& f, uint32_t p, uint32_t& x, uint32_t& y) {
-    const uint32_t j = p >> 8, lane = p & 255u;
+__device__ __forceinline__ bool tile_pixel(const FrameArgs& f, uint32_t j, uint32_t lane, uint32_t& x, uint32_t& y) {
     const uint32_t tile = f.rank + j * f.n_ranks;
     uint32_t lx, ly;
     tile_lane_xy(lane, lx, ly);
     x = (tile % f.tiles_x) * kTileW + lx;
     y = (tile / f.tiles_x) * kTileW + ly;
     return tile < f.num_tiles && x < f.width && y < f.height;
+}
+// A window chain's frame b holds tile blocks [b*batch_tiles, (b+1)*batch_tiles).
+__device__ __forceinline__ bool path_pixel(const FrameArgs& f, uint32_t p, uint32_t& x, uint32_t& y) {
+    const uint32_t j = p >> 8;
+    return tile_pixel(f, f.batch_tiles ? j % f.batch_tiles : j, p & 255u, x, y);
+}
+// Paths of frames that never join a window chain (the static-camera path).
+__device__ __forceinline__ bool path_pixel_single(const FrameArgs& f, uint32_t p, uint32_t& x, uint32_t& y) {
+    return tile_pixel(f, p >> 8, p & 255u, x, y);
+}
+// The frame of path p in a window chain (FrameArgs::batch_tiles).
+__device__ __forceinline__ uint32_t path_frame(const FrameArgs& f, uint32_t p) {
+    return f.frame_index + (f.batch_tiles ? (p >> 8) / f.batch_tiles : 0u);
 }
 
 // Sum over the wave (every lane gets it).  DPP row shifts / mirrors rather than __shfl_xor:
@@ -468,7 +483,7 @@ __device__ __forceinline__ bool shade_path(const SceneView& sv, const FrameArgs&
             ray.inside = L0 ? false : (hm & 0x80000000u) != 0u;
             if ((f.flags & kFlagReproject) && level == 0) {  // RayDataReproject::GetRayInfo (renderer.h:31-34)
                 uint32_t x, y;
-                if (path_pixel(f, p, x, y)) {
+                if (path_pixel_single(f, p, x, y)) {
                     const f3 ip = ray_point(ray);
                     w.RD[(uint64_t)y * f.width + x] = make_float4(ip.x, ip.y, ip.z, __uint_as_float(ray.mat));
                 }
@@ -906,7 +921,7 @@ __device__ __forceinline__ void primary_tile(const SceneView& sv, const FrameArg
         r.O = r.D = mk(0.f, 0.f, 0.f);
         uint32_t rng = 0, flags = 0;
         if (go) {
-            Rng g{pixel_seed(f.seed_base, f.frame_index, f.width, f.height, x, y)};
+            Rng g{pixel_seed(f.seed_base, path_frame(f, p), f.width, f.height, x, y)};
             r = primary_ray(f, x, y, g, sv.x86);
             rng = g.s;
             prim = 1;
@@ -1674,7 +1689,8 @@ __device__ __forceinline__ void finish_path(const FrameArgs& f, const WaveBufs& 
                                             const LightSum* ls = nullptr) {
     if (p >= w.P) return;
     uint32_t x, y;
-    const bool valid = path_pixel(f, p, x, y);
+    // window chains finish into packed samples only
+    const bool valid = MODE == kFinishPackedSample ? path_pixel(f, p, x, y) : path_pixel_single(f, p, x, y);
     f3 v = mk(0.f, 0.f, 0.f);
     if (valid) {
         const uint32_t forms = w.forms[p];
@@ -1861,9 +1877,11 @@ constexpr uint32_t kFuseFrameTiles = VPX_FUSE_FRAME_TILES;
 // as p (level 0 and slot 0 only: every index is p).  HBM sees the accumulator / screen.
 template <bool ONE, int MODE, bool X86 = false>
 __global__ __launch_bounds__(256) VPX_WPE(ONE ? VPX_WPE_FRAME : VPX_WPE_MULTI_NEAREST) void k_frame0(
-    SceneView sv_, FrameArgs f, WaveBufs w, unsigned long long* __restrict__ ctr, float4* __restrict__ accum,
+    SceneView sv_, FrameArgs f_, WaveBufs w, unsigned long long* __restrict__ ctr, float4* __restrict__ accum,
     uint32_t* __restrict__ rgb8, float4* __restrict__ packed) {
     const SceneView sv = arith_view<X86>(sv_);
+    FrameArgs f = f_;
+    f.batch_tiles = 0;  // window chains do not take this launch (launch_render)
     __shared__ HeadLds<true> L;
     __shared__ float4 s_val[256];  // LA (a) or leaf of the path's one level
     __shared__ float4 s_sm[256];   // SM: the pending light
@@ -1916,7 +1934,7 @@ __global__ __launch_bounds__(256) void k_finish_reproject(FrameArgs f, WaveBufs 
     const uint32_t p = blockIdx.x * 256u + threadIdx.x;
     if (p >= w.P) return;
     uint32_t x, y;
-    if (!path_pixel(f, p, x, y)) return;
+    if (!path_pixel_single(f, p, x, y)) return;
     const uint64_t px = (uint64_t)y * f.width + x;
     f3 A = mk(0.f, 0.f, 0.f), I = mk(0.f, 0.f, 0.f);  // TraceReproject(ray, depth < 0) = {0, 0}
     if (f.max_bounces < 0) {
@@ -1970,7 +1988,7 @@ __global__ __launch_bounds__(256) void k_reproject_setup(FrameArgs f, WaveBufs w
     uint32_t x, y;
     uint32_t slots = 0;
     w.SM[p] = make_float4(0.f, 0.f, 0.f, __uint_as_float(0u));
-    if (path_pixel(f, p, x, y)) {
+    if (path_pixel_single(f, p, x, y)) {
         const float4 rd = w.RD[(uint64_t)y * f.width + x];
         const f3 P = mk(rd.x, rd.y, rd.z);
         const f3 delta = P - pc.pos;
@@ -2020,7 +2038,7 @@ __global__ __launch_bounds__(256) void k_reproject_resolve(FrameArgs f, WaveBufs
     const uint32_t p = blockIdx.x * 256u + threadIdx.x;
     if (p >= w.P) return;
     uint32_t x, y;
-    if (!path_pixel(f, p, x, y)) return;
+    if (!path_pixel_single(f, p, x, y)) return;
     const uint64_t px = (uint64_t)y * f.width + x;
     const f3 ns = ld4(ill, px);
     f3 fin = ns;

@@ -198,6 +198,22 @@ class ShardedAccumFrame:
         self.last = p
         self.frame = f + 1
 
+    def render_window(self, first, n_frames):
+        """Frames first .. first + n_frames - 1 of this rank's tiles in order: one library call
+        (vpx_render_tiles_accum_window, several frames per chain of launches) when the context
+        has it, else frame by frame.  Same accumulator and RGB8 as n_frames render() calls."""
+        if n_frames <= 0:
+            return
+        win = getattr(self.ctx, "render_tiles_accum_window", None)
+        if win is None:
+            for f in range(first, first + n_frames):
+                self.render(f)
+            return
+        p = self.desc.frame_params(frame_index=first)
+        win(p, n_frames, self.rank, self.n, self.accum.data_ptr(), self.rgb[self.buf].data_ptr())
+        self.last = self.desc.frame_params(frame_index=first + n_frames - 1)
+        self.frame = first + n_frames
+
     def publish(self):
         import torch
         import torch.distributed as dist

@@ -142,3 +142,86 @@ def test_static_camera_reprojection_instances(pkg, orc, depth):
         assert np.array_equal(rgb_g, rgb_o), f"frame {f}: rgb8"
         assert (st.shadow_rays, st.bounce_rays, st.dda_cells) == (ost.shadow_rays, ost.bounce_rays, ost.dda_cells)
     r.ctx.close()
+
+
+def _window_image(pkg, desc, first, n, lanes, pre=0):
+    """`pre` per-frame renders, then frames pre .. pre + n - 1 as one vpx_render_window."""
+    ctx = pkg.context.Context(0)
+    s = torch.cuda.Stream()
+    ctx.set_stream(s.cuda_stream)
+    ctx.load_scene(desc)
+    ctx.set_pipeline(lanes)
+    W, H = desc.width, desc.height
+    acc = torch.zeros(W * H * 4, dtype=torch.float32, device="cuda")
+    rgb = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    ctx.counters(reset=True)
+    with torch.cuda.stream(s):
+        for f in range(pre):
+            ctx.render(desc.frame_params(f), acc.data_ptr(), rgb.data_ptr())
+        ctx.render_window(desc.frame_params(first), n, acc.data_ptr(), rgb.data_ptr())
+    ctx.synchronize()
+    st = ctx.counters()
+    out = (bits(acc.cpu().numpy().reshape(-1, 4)), rgb.cpu().numpy().view(np.uint32),
+           tuple(int(getattr(st, k)) for k in ("primary_rays", "shadow_rays", "bounce_rays", "dda_cells")))
+    ctx.close()
+    return out
+
+
+@pytest.mark.parametrize("depth", [0, 2])
+def test_window_image_bit_exact(pkg, orc, depth):
+    """vpx_render_window over the instance lattice (64x48: 12 tiles, so the whole window is one
+    chain of launches, each frame in its own tile blocks with its own seeds): accumulator, RGB8
+    and ray / cell counts equal the oracle's frame-by-frame accumulation, with and without
+    lanes, from frame 0 and continuing a running average from frame 1."""
+    desc = lattice_scene(pkg, 1, depth, sphere=True)
+    frames = 4
+    a_o, r_o, c_o = oracle(orc, pkg, desc, frames)
+    for lanes in (0, 3):
+        for pre in (0, 1):
+            a_g, r_g, c_g = _window_image(pkg, desc, pre, frames - pre, lanes, pre)
+            assert np.array_equal(a_g, a_o), f"accumulator differs (lanes {lanes}, pre {pre})"
+            assert np.array_equal(r_g, r_o), f"RGB8 differs (lanes {lanes}, pre {pre})"
+            assert c_g == c_o, (lanes, pre, c_g, c_o)
+
+
+def _tiles_accum(pkg, desc, R, frames, lanes, window):
+    ctx = pkg.context.Context(0)
+    s = torch.cuda.Stream()
+    ctx.set_stream(s.cuda_stream)
+    ctx.load_scene(desc)
+    ctx.set_pipeline(lanes)
+    L = ctx.packed_len(desc.width, desc.height, R)
+    out = []
+    torch.cuda.synchronize()
+    with torch.cuda.stream(s):
+        for r in range(R):
+            acc = torch.zeros(L * 4, dtype=torch.float32, device="cuda")
+            rgb = torch.zeros(L, dtype=torch.int32, device="cuda")
+            if window:
+                ctx.render_tiles_accum_window(desc.frame_params(0), frames, r, R, acc.data_ptr(), rgb.data_ptr())
+            else:
+                for f in range(frames):
+                    ctx.render_tiles_accum(desc.frame_params(f), r, R, acc.data_ptr(), rgb.data_ptr())
+            out.append((acc, rgb))
+    ctx.synchronize()
+    res = [(bits(a.cpu().numpy().reshape(-1, 4)), g.cpu().numpy().view(np.uint32)) for a, g in out]
+    ctx.close()
+    return res
+
+
+@pytest.mark.parametrize("depth", [0, 2])
+def test_window_tiles_accum_matches_per_frame(pkg, depth):
+    """vpx_render_tiles_accum_window against frame-by-frame vpx_render_tiles_accum (itself
+    checked against the oracle in test_gpu_parity): 512x512 at 3 ranks (342 tiles a rank: the
+    40 frames in one chain) and at one rank (1024 tiles: chains of 32 frames, so the window
+    splits 32 + 8); lanes 0 and 3; every rank's packed accumulator and RGB8 bit-exact."""
+    desc = lattice_scene(pkg, 2, depth).with_size(512, 512)
+    desc.area_samples = 2
+    for R in (3, 1):
+        ref = _tiles_accum(pkg, desc, R, 40, 0, False)
+        for lanes in (0, 3):
+            got = _tiles_accum(pkg, desc, R, 40, lanes, True)
+            for r in range(R):
+                assert np.array_equal(got[r][0], ref[r][0]), f"R={R} rank {r} lanes {lanes}: accumulator"
+                assert np.array_equal(got[r][1], ref[r][1]), f"R={R} rank {r} lanes {lanes}: RGB8"
