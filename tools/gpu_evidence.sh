@@ -26,6 +26,7 @@ if [ "${PART:-1}" = 1 ]; then
   step share_C3p4 300 env CFG=C3 PIPE=4 python tools/rank_share.py
   step share_C4p4 600 env CFG=C4 PIPE=4 K=5 python tools/rank_share.py
   step share_C4p3 600 env CFG=C4 PIPE=3 K=5 python tools/rank_share.py
+  step share_C4p4w0 600 env CFG=C4 PIPE=4 K=5 WINDOW=0 python tools/rank_share.py
 else
   declare -A WH=([C1]="1920 1080" [C2]="1920 1080" [C3]="3840 2160" [C4]="3840 2160" [Z1]="1920 1080")
   for c in ${PMC_CFGS:-C1 C2 C3 C4 Z1}; do
