@@ -120,6 +120,12 @@ class _OracleTileCtx:
         acc[ok] = a
         rgb[ok] = r
 
+    def render_tiles_accum_window(self, p, n_frames, rank, n, acc_ptr, rgb_ptr):
+        """vpx_render_tiles_accum_window's contract: frames p.frame_index .. + n_frames - 1 in order."""
+        self.window_calls = getattr(self, "window_calls", 0) + 1
+        for f in range(p.frame_index, p.frame_index + n_frames):
+            self.render_tiles_accum(self.desc.frame_params(f), rank, n, acc_ptr, rgb_ptr)
+
     def composite_rgb8(self, p, n, gathered_ptr, screen_ptr):
         w, h = self.desc.width, self.desc.height
         L = self.pkg.dist.packed_len(w, h, n)
@@ -130,7 +136,8 @@ class _OracleTileCtx:
 
 def _worker_window(rank, world, port, w, h, spp, q):
     """dist.ShardedAccumFrame itself (host gather over gloo): two accumulation windows of
-    `spp` frames each, one publish per window (bench.py's C4 step); rank 0's screen after
+    `spp` frames each, one publish per window (bench.py's C4 step) — the first frame by frame,
+    the second as one render_window call (vpx_render_tiles_accum_window); rank 0's screen after
     each flush equals the oracle's whole-frame RGB8 after frame spp - 1."""
     sys.path.insert(0, REPO)
     import __graft_entry__ as entry
@@ -141,15 +148,19 @@ def _worker_window(rank, world, port, w, h, spp, q):
         pkg, orc = entry.load_package(), entry.load_oracle()
         desc = pkg.scene.model_scene("monu3", 64, w, h, 1, city_lights=True)
         desc.flags = pkg.abi.VPX_FLAG_AA
-        fr = pkg.dist.ShardedAccumFrame(_OracleTileCtx(pkg, orc, desc), desc, rank, world, torch.device("cpu"),
-                                        host_gather=True)
+        tctx = _OracleTileCtx(pkg, orc, desc)
+        fr = pkg.dist.ShardedAccumFrame(tctx, desc, rank, world, torch.device("cpu"), host_gather=True)
         ok = True
         acc = None
         for f in range(spp):
             acc, want, _ = orc.Oracle(pkg.abi, desc).render(desc.frame_params(f), accum=acc, threads=2)
-        for _ in range(2):
-            for f in range(spp):
-                fr.render(f)
+        for win in range(2):
+            if win == 0:
+                for f in range(spp):
+                    fr.render(f)
+            else:
+                fr.render_window(0, spp)
+                ok &= getattr(tctx, "window_calls", 0) == 1 and fr.last.frame_index == spp - 1 and fr.frame == spp
             fr.publish()
             fr.flush()
             if rank == 0:
