@@ -92,13 +92,6 @@ __global__ __launch_bounds__(kThreads) void blend_packed(FrameArgs f, const floa
     }
 }
 
-// Frame weights of one window chain (renderer.cpp:1651's 1/(n+1), computed on the host as
-// frame_of does, so every blend uses the per-frame path's exact weights).
-constexpr uint32_t kMaxWindow = 64;
-struct WindowWeights {
-    float w[kMaxWindow], iw[kMaxWindow];
-};
-
 // An accumulation window's samples (frame b of the chain at [b*T*256, (b+1)*T*256)) folded
 // into the accumulator in frame order: per pixel the same blend of the same samples as B
 // calls of k_finish / composite_tiles / blend_packed, and the tonemap of the last.  image:
@@ -875,11 +868,13 @@ struct Reproj {  // the static-camera tail (vpx_render_reproject)
 };
 
 // tail_wait: an event the frame's separate tail launch (k_resolve_finish, after the shadow
-// pool) waits for — frames in flight that blend on their own lane (lane_tail_ok).
+// pool) waits for — frames in flight that blend on their own lane (lane_tail_ok).  wtail: a
+// window chain (tiles = B frames' tiles) whose separate tail blends its frames in order
+// (k_finish_window) instead of writing samples.
 template <int MODE>
 int launch_render(vpx_ctx* c, hipStream_t s, vpx_ctx::WaveStore& ws, const SceneView& sv, const FrameArgs& f,
                   uint32_t tiles, float4* accum, uint32_t* rgb8, float4* packed, const Reproj* rp = nullptr,
-                  const hipEvent_t* tail_wait = nullptr) {
+                  const hipEvent_t* tail_wait = nullptr, const WindowTail* wtail = nullptr) {
     const uint32_t P = tiles * (uint32_t)kTilePix;
     const uint32_t L = (uint32_t)std::max(1, f.max_bounces + 1);
     // shadow slots per path: an area-light sample each, else one (point / spot / directional
@@ -924,6 +919,8 @@ int launch_render(vpx_ctx* c, hipStream_t s, vpx_ctx::WaveStore& ws, const Scene
 #define VPX_SPOOL_ONE_SERIAL 0
 #endif
     const bool spool = !rp && (S > 1 || (one && VPX_SPOOL_ONE_SLOT && (VPX_SPOOL_ONE_SERIAL || &ws != &c->wave)));
+    if (wtail && (!spool || f.max_bounces < 0 || !f.batch_tiles || tiles % wtail->B))
+        return fail(c, VPX_E_INVALID, "window tail: needs a window chain with the shadow pool");
     if (!spool) w.occb = nullptr;  // k_resolve reads the slots' SD flags
     const uint32_t sgrab = std::max(1u, std::min(4u, kShadowList / (64u * S)));
     // persistent launches over a level's live list (its length is on the device): as many
@@ -1043,7 +1040,11 @@ int launch_render(vpx_ctx* c, hipStream_t s, vpx_ctx::WaveStore& ws, const Scene
             if (spool) {
                 if (tail_wait) VPX_HIP(c, hipStreamWaitEvent(s, *tail_wait, 0));
                 prof_mark(c, s, VPX_STAGE_FINISH);
-                hipLaunchKernelGGL((k_resolve_finish<MODE>), grid, block, 0, s, sv, f, w, accum, rgb8, packed);
+                if (wtail)
+                    hipLaunchKernelGGL(k_finish_window<true>, dim3(tiles / wtail->B), block, 0, s, sv, f, w, *wtail,
+                                       accum, rgb8);
+                else
+                    hipLaunchKernelGGL((k_resolve_finish<MODE>), grid, block, 0, s, sv, f, w, accum, rgb8, packed);
                 prof_mark(c, s, -1);
             }
             break;
@@ -1096,7 +1097,11 @@ int launch_render(vpx_ctx* c, hipStream_t s, vpx_ctx::WaveStore& ws, const Scene
     if (!finished && tail_wait) VPX_HIP(c, hipStreamWaitEvent(s, *tail_wait, 0));
     if (!finished) prof_mark(c, s, VPX_STAGE_FINISH);
     if (!rp) {
-        if (!finished) hipLaunchKernelGGL((k_finish<MODE>), grid, block, 0, s, f, w, accum, rgb8, packed);
+        if (!finished && wtail)
+            hipLaunchKernelGGL(k_finish_window<false>, dim3(tiles / wtail->B), block, 0, s, sv, f, w, *wtail, accum,
+                               rgb8);
+        else if (!finished)
+            hipLaunchKernelGGL((k_finish<MODE>), grid, block, 0, s, f, w, accum, rgb8, packed);
     } else {  // Renderer::Tick static branch, second pass (renderer.cpp:2024-2100)
         hipLaunchKernelGGL(k_finish_reproject, grid, block, 0, s, f, w, rp->alb, rp->ill);
         hipLaunchKernelGGL(k_reproject_setup, grid, block, 0, s, f, w, rp->prev);
@@ -2035,6 +2040,14 @@ static int render_tiles_impl(int MODE, vpx_ctx* c, const vpx_frame_params* p, ui
 #ifndef VPX_WINDOW_TILES
 #define VPX_WINDOW_TILES 131072
 #endif
+// Window chains of big frames (at least this many tiles a frame) whose tail is a launch of
+// its own blend in that tail (k_finish_window), once the previous chain's tail has run: C4 one
+// GPU 26.60-26.66 vs 26.95 ms per step.  Small shares keep the blend on the caller's stream
+// (blend_window): the tail's wait for the previous chain held each lane (C4 rank 0 of 8: 4.12
+// vs 3.68 ms), profiles/r06_window_ab.txt.  0 = never.
+#ifndef VPX_WINDOW_FUSED
+#define VPX_WINDOW_FUSED 16384
+#endif
 #ifndef VPX_WINDOW_LANE_CAP
 #define VPX_WINDOW_LANE_CAP 1
 #endif
@@ -2078,6 +2091,28 @@ static int render_window_impl(vpx_ctx* c, const vpx_frame_params* p, uint32_t n,
         }
         float4* samples = nullptr;
         vpx_ctx::Lane* L = nullptr;
+        if (!c->lanes.empty() && VPX_WINDOW_FUSED && T >= VPX_WINDOW_FUSED && lane_tail_ok(sv, f)) {
+            // the chain's own tail blends its frames into the accumulator (k_finish_window) on
+            // its lane, once the caller's stream has reached this call — which orders it after
+            // the previous chain's tail, as vpx_render's lane_tail_ok frames
+            vpx_ctx::Lane& FL = c->lanes[c->lane_next];
+            c->lane_next = (c->lane_next + 1u) % (uint32_t)c->lanes.size();
+            if (FL.used) VPX_HIP(c, hipStreamWaitEvent(FL.s, FL.consumed, 0));
+            VPX_HIP(c, hipEventRecord(FL.caller, c->stream));
+            WindowTail wt;
+            wt.B = B;
+            wt.image = image ? 1 : 0;
+            wt.ww = ww;
+            if ((rc = launch_render<kFinishPackedSample>(c, FL.s, FL.ws, sv, f, B * T, reinterpret_cast<float4*>(accum),
+                                                         rgb8, nullptr, nullptr, &FL.caller, &wt)))
+                return rc;
+            VPX_HIP(c, hipEventRecord(FL.rendered, FL.s));
+            VPX_HIP(c, hipStreamWaitEvent(c->stream, FL.rendered, 0));
+            VPX_HIP(c, hipEventRecord(FL.consumed, FL.s));
+            FL.used = true;
+            i += B;
+            continue;
+        }
         if (!c->lanes.empty()) {
             if ((rc = lane_render(c, sv, f, B * T, nullptr, L))) return rc;
             samples = L->cur;

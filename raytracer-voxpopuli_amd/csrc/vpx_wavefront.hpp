@@ -1682,7 +1682,37 @@ __device__ __forceinline__ float4 blend(float4 acc, f3 px, float w, float iw) {
 // accumulator sharded with the tiles; only the RGB8 travels).
 enum FinishMode : int { kFinishImage = 0, kFinishPackedSample = 1, kFinishPackedAccum = 2 };
 
-// Fold the level records bottom-up (the recursion's rounding order), then write per MODE.
+// A path's value: the level records folded bottom-up (the recursion's rounding order); ls: the
+// last level's light sum when the launch resolved it (fused tails).
+__device__ __forceinline__ f3 path_value(const WaveBufs& w, uint32_t p, const LightSum* ls) {
+    f3 v = mk(0.f, 0.f, 0.f);
+    const uint32_t forms = w.forms[p];
+    if (forms & kLeafBit) {
+        const float4 lf = w.leaf[p];
+        v = mk(lf.x, lf.y, lf.z);
+    }
+    for (int i = (int)forms_count(forms) - 1; i >= 0; --i) {
+        const uint32_t form = (forms >> (2 * i)) & 3u;
+        const uint64_t li = (uint64_t)i * w.P + p;
+        const float4 a4 = w.LA[li];
+        const f3 a = mk(a4.x, a4.y, a4.z);
+        if (form == kFormMulAdd || form == kFormAddMul) {
+            f3 b;
+            if (ls && ls->lvl == (uint32_t)i) {
+                b = ls->inc;  // this launch's resolve (fused tail)
+            } else {
+                const float4 b4 = w.LB[li];
+                b = mk(b4.x, b4.y, b4.z);
+            }
+            v = form == kFormMulAdd ? b + v * a : (v + b) * a;
+        } else if (form == kFormMul) {
+            v = v * a;
+        }
+    }
+    return v;
+}
+
+// Fold the level records (path_value), then write per MODE.
 template <int MODE>
 __device__ __forceinline__ void finish_path(const FrameArgs& f, const WaveBufs& w, uint32_t p, float4* __restrict__ accum,
                                             uint32_t* __restrict__ rgb8, float4* __restrict__ packed,
@@ -1691,32 +1721,7 @@ __device__ __forceinline__ void finish_path(const FrameArgs& f, const WaveBufs& 
     uint32_t x, y;
     // window chains finish into packed samples only
     const bool valid = MODE == kFinishPackedSample ? path_pixel(f, p, x, y) : path_pixel_single(f, p, x, y);
-    f3 v = mk(0.f, 0.f, 0.f);
-    if (valid) {
-        const uint32_t forms = w.forms[p];
-        if (forms & kLeafBit) {
-            const float4 lf = w.leaf[p];
-            v = mk(lf.x, lf.y, lf.z);
-        }
-        for (int i = (int)forms_count(forms) - 1; i >= 0; --i) {
-            const uint32_t form = (forms >> (2 * i)) & 3u;
-            const uint64_t li = (uint64_t)i * w.P + p;
-            const float4 a4 = w.LA[li];
-            const f3 a = mk(a4.x, a4.y, a4.z);
-            if (form == kFormMulAdd || form == kFormAddMul) {
-                f3 b;
-                if (ls && ls->lvl == (uint32_t)i) {
-                    b = ls->inc;  // this launch's resolve (fused tail)
-                } else {
-                    const float4 b4 = w.LB[li];
-                    b = mk(b4.x, b4.y, b4.z);
-                }
-                v = form == kFormMulAdd ? b + v * a : (v + b) * a;
-            } else if (form == kFormMul) {
-                v = v * a;
-            }
-        }
-    }
+    const f3 v = valid ? path_value(w, p, ls) : mk(0.f, 0.f, 0.f);
     if (MODE == kFinishPackedSample) {
         packed[p] = make_float4(v.x, v.y, v.z, 0.0f);
     } else if (MODE == kFinishPackedAccum) {  // accum / rgb8 are this rank's packed buffers
@@ -1755,6 +1760,53 @@ __global__ __launch_bounds__(256) void k_resolve_finish(SceneView sv, FrameArgs 
     LightSum ls;
     resolve_path(sv, w, p, nullptr, &ls);
     finish_path<MODE>(f, w, p, accum, rgb8, packed, &ls);
+}
+
+// An accumulation window's frame weights (renderer.cpp:1651's 1/(n+1), computed on the host as
+// frame_of does, so every blend uses the per-frame path's exact weights).
+constexpr uint32_t kMaxWindow = 64;
+struct WindowWeights {
+    float w[kMaxWindow], iw[kMaxWindow];
+};
+struct WindowTail {
+    uint32_t B;  // frames in the chain (frame b: tile blocks [b*batch_tiles, (b+1)*batch_tiles))
+    int image;   // accum / rgb8 indexed by pixel (one GPU), else a rank's packed buffers
+    WindowWeights ww;
+};
+
+// A window chain's tail on its lane (vpx_render_window, frames whose tail is a launch of its
+// own): one thread per pixel of the chain resolves (RESOLVE: k_resolve_finish's last-level light
+// sum) and folds each of its B frames' paths and blends them into the accumulator in frame
+// order — the B per-frame blends of the same values, with no samples written or re-read.
+template <bool RESOLVE>
+__global__ __launch_bounds__(256) void k_finish_window(SceneView sv, FrameArgs f, WaveBufs w, WindowTail wt,
+                                                       float4* __restrict__ accum, uint32_t* __restrict__ rgb8) {
+    const uint32_t p0 = blockIdx.x * 256u + threadIdx.x;
+    uint32_t x, y;
+    const bool valid = path_pixel(f, p0, x, y);
+    if (wt.image && !valid) return;
+    const uint64_t at = wt.image ? (uint64_t)y * f.width + x : p0;
+    if (!valid) {
+        accum[at] = make_float4(0.f, 0.f, 0.f, 0.f);
+        rgb8[at] = 0u;
+        return;
+    }
+    float4 a = accum[at];
+    const uint32_t stride = f.batch_tiles * 256u;
+    for (uint32_t b = 0; b < wt.B; ++b) {
+        const uint32_t p = p0 + b * stride;
+        f3 v;
+        if (RESOLVE) {
+            LightSum ls;
+            resolve_path(sv, w, p, nullptr, &ls);
+            v = path_value(w, p, &ls);
+        } else {
+            v = path_value(w, p, nullptr);
+        }
+        a = blend(a, v, wt.ww.w[b], wt.ww.iw[b]);
+    }
+    accum[at] = a;
+    if (rgb8) rgb8[at] = tonemap_pack(a);
 }
 
 // The deep levels in one launch (k_tail): from level `level` on, each lane carries one path of

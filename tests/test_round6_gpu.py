@@ -225,3 +225,23 @@ def test_window_tiles_accum_matches_per_frame(pkg, depth):
             for r in range(R):
                 assert np.array_equal(got[r][0], ref[r][0]), f"R={R} rank {r} lanes {lanes}: accumulator"
                 assert np.array_equal(got[r][1], ref[r][1]), f"R={R} rank {r} lanes {lanes}: RGB8"
+
+
+@pytest.mark.parametrize("size", [(64, 40), (2048, 2048)])
+@pytest.mark.parametrize("pipe", [3, 4])
+def test_window_deep_area_lights_matches_per_frame(pkg, pipe, size):
+    """Window chains with area lights (several slots per path) at depth 14 (the frames run
+    k_tail) and depth 2 over the lattice.  At 2048x2048 (16384 tiles, VPX_WINDOW_FUSED) each
+    chain blends in its own tail after the caller's event (k_finish_window, with the resolve at
+    depth 2, without it after k_tail); small frames blend on the caller's stream.  Against
+    frame-by-frame vpx_render on the stream (itself checked against the oracle): 6 frames,
+    accumulator and RGB8 bit-exact."""
+    sc = pkg.scene
+    W, H = size
+    for desc in (sc.city_scene("roomGlass", 128, W, H, 14, areas=sc.C3_AREAS[:2]), lattice_scene(pkg, 1, 2).with_size(W, H)):
+        desc.area_samples = 3
+        desc.flags = pkg.abi.VPX_FLAG_AA
+        a_r, r_r, _ = render(pkg, desc, 6, 0)
+        a_w, r_w, _ = _window_image(pkg, desc, 0, 6, pipe)
+        assert np.array_equal(a_w, a_r), f"accumulator differs (depth {desc.max_bounces}, {pipe} lanes)"
+        assert np.array_equal(r_w, r_r), f"RGB8 differs (depth {desc.max_bounces}, {pipe} lanes)"
