@@ -222,7 +222,7 @@ __global__ __launch_bounds__(256) void bvh_intersect_k(const uint32_t* __restric
 }
 
 template <int LEVELS>
-__global__ void trace_k(SceneView sv, const vpx_ray* rays, const uint32_t* seeds, uint32_t n, int32_t depth,
+__global__ __launch_bounds__(256) void trace_k(SceneView sv, const vpx_ray* rays, const uint32_t* seeds, uint32_t n, int32_t depth,
                         float* out) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
